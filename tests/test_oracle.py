@@ -1,0 +1,259 @@
+"""CPU tests of the oracle (oracle/mimo_ref.c) against the committed golden fixtures, the
+independent numpy model, and reference-derived known answers."""
+import glob
+import os
+
+import numpy as np
+import pytest
+
+from oracle import codes, numpy_model as nm, ref
+
+GOLDEN = sorted(glob.glob(os.path.join(os.path.dirname(__file__), "golden", "m[0-9]*.npz")))
+
+
+def load(path):
+    return dict(np.load(path, allow_pickle=False))
+
+
+def run_oracle(g, chunks=None):
+    N = int(g["N"])
+    fs = ref.FrameSyncRef(int(g["M"]), int(g["cp"]), N, int(g["nac"]), pid_max=int(g["pid"]),
+                          detector=int(g["detector"]),
+                          keep_identity_bias=bool(g["keep_identity_bias"]), p=g["p"],
+                          siso_tx=int(g["siso_tx"]), siso_rx=int(g["siso_rx"]), trace_sc=True)
+    rx = g["rx"]
+    if chunks is None:
+        fs.execute(rx)
+    else:
+        pos = 0
+        for c in chunks:
+            fs.execute([r[pos:pos + c] for r in rx], min(c, rx.shape[1] - pos))
+            pos += c
+            if pos >= rx.shape[1]:
+                break
+    return fs
+
+
+def test_msequence_periods():
+    assert ref.msequence_period(12, codes.S0_POLY) == 4095
+    for g in codes.S1_POLYS:
+        assert ref.msequence_period(13, g) == 8191, oct(g)
+    # config.h:73 second small polynomial is primitive too
+    assert ref.msequence_period(12, 0o10151) == 4095
+
+
+def test_msequence_golden_bits(golden_dir):
+    bits = np.load(os.path.join(golden_dir, "msequence_bits.npz"))
+    for key in bits.files:
+        m, g = (12, int(key[3:], 8)) if key.startswith("s0_") else (13, int(key[3:], 8))
+        assert (ref.draw_bits(m, g, 1, 256) == bits[key]).all(), key
+        assert (nm.msequence_bits(m, g, 1, 256) == bits[key]).all(), key
+
+
+def test_sctype_variants():
+    p = ref.default_sctype(2048)
+    assert ref.validate_sctype(p) == (0, 0, 2048)
+    q = ref.liquid_sctype(1024)
+    n0, n1, n2 = ref.validate_sctype(q)
+    assert n1 + n2 == 818  # mimo/apps/plot.py:12 hard-codes 818 occupied carriers at M=1024
+    with pytest.raises(ValueError):
+        ref.validate_sctype(np.array([0, 1, 2, 7], np.uint8))
+
+
+def test_fft_matches_numpy():
+    rng = np.random.default_rng(0)
+    for n in (2, 8, 64, 128, 2048, 8192):
+        x = (rng.standard_normal(n) + 1j * rng.standard_normal(n)).astype(np.complex64)
+        X = ref.fft(x)
+        ref64 = np.fft.fft(x.astype(np.complex128))
+        assert np.abs(X - ref64).max() / np.abs(ref64).max() < 2e-6
+        xi = ref.fft(X, inverse=True) / n
+        assert np.abs(xi - x).max() < 1e-5
+
+
+def test_S0_S1_structure():
+    M = 128
+    p = ref.default_sctype(M)
+    b0 = ref.draw_bits(12, codes.S0_POLY, 1, M)
+    S0, s0 = ref.init_S0(p, b0)
+    assert np.all(S0[1::2] == 0) and np.all(np.abs(S0[0::2]) == 1)
+    # S0 only on even bins -> time-domain period M/2 (what the S&C plateau relies on)
+    assert np.abs(s0[:M // 2] - s0[M // 2:]).max() < 1e-6
+    b1 = ref.draw_bits(13, codes.S1_POLYS[0], 1, 3 * M)
+    S1, s1 = ref.init_S1(p, 3, b1)
+    assert np.all(np.abs(S1) == 1)
+    # |S1|=1 on every bin -> circular autocorrelation of s1 is a delta
+    ac = np.fft.ifft(np.abs(np.fft.fft(s1[0])) ** 2)
+    assert abs(ac[0]) > 1e3 * np.abs(ac[1:]).max()
+    # scale sqrt(1/M) (framing.cc:1228)
+    assert abs(np.sum(np.abs(s1[0]) ** 2) - M) / M < 1e-5
+
+
+def test_invert2_known_answer():
+    G = np.array([[1 + 2j, 0.5 - 1j], [0.25j, 2 - 0.5j]], np.complex64)
+    W, g = ref.invert2(G)
+    assert np.allclose(W * g, np.linalg.inv(G.astype(np.complex128)), rtol=1e-5, atol=1e-6)
+
+
+def test_qam_roundtrip():
+    for q in (4, 16, 64, 256):
+        pts = np.array([ref.qam_point(i, q) for i in range(q)])
+        assert abs(np.mean(np.abs(pts) ** 2) - 1.0) < 1e-5
+        for i in range(q):
+            assert ref.qam_demap(pts[i] * (1 + 0.01j), q) == i
+        # Gray: nearest horizontal neighbours differ in one bit
+        L = int(np.sqrt(q))
+        for i in range(q):
+            for j in range(q):
+                d = abs(pts[i] - pts[j])
+                if 0 < d < 1.01 * (2 * np.sqrt(3 / (2 * (L * L - 1)))):
+                    assert bin(i ^ j).count("1") == 1
+
+
+def test_sc_metric_exact_matches_trace(golden_dir):
+    g = load(os.path.join(golden_dir, "m64_2x2_zf2.npz"))
+    rx = g["rx"][0]
+    y = g["y0"]
+    for n in list(range(0, 200, 7)) + list(range(int(g["plateau_start"][0]) - 5,
+                                                int(g["plateau_end"][0]) + 1)):
+        assert ref.sc_metric_at(rx, n, int(g["M"])) == y[n] or (np.isnan(y[n]))
+
+
+@pytest.mark.parametrize("path", GOLDEN, ids=[os.path.basename(p) for p in GOLDEN])
+def test_oracle_matches_golden(path):
+    g = load(path)
+    fs = run_oracle(g)
+    N = int(g["N"])
+    assert fs.get_sync_index() == int(g["sync_index"])
+    assert fs.get_num_samples_processed() == int(g["num_samples_processed"])
+    assert [fs.get_plateau_start(s) for s in range(N)] == list(g["plateau_start"])
+    assert [fs.get_plateau_end(s) for s in range(N)] == list(g["plateau_end"])
+    ci, cm, si, sm = fs.get_corr()
+    assert (ci == g["corr_idx"]).all() and (si == g["s0_idx"]).all()
+    assert np.allclose(fs.get_G(), g["G"], rtol=1e-6, atol=1e-7)
+    syms = fs.symbols()
+    assert syms.shape == g["symbols"].shape
+    scale = np.abs(g["symbols"]).max()
+    assert np.abs(syms - g["symbols"]).max() / scale < 1e-6
+
+
+@pytest.mark.parametrize("path", [p for p in GOLDEN if "siso" not in p],
+                         ids=[os.path.basename(p) for p in GOLDEN if "siso" not in p])
+def test_numpy_model_matches_golden(path):
+    g = load(path)
+    M, cp, N, nac, pid = (int(g[k]) for k in ("M", "cp", "N", "nac", "pid"))
+    s0b, s1b = ref.code_bits(M, N, nac, codes.s1_polynomials(N))
+    det = {ref.DET_ZF2: "zf2", ref.DET_ZF: "zf", ref.DET_MMSE: "mmse"}[int(g["detector"])]
+    out = nm.receive(g["rx"], M, cp, N, nac, pid, s0b, s1b, p=g["p"], detector=det,
+                     keep_identity_bias=bool(g["keep_identity_bias"]))
+    assert out["sync_index"] == int(g["sync_index"])
+    assert (out["corr_idx"] == g["corr_idx"]).all()
+    scale = np.abs(g["symbols"]).max()
+    assert np.abs(out["symbols"] - g["symbols"]).max() / scale < 1e-5
+
+
+KA = [p for p in GOLDEN if os.path.basename(p).split(".")[0] in
+      ("m64_2x2_zf2", "m64_1x1_zf", "m128_4x4_mmse", "m64_2x2_siso")]
+
+
+@pytest.mark.parametrize("path", KA, ids=[os.path.basename(p) for p in KA])
+def test_reference_known_answers(path):
+    """Facts that follow from framing.cc / main.cc, independent of any implementation."""
+    g = load(path)
+    M, cp, N, nac, pid = (int(g[k]) for k in ("M", "cp", "N", "nac", "pid"))
+    SL = M + cp
+    base = int(g["sync_index"]) - SL                # window start, framing.cc:639-651
+    ci = g["corr_idx"].astype(np.int64)
+    # corr_indices land on symbol-body starts, one SL apart per TDMA slot
+    d = np.diff(ci, axis=1)
+    assert (d == SL).all()
+    assert (ci == ci[0]).all()                     # all rx agree
+    # the frame's S0 starts SL*(N*nac+1)+u in; slot ac body = S0 start + SL*(ac+1) + cp
+    assert (ci[0] - SL * (np.arange(N * nac) + 1)) .std() == 0
+    # replay start corr[N-1][last]+M is a data-symbol CP start: PID+2 callbacks
+    i0 = int(ci[N - 1, -1]) + M
+    win_len = SL * (nac * N + 4) + pid * SL
+    assert (win_len - i0) // SL == pid + 2
+    assert g["symbols"].shape[0] == pid + 2
+    # window/sync relation: estimate_channel ran at sample base+win_len -> nsp = that + 2
+    assert int(g["num_samples_processed"]) == base + win_len + 2
+    # plateau rule: run length at trigger > cp for the last antenna to qualify
+    assert (g["plateau_end"] - g["plateau_start"] > cp).all()
+    assert int(g["sync_index"]) == int(np.sum(g["plateau_start"])) // N
+    # identity bias on the diagonal of G (framing.cc:309-311, 811, 821)
+    if bool(g["keep_identity_bias"]) and int(g["detector"]) == ref.DET_ZF2:
+        W, G, gain = g["W"], g["G"], g["gain"]
+        for sc in range(0, M, 7):   # W*gain = G^-1 (framing.cc:1352-1365)
+            inv = np.linalg.inv(G[sc].astype(np.complex128))
+            assert np.allclose(W[sc] * gain[sc], inv, rtol=1e-4, atol=1e-5)
+
+
+def test_identity_bias_magnitude():
+    """G = 0.25*H + I/(sqrt(M_occ)*NAC) on a noiseless flat channel (BASEBAND_GAIN 0.25).
+    (An identity channel never syncs: S0 goes out on tx0 only, framing.cc:183-190, and
+    every rx antenna must see the plateau, framing.cc:613-615.)"""
+    M, cp, N, nac, pid = 64, 16, 2, 4, 4
+    rx, _, H = ref.synth_frame(M, cp, N, nac, pid, 16, seed=9, offset=10, snr_db=200.0)
+    fs = ref.FrameSyncRef(M, cp, N, nac, pid_max=pid)
+    assert fs.execute(rx) == ref.STATE_MIMO
+    G = fs.get_G()
+    expect = 0.25 * H + np.eye(N) / (np.sqrt(M) * nac)
+    assert np.abs(G - expect[None]).max() < 1e-4
+    ident = ref.synth_frame(M, cp, N, nac, pid, 16, seed=9, offset=10, snr_db=200.0,
+                            identity_channel=True)[0]
+    fs2 = ref.FrameSyncRef(M, cp, N, nac, pid_max=pid)
+    assert fs2.execute(ident) == ref.STATE_SEEK_PLATEAU
+
+
+def test_chunked_execute_equals_one_shot(golden_dir):
+    g = load(os.path.join(golden_dir, "m64_2x2_zf2.npz"))
+    a = run_oracle(g)
+    b = run_oracle(g, chunks=[1, 2, 3, 500, 77, 1000, 5, 100000])
+    assert a.get_sync_index() == b.get_sync_index()
+    # the chunked run processes every sample the one-shot run processed
+    assert b.get_num_samples_processed() == a.get_num_samples_processed()
+    assert np.array_equal(a.symbols(), b.symbols())
+
+
+def test_incomplete_capture_stays_in_save_state(golden_dir):
+    g = load(os.path.join(golden_dir, "m64_2x2_zf2.npz"))
+    M, cp, N, nac, pid = (int(g[k]) for k in ("M", "cp", "N", "nac", "pid"))
+    SL = M + cp
+    n_e = int(g["sync_index"]) - SL + SL * (nac * N + 4) + pid * SL
+    fs = ref.FrameSyncRef(M, cp, N, nac, pid_max=pid)
+    st = fs.execute(g["rx"][:, :n_e])          # capture ends just before n_e
+    assert st == ref.STATE_SAVE_ACCESS_CODES and len(fs.symbols()) == 0
+    st = fs.execute(g["rx"][:, n_e:n_e + 1])   # exactly sample n_e -> estimate runs
+    assert st == ref.STATE_MIMO and fs.get_num_samples_processed() == n_e + 1
+    fs.execute(g["rx"][:, n_e + 1:])           # MIMO: one sample consumed then break
+    assert fs.get_num_samples_processed() == n_e + 2
+
+
+def test_no_sync_on_noise():
+    rng = np.random.default_rng(3)
+    x = (rng.standard_normal((2, 5000)) + 1j * rng.standard_normal((2, 5000))).astype(np.complex64)
+    fs = ref.FrameSyncRef(64, 16, 2, 4, pid_max=4)
+    assert fs.execute(x * 0.01) == ref.STATE_SEEK_PLATEAU
+    assert fs.get_num_samples_processed() == 5000
+
+
+def test_zero_input_nan_metric_never_triggers():
+    x = np.zeros((1, 3000), np.complex64)
+    fs = ref.FrameSyncRef(64, 16, 1, 4, pid_max=4, detector=ref.DET_ZF, trace_sc=True)
+    assert fs.execute(x) == ref.STATE_SEEK_PLATEAU
+    assert np.isnan(fs.sc_trace(0)).all()
+
+
+def test_faded_link_search_is_junk_in_reference_too(golden_dir):
+    """m256_8x8: deep-faded links lose the argmax to adjacent-slot cross-correlation --
+    the reference's per-(rx,ac) search has no combining (framing.cc:733-740)."""
+    g = load(os.path.join(golden_dir, "m256_8x8_mmse.npz"))
+    SL = int(g["M"]) + int(g["cp"])
+    d = np.diff(g["corr_idx"].astype(np.int64), axis=1)
+    bad = np.argwhere(d != SL)
+    assert len(bad) > 0
+    H2 = np.abs(g["H"]) ** 2
+    for r, k in bad:
+        ac = k + 1 if abs(d[r, k]) > SL else k
+        t = ac % int(g["N"])
+        assert H2[r, t] < 0.05
