@@ -1,0 +1,213 @@
+/*
+ * include/mimo_rx.h -- C-ABI of librub_mimo_amd.so, the MI355X (gfx950) OFDM-MIMO receive
+ * pipeline. Plain pointers and sizes only; no torch or C++ types cross this boundary.
+ *
+ * Each entry point replaces a piece of the reference C++ API in /root/reference/mimo/framing.h
+ * (cited per function). The C++ facade include/framing.h re-exposes the reference classes
+ * rx_beamforming::framesync / framegen on top of these calls, so mimo/main.cc-style callers
+ * compile unchanged.
+ *
+ * Conventions
+ *   - complex samples are interleaved fp32 (re, im) = std::complex<float> = gr_complex.
+ *   - antenna buffers are planar: one array per antenna (framing.cc:481-484 reads in_buff[s][i]).
+ *   - every function returns MIMO_OK (0) or a negative MIMO_ERR_*; nothing calls exit()
+ *     (the reference exits at framing.cc:497-499, 1020-1022).
+ *   - a handle owns one HIP stream (or the caller's) and is single-caller-thread.
+ *   - device pointers (d_*) are HIP device memory (e.g. torch tensor data_ptr()).
+ */
+#ifndef RUB_MIMO_AMD_MIMO_RX_H
+#define RUB_MIMO_AMD_MIMO_RX_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MIMO_OK 0
+#define MIMO_ERR_ARG (-1)
+#define MIMO_ERR_HIP (-2)
+#define MIMO_ERR_STATE (-3)
+#define MIMO_ERR_NOMEM (-4)
+#define MIMO_ERR_SCTYPE (-5)
+#define MIMO_ERR_UNSUPPORTED (-6)
+
+#define MIMO_MAX_STREAMS 8
+
+/* framesync_states_t, framing.h:34-39 */
+enum { MIMO_STATE_SEEK_PLATEAU = 0, MIMO_STATE_SAVE_ACCESS_CODES = 1, MIMO_STATE_WAIT = 2,
+       MIMO_STATE_MIMO = 3 };
+
+/* detectors: ZF2 = reference 2x2 adjugate*conj(det) + gain 1/|det|^2 (framing.cc:1344-1367);
+ * ZF / MMSE = NxN in fp64, stored fp32; SISO = X/G[rx][tx] on one stream (framing.cc:508-533) */
+enum { MIMO_DET_ZF2 = 0, MIMO_DET_ZF = 1, MIMO_DET_MMSE = 2, MIMO_DET_SISO = 3 };
+
+/* per-frame status of the batched path */
+enum { MIMO_FRAME_OK = 0, MIMO_FRAME_NO_SYNC = 1, MIMO_FRAME_INCOMPLETE = 2 };
+
+/* subcarrier types, liquid OFDMFRAME_SCTYPE_{NULL,PILOT,DATA} */
+enum { MIMO_SC_NULL = 0, MIMO_SC_PILOT = 1, MIMO_SC_DATA = 2 };
+
+/* Receiver configuration: the framesync constructor arguments (framing.h:189-196) plus the
+ * config.h constants the reference reads at compile time (PID_MAX, PLATEAU_THREASHOLD). */
+typedef struct mimo_rx_config {
+  uint32_t M;                 /* _M, number of subcarriers (power of two, 64..4096) */
+  uint32_t cp_len;            /* _cp_len */
+  uint32_t num_streams;       /* _num_streams (1..8) */
+  uint32_t num_access_codes;  /* _num_access_codes */
+  uint32_t pid_max;           /* PID_MAX (config.h:92): data symbols per frame window */
+  const uint8_t *p;           /* _p, M subcarrier types; copied */
+  const uint8_t *s0_bits;     /* M draws msequence_generate_symbol(ms_S0,1)&1 (framing.cc:1075) */
+  const uint8_t *s1_bits;     /* num_streams*num_access_codes*M draws, stream-major
+                                 (framing.cc:1240, one generator per stream) */
+  int32_t detector;           /* MIMO_DET_* (INVERT_CHANNEL, config.h:102) */
+  float noise_var;            /* MMSE sigma^2; < 0: estimate from the training residuals */
+  int32_t keep_identity_bias; /* 1 = reference: G starts at identity (framing.cc:309-311) */
+  uint32_t siso_tx, siso_rx;  /* set_siso_tx / set_siso_rx (framing.h:211-212) */
+  double plateau_threshold;   /* PLATEAU_THREASHOLD (config.h:87), 0.95 */
+  uint32_t qam_order;         /* square Gray QAM for the fused demap/EVM stage (4..256) */
+} mimo_rx_config;
+
+typedef struct mimo_rx mimo_rx;
+
+/* callback, framing.h:30-31: eq[t] points at M_occ equalised symbols of stream t, valid
+ * only during the call (framing.cc:587). */
+typedef void (*mimo_rx_symbol_cb)(const float *const *eq, uint32_t n_streams, uint32_t m_occ,
+                                  void *user);
+
+/* framesync::framesync (framing.cc:268-436). hip_stream: hipStream_t or NULL (own stream). */
+int mimo_rx_create(const mimo_rx_config *cfg, void *hip_stream, mimo_rx **out);
+/* framesync::~framesync (framing.cc:916-943) */
+int mimo_rx_destroy(mimo_rx *h);
+/* the mimo_callback argument of the constructor (framing.h:196) */
+int mimo_rx_set_callback(mimo_rx *h, mimo_rx_symbol_cb cb, void *user);
+/* framesync::execute (framing.cc:471-506): host planar complex64 input, any chunking;
+ * state persists across calls; *state_out receives the framesync_states_t. */
+int mimo_rx_execute(mimo_rx *h, const float *const *iq_planar, uint32_t n_ant, uint64_t n,
+                    int32_t *state_out);
+/* framesync::reset (framing.cc:461-464): back to STATE_SEEK_PLATEAU */
+int mimo_rx_reset(mimo_rx *h);
+int mimo_rx_set_siso(mimo_rx *h, uint32_t siso_tx, uint32_t siso_rx);
+int mimo_rx_get_state(const mimo_rx *h, int32_t *state);
+/* get_sync_index / get_num_samples_processed / get_plateau_start|end (framing.h:200-206) */
+int mimo_rx_get_sync_index(const mimo_rx *h, uint64_t *out);
+int mimo_rx_get_num_samples_processed(const mimo_rx *h, uint64_t *out);
+int mimo_rx_get_plateau(const mimo_rx *h, uint32_t stream, uint64_t *start, uint64_t *end);
+/* get_G (framing.h:201): [M][N][N] complex64 ([sc][rx][tx]); W likewise ([sc][out][rx]) */
+int mimo_rx_get_G(mimo_rx *h, float *G);
+int mimo_rx_get_W(mimo_rx *h, float *W);
+/* normalize_gain (framing.cc:404-409), M_occ floats */
+int mimo_rx_get_gain(mimo_rx *h, float *gain);
+int mimo_rx_get_noise_var(mimo_rx *h, float *out);
+/* corr_indices [N][N*nac] (window index, framing.cc:737) and s0_corr_index [N] (:720) */
+int mimo_rx_get_corr(mimo_rx *h, uint32_t *corr_idx, uint32_t *s0_idx);
+int mimo_rx_get_m_occ(const mimo_rx *h, uint32_t *m_occ);
+
+/* ---------------- batched device-resident frames (the hot path the bench times) ---------
+ * n_frames independent captures, each num_streams planar antenna arrays of frame_len
+ * complex64 at d_iq + (f*num_streams + s)*stride (complex units). Every frame runs the whole
+ * receive chain (S&C + plateau, access-code search, LS, weights, decode, demap, EVM) with
+ * no host synchronisation. */
+typedef struct mimo_batch {
+  const void *d_iq;
+  uint64_t stride;        /* complex samples between antenna arrays (>= frame_len) */
+  uint64_t frame_len;
+  uint32_t n_frames;
+  uint32_t max_out_syms;  /* symbols kept per frame (main.cc keeps PID_MAX, main.cc:106) */
+  void *d_out_sym;        /* [n_frames][N][max_out_syms][M_occ] complex64, or NULL */
+  void *d_out_idx;        /* same layout, uint8 demapped index, or NULL */
+  int32_t ref_mode;       /* 0: decision-directed EVM; 1: d_ref_idx; 2: synthetic hash */
+  const void *d_ref_idx;  /* ref_mode 1: same layout as d_out_idx */
+  uint64_t ref_seed;      /* ref_mode 2: seed of mimo_synth_frames */
+  uint64_t frame_id0;     /* ref_mode 2: frame id of frame 0 */
+} mimo_batch;
+
+typedef struct mimo_frame_result {
+  int32_t status;                          /* MIMO_FRAME_* */
+  uint32_t n_sym;                          /* decode callbacks (PID+2 in the reference) */
+  uint64_t trigger;                        /* sample where the plateau rule fired */
+  uint64_t sync_index;
+  uint64_t num_samples_processed;          /* as one framesync::execute over the frame */
+  uint64_t plateau_start[MIMO_MAX_STREAMS];
+  uint64_t plateau_end[MIMO_MAX_STREAMS];
+  float noise_var;
+  float pad_;
+  double evm_num[MIMO_MAX_STREAMS];        /* sum |y - s|^2 over kept symbols */
+  double evm_den[MIMO_MAX_STREAMS];        /* sum |s|^2 */
+  uint64_t errors[MIMO_MAX_STREAMS];       /* symbol errors (ref_mode 1/2) */
+} mimo_frame_result;
+
+int mimo_rx_process_batch(mimo_rx *h, const mimo_batch *b, void *hip_stream);
+/* copies the last batch's per-frame results to host (synchronises the stream) */
+int mimo_rx_batch_results(mimo_rx *h, mimo_frame_result *out, uint32_t n_frames);
+/* per-frame detail of the last batch, host copies: corr [F][N][N*nac], G [F][M][N][N] */
+int mimo_rx_batch_corr(mimo_rx *h, uint32_t *corr_idx, uint32_t *s0_idx, uint32_t n_frames);
+int mimo_rx_batch_G(mimo_rx *h, float *G, uint32_t n_frames);
+int mimo_rx_batch_W(mimo_rx *h, float *W, uint32_t n_frames);
+
+/* stage timing with HIP events on the handle's launch stream (for the roofline line).
+ * stages: 0 S&C, 1 plateau, 2 search, 3 LS, 4 weights, 5 decode, 6 EVM reduce */
+#define MIMO_NUM_STAGES 7
+int mimo_rx_set_timing(mimo_rx *h, int enable);
+/* sums of stage durations (ms) and launch counts since the last call; synchronises */
+int mimo_rx_get_stage_times(mimo_rx *h, double *ms, uint32_t *launches);
+
+/* ---------------- transmitter: framegen (framing.h:42-103) ---------------- */
+typedef struct mimo_tx mimo_tx;
+int mimo_tx_create(uint32_t M, uint32_t cp_len, uint32_t num_streams,
+                   uint32_t num_access_codes, const uint8_t *p, const uint8_t *s0_bits,
+                   const uint8_t *s1_bits, mimo_tx **out);
+int mimo_tx_destroy(mimo_tx *h);
+/* framegen::write_sync_words (framing.cc:169-208): host buffers, (nac*N+1)*SL each */
+int mimo_tx_write_sync_words(mimo_tx *h, float *const *tx, uint32_t *n_written);
+/* framegen::assemble_mimo_packet (framing.cc:210-235): in[t] M_occ symbols -> SL samples */
+int mimo_tx_assemble_mimo_packet(mimo_tx *h, float *const *tx, const float *const *in,
+                                 uint32_t *n_written);
+int mimo_tx_get_codes(mimo_tx *h, float *s0 /* M */, float *s1 /* N*nac*M */);
+
+/* ---------------- synthetic captures on the GPU (tx_worker layout + channel + AWGN) -----
+ * [lead zeros SL*(N*nac+1)+u][sync words][pid data symbols][tail zeros], x0.25 baseband
+ * gain (main.cc:1048-1053), flat Rayleigh H ~ CN(0,1) per frame, AWGN. */
+typedef struct mimo_synth_config {
+  uint32_t M, cp_len, num_streams, num_access_codes, pid, qam_order;
+  uint64_t seed;
+  float snr_db;
+  uint32_t tail_syms;
+  int32_t identity_channel;
+  int32_t offset;         /* lead offset u; < 0: drawn per frame from the seed in [0, SL) */
+  const uint8_t *p, *s0_bits, *s1_bits;
+} mimo_synth_config;
+/* length of frame `frame_id` (depends on its offset u) */
+int mimo_synth_frame_len(const mimo_synth_config *c, uint64_t frame_id, uint64_t *len);
+/* writes n_frames captures into d_out (layout of mimo_batch; samples past a frame's own
+ * length are zero-padded noise), optional d_tx_idx [F][N][pid][M_occ] and d_H [F][N][N] */
+int mimo_synth_frames(const mimo_synth_config *c, uint64_t frame_id0, uint32_t n_frames,
+                      void *d_out, uint64_t stride, uint64_t frame_len, void *d_tx_idx,
+                      void *d_H, void *hip_stream);
+
+/* ---------------- helpers (setup-time, host) ---------------- */
+int mimo_sctype_default(uint8_t *p, uint32_t M);   /* ofdmframe_init_default_sctype */
+int mimo_sctype_liquid(uint8_t *p, uint32_t M);    /* compiled-out guard/pilot variant */
+int mimo_sctype_validate(const uint8_t *p, uint32_t M, uint32_t *M_null, uint32_t *M_pilot,
+                         uint32_t *M_data);        /* ofdmframe_validate_sctype */
+int mimo_msequence_draw_bits(uint32_t m, uint32_t g, uint32_t a, uint32_t count,
+                             uint8_t *out);        /* liquid msequence draws */
+/* 2x2 invert (framing.cc:1344-1367) on host arrays: returns gain */
+float mimo_invert2(float *W /* 4 complex */, const float *G /* 4 complex */);
+
+/* device memory / stream helpers so callers need no HIP headers */
+int mimo_dev_alloc(void **ptr, size_t bytes);
+int mimo_dev_free(void *ptr);
+int mimo_memcpy_h2d(void *dst, const void *src, size_t bytes, void *hip_stream);
+int mimo_memcpy_d2h(void *dst, const void *src, size_t bytes, void *hip_stream);
+int mimo_memset_d(void *dst, int value, size_t bytes, void *hip_stream);
+int mimo_stream_sync(void *hip_stream);
+int mimo_device_count(int *n);
+const char *mimo_last_error(void);
+const char *mimo_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

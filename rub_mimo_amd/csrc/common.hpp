@@ -1,0 +1,107 @@
+// rub_mimo_amd/csrc/common.hpp -- shared device helpers for the gfx950 receive pipeline.
+//
+// Complex values are float2 (x = re, y = im), the interleaved std::complex<float> layout of
+// gr_complex. Arithmetic helpers spell out every product and sum: the translation units that
+// must agree bit-for-bit with the CPU oracle compile with -ffp-contract=off.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define MIMO_DEV __device__ __forceinline__
+
+namespace mimo {
+
+constexpr int kMaxStreams = 8;
+constexpr int kTwLog2 = 14;             // twiddle table covers transforms up to 16384 points
+constexpr int kTwN = 1 << kTwLog2;
+
+MIMO_DEV float2 cadd(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
+MIMO_DEV float2 csub(float2 a, float2 b) { return make_float2(a.x - b.x, a.y - b.y); }
+MIMO_DEV float2 cmul(float2 a, float2 b) {
+  return make_float2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
+}
+MIMO_DEV float2 cmulc(float2 a, float2 b) {  // a * conj(b)
+  return make_float2(a.x * b.x + a.y * b.y, a.y * b.x - a.x * b.y);
+}
+MIMO_DEV float2 cconj(float2 a) { return make_float2(a.x, -a.y); }
+MIMO_DEV float2 cneg(float2 a) { return make_float2(-a.x, -a.y); }
+MIMO_DEV float2 cscale(float2 a, float s) { return make_float2(a.x * s, a.y * s); }
+MIMO_DEV float cabs2(float2 a) { return a.x * a.x + a.y * a.y; }
+MIMO_DEV float2 cdiv(float2 a, float2 b) {  // (a conj b)/|b|^2, exact for b = +-1
+  float d = b.x * b.x + b.y * b.y;
+  return make_float2((a.x * b.x + a.y * b.y) / d, (a.y * b.x - a.x * b.y) / d);
+}
+
+// ---------------- counter-based PRNG, bit-identical to oracle ref_hash5 ----------------
+MIMO_DEV uint64_t mix64(uint64_t z) {
+  z += 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+MIMO_DEV uint64_t hash5(uint64_t seed, uint64_t dom, uint64_t a, uint64_t b, uint64_t c) {
+  uint64_t h = mix64(seed ^ (dom * 0xD6E8FEB86659FD93ull));
+  h = mix64(h ^ a);
+  h = mix64(h ^ b);
+  h = mix64(h ^ c);
+  return h;
+}
+enum { DOM_DATA = 1, DOM_CHAN = 2, DOM_NOISE = 3, DOM_OFFSET = 4 };
+
+MIMO_DEV float2 hash_cnormal(uint64_t h) {  // CN(0,1), Box-Muller
+  float u1 = (float)((h >> 40) + 1ull) * 5.9604644775390625e-08f;
+  float u2 = (float)((h >> 16) & 0xFFFFFFull) * 5.9604644775390625e-08f;
+  float r = sqrtf(-2.0f * logf(u1));
+  float th = 6.283185307179586f * u2;
+  float s, c;
+  sincosf(th, &s, &c);
+  return make_float2(r * c * 0.70710678118654752f, r * s * 0.70710678118654752f);
+}
+
+// ---------------- square Gray QAM (same definition as oracle ref_qam_*) ----------------
+struct Qam {
+  uint32_t b;      // bits per dimension
+  uint32_t L;      // levels per dimension
+  float scale;     // 1/sqrt(2(L^2-1)/3)
+  float inv_scale; // sqrt(2(L^2-1)/3)
+};
+
+MIMO_DEV uint32_t gray_enc(uint32_t m) { return m ^ (m >> 1); }
+MIMO_DEV uint32_t gray_dec(uint32_t g) {
+  uint32_t m = g;
+  m ^= m >> 1; m ^= m >> 2; m ^= m >> 4; m ^= m >> 8;
+  return m;
+}
+MIMO_DEV float2 qam_point(uint32_t idx, const Qam &q) {
+  uint32_t mI = gray_dec(idx >> q.b), mQ = gray_dec(idx & (q.L - 1));
+  return make_float2((float)(int32_t)(2 * mI - (q.L - 1)) * q.scale,
+                     (float)(int32_t)(2 * mQ - (q.L - 1)) * q.scale);
+}
+MIMO_DEV uint32_t qam_level(float v, uint32_t L) {
+  float t = (v + (float)L) * 0.5f;
+  if (t != t) return 0;
+  float f = floorf(t);
+  int32_t m = (f < 0.0f) ? 0 : ((f > (float)(L - 1)) ? (int32_t)(L - 1) : (int32_t)f);
+  return (uint32_t)m;
+}
+MIMO_DEV uint32_t qam_demap(float2 y, const Qam &q) {
+  uint32_t mI = qam_level(y.x * q.inv_scale, q.L), mQ = qam_level(y.y * q.inv_scale, q.L);
+  return (gray_enc(mI) << q.b) | gray_enc(mQ);
+}
+
+// ---------------- per-frame bookkeeping shared by the stages ----------------
+struct FrameInfo {
+  int32_t status;          // MIMO_FRAME_*
+  uint32_t n_sym;          // decode callbacks available in the window
+  uint64_t trigger;
+  uint64_t sync_index;
+  uint64_t nsp;            // num_samples_processed after one execute over the frame
+  int64_t base;            // window start = sync_index - SL (absolute sample index)
+  uint64_t plateau_start[kMaxStreams];
+  uint64_t plateau_end[kMaxStreams];
+  float noise_var;
+  uint32_t i0;             // replay start, window index corr[N-1][last] + M
+};
+
+}  // namespace mimo

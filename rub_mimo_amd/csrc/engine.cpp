@@ -1,0 +1,1135 @@
+// rub_mimo_amd/csrc/engine.cpp -- host side of librub_mimo_amd.so: the C-ABI of
+// include/mimo_rx.h, device tables and workspaces, and the stage orchestration.
+//
+// Two drivers share the same kernels:
+//   * mimo_rx_process_batch: n_frames device-resident captures, every stage launched once
+//     for the whole batch on one stream, no host synchronisation (the bench's step).
+//   * mimo_rx_execute: the reference's streaming framesync::execute (framing.cc:471-506)
+//     over host chunks of any size -- samples are appended to a device capture buffer, the
+//     S&C kernels run over the new chunks only, and the channel estimate + replay decode run
+//     once the window [sync_index - SL, sync_index - SL + ACB + TX) is complete; decoded
+//     symbols are handed to the callback one OFDM symbol at a time (framing.cc:587).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "../../include/mimo_rx.h"
+#include "kernels.hpp"
+
+using namespace mimo;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string &msg) {
+  g_err = msg;
+  return code;
+}
+
+#define HIPCHK(x)                                                                       \
+  do {                                                                                  \
+    hipError_t e_ = (x);                                                                \
+    if (e_ != hipSuccess)                                                               \
+      return fail(MIMO_ERR_HIP, std::string(#x) + ": " + hipGetErrorString(e_));        \
+  } while (0)
+
+template <class T>
+struct DevBuf {
+  T *p = nullptr;
+  size_t n = 0;
+  DevBuf() = default;
+  DevBuf(const DevBuf &) = delete;
+  DevBuf &operator=(const DevBuf &) = delete;
+  ~DevBuf() { release(); }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    n = 0;
+  }
+  hipError_t ensure(size_t cnt) {
+    if (cnt <= n && p) return hipSuccess;
+    release();
+    hipError_t e = hipMalloc(reinterpret_cast<void **>(&p), sizeof(T) * std::max<size_t>(cnt, 1));
+    if (e == hipSuccess) n = cnt;
+    return e;
+  }
+};
+
+int ilog2(uint32_t v) {
+  int l = 0;
+  while ((1u << l) < v) l++;
+  return ((1u << l) == v) ? l : -1;
+}
+
+// twiddle table tw[k] = exp(-2 pi i k / kTwN), shared by all handles (device 0 of the caller)
+std::mutex g_tw_mu;
+float2 *g_tw = nullptr;
+int g_tw_dev = -1;
+
+int get_twiddles(float2 **out) {
+  std::lock_guard<std::mutex> lk(g_tw_mu);
+  int dev = 0;
+  HIPCHK(hipGetDevice(&dev));
+  if (!g_tw || g_tw_dev != dev) {
+    std::vector<float2> h(kTwN);
+    for (int k = 0; k < kTwN; k++) {
+      const double a = -2.0 * M_PI * (double)k / (double)kTwN;
+      h[k] = make_float2((float)std::cos(a), (float)std::sin(a));
+    }
+    float2 *d = nullptr;
+    HIPCHK(hipMalloc(&d, sizeof(float2) * kTwN));
+    HIPCHK(hipMemcpy(d, h.data(), sizeof(float2) * kTwN, hipMemcpyHostToDevice));
+    g_tw = d;
+    g_tw_dev = dev;
+  }
+  *out = g_tw;
+  return MIMO_OK;
+}
+
+Qam make_qam(uint32_t order) {
+  Qam q;
+  uint32_t b = 0;
+  while ((1u << (2 * b)) < order) b++;
+  q.b = b;
+  q.L = 1u << b;
+  const double e = 2.0 * ((double)q.L * q.L - 1.0) / 3.0;
+  q.scale = (float)(1.0 / std::sqrt(e));
+  q.inv_scale = (float)std::sqrt(e);
+  return q;
+}
+
+int validate_sctype(const uint8_t *p, uint32_t M, uint32_t *n0, uint32_t *n1, uint32_t *n2) {
+  uint32_t a = 0, b = 0, c = 0;
+  for (uint32_t i = 0; i < M; i++) {
+    if (p[i] == MIMO_SC_NULL) a++;
+    else if (p[i] == MIMO_SC_PILOT) b++;
+    else if (p[i] == MIMO_SC_DATA) c++;
+    else return fail(MIMO_ERR_SCTYPE, "invalid subcarrier type " + std::to_string(p[i]));
+  }
+  *n0 = a; *n1 = b; *n2 = c;
+  return MIMO_OK;
+}
+
+struct StageTimer {
+  bool on = false;
+  std::vector<std::pair<int, std::pair<hipEvent_t, hipEvent_t>>> ev;
+  hipEvent_t begin(hipStream_t s) {
+    if (!on) return nullptr;
+    hipEvent_t e;
+    if (hipEventCreate(&e) != hipSuccess) return nullptr;
+    (void)hipEventRecord(e, s);
+    return e;
+  }
+  void end(int stage, hipEvent_t b, hipStream_t s) {
+    if (!on || !b) return;
+    hipEvent_t e;
+    if (hipEventCreate(&e) != hipSuccess) return;
+    (void)hipEventRecord(e, s);
+    ev.push_back({stage, {b, e}});
+  }
+};
+
+// code tables common to the receiver and the transmitter
+struct Codes {
+  DevBuf<float2> code_time;   // [n_slots][M]
+  DevBuf<float2> codespec;    // [n_slots][F]
+};
+
+int build_codes(Codes &c, uint32_t M, uint32_t N, uint32_t nac, const uint8_t *p,
+                const uint8_t *s0_bits, const uint8_t *s1_bits, int log2F, bool spectra,
+                hipStream_t s) {
+  const uint32_t n_slots = N * nac + 1;
+  uint32_t n0, n1, n2;
+  int rc = validate_sctype(p, M, &n0, &n1, &n2);
+  if (rc) return rc;
+  uint32_t m_s0 = 0;
+  for (uint32_t i = 0; i < M; i += 2)
+    if (p[i] != MIMO_SC_NULL) m_s0++;
+  if (m_s0 == 0) return fail(MIMO_ERR_SCTYPE, "ofdmframe_init_S0: no subcarriers enabled");
+  DevBuf<uint8_t> dp, d0, d1;
+  HIPCHK(dp.ensure(M));
+  HIPCHK(d0.ensure(M));
+  HIPCHK(d1.ensure((size_t)N * nac * M));
+  HIPCHK(hipMemcpyAsync(dp.p, p, M, hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemcpyAsync(d0.p, s0_bits, M, hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemcpyAsync(d1.p, s1_bits, (size_t)N * nac * M, hipMemcpyHostToDevice, s));
+  HIPCHK(c.code_time.ensure((size_t)n_slots * M));
+  const uint32_t F = 1u << log2F;
+  if (spectra) HIPCHK(c.codespec.ensure((size_t)n_slots * F));
+  CodesArgs a{};
+  a.M = M; a.N = N; a.nac = nac; a.n_slots = n_slots;
+  a.p = dp.p; a.s0_bits = d0.p; a.s1_bits = d1.p;
+  a.dn_s0 = (float)std::sqrt(1.0 / (double)(float)m_s0);   // framing.cc:1100
+  a.dn_s1 = (float)std::sqrt(1.0 / (double)(float)M);      // framing.cc:1228
+  a.code_time = c.code_time.p;
+  a.codespec = spectra ? c.codespec.p : nullptr;
+  int rc2 = get_twiddles(const_cast<float2 **>(&a.tw));
+  if (rc2) return rc2;
+  launch_codes(a, ilog2(M), log2F, s);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipStreamSynchronize(s));  // the staging buffers die with this scope
+  return MIMO_OK;
+}
+
+}  // namespace
+
+// ======================================================================================
+struct mimo_rx {
+  // configuration (framesync ctor arguments + config.h constants)
+  uint32_t M = 0, cp = 0, SL = 0, N = 0, nac = 0, pid = 0;
+  uint32_t M_null = 0, M_pilot = 0, M_data = 0, M_occ = 0;
+  int log2M = 0, log2F = 0;
+  uint32_t F = 0, lagc = 0, n_lagc = 0, n_slots = 0;
+  int det = 0;
+  float noise_var = -1.0f;
+  int keep_bias = 1;
+  uint32_t siso_tx = 0, siso_rx = 0;
+  double thr = 0.95;
+  Qam qam{};
+  uint64_t acb = 0, txl = 0, win_len = 0;
+  float dn = 1.0f, ls_scale = 1.0f;
+  double nv_norm = 0.0;
+  std::vector<uint8_t> p;
+  std::vector<int32_t> occ_index;
+  hipStream_t stream = nullptr;
+  bool own_stream = false;
+  // device tables
+  float2 *tw = nullptr;
+  Codes codes;
+  DevBuf<float> vscale;
+  DevBuf<int8_t> s1sign;
+  DevBuf<int32_t> occ;
+  // workspace
+  uint32_t cap_frames = 0;
+  uint64_t cap_words = 0;
+  uint64_t cap_evm = 0;
+  DevBuf<unsigned long long> trig, keys;
+  DevBuf<uint64_t> bits;
+  DevBuf<FrameInfo> info;
+  DevBuf<float2> G, W;
+  DevBuf<float> gain;
+  DevBuf<double> nvp, evm_part, evm_out;
+  uint32_t last_frames = 0, last_max_out = 0;
+  uint64_t last_words = 0;
+  // streaming state (facade)
+  DevBuf<float2> capbuf;
+  uint64_t cap_len = 0, total = 0;
+  int state = MIMO_STATE_SEEK_PLATEAU;
+  uint64_t nsp = 0;
+  bool have_sync = false, have_est = false;
+  FrameInfo sinfo{};
+  DevBuf<float2> symbuf;
+  std::vector<float2> symhost;
+  mimo_rx_symbol_cb cb = nullptr;
+  void *user = nullptr;
+  StageTimer timer;
+};
+
+struct mimo_tx {
+  uint32_t M = 0, cp = 0, SL = 0, N = 0, nac = 0, M_occ = 0;
+  int log2M = 0;
+  float dn = 1.0f;
+  hipStream_t stream = nullptr;
+  Codes codes;
+  std::vector<float2> s0, s1;  // host copies of the time-domain codes
+  DevBuf<int32_t> occ_list;
+  DevBuf<float2> din, dout;
+  float2 *tw = nullptr;
+};
+
+namespace {
+
+// Per-frame arrays grow with F; the plateau bitmask grows with F * words. A growing
+// single-frame bitmask (streaming capture) keeps its earlier words: chunks already final
+// are never recomputed, and trig[] is untouched when only the capture length grows.
+int ensure_workspace(mimo_rx *h, uint32_t F, uint64_t words, uint64_t evm_entries) {
+  if (F > h->cap_frames) {
+    const uint32_t nf = F;
+    HIPCHK(h->trig.ensure(nf));
+    HIPCHK(h->keys.ensure((size_t)nf * h->N * h->n_slots));
+    HIPCHK(h->info.ensure(nf));
+    HIPCHK(h->G.ensure((size_t)nf * h->M * h->N * h->N));
+    HIPCHK(h->W.ensure((size_t)nf * h->M * h->N * h->N));
+    HIPCHK(h->gain.ensure((size_t)nf * h->M));
+    HIPCHK(h->nvp.ensure((size_t)nf * h->N * h->N));
+    HIPCHK(h->evm_out.ensure((size_t)nf * h->N * 3));
+    h->cap_frames = nf;
+    HIPCHK(h->bits.ensure((size_t)nf * h->N * h->cap_words));
+  }
+  if (words > h->cap_words) {
+    const uint64_t nw = std::max<uint64_t>(words, h->cap_words * 2);
+    uint64_t *np = nullptr;
+    HIPCHK(hipMalloc(&np, sizeof(uint64_t) * (size_t)h->cap_frames * h->N * nw));
+    if (h->bits.p && h->cap_words && h->cap_frames == 1) {
+      HIPCHK(hipMemcpy2D(np, sizeof(uint64_t) * nw, h->bits.p, sizeof(uint64_t) * h->cap_words,
+                         sizeof(uint64_t) * h->cap_words, h->N, hipMemcpyDeviceToDevice));
+    }
+    h->bits.release();
+    h->bits.p = np;
+    h->bits.n = (size_t)h->cap_frames * h->N * nw;
+    h->cap_words = nw;
+  }
+  if (evm_entries > h->cap_evm) {
+    HIPCHK(h->evm_part.ensure(evm_entries));
+    h->cap_evm = evm_entries;
+  }
+  return MIMO_OK;
+}
+
+// S&C + plateau over chunks [chunk_lo, end) of every frame
+int run_sync(mimo_rx *h, const float2 *iq, uint64_t stride, uint32_t F, uint64_t frame_len,
+             uint64_t chunk_lo, bool reset_trig, hipStream_t s) {
+  const uint64_t words = (frame_len + 63) / 64;
+  int rc = ensure_workspace(h, F, words, 0);
+  if (rc) return rc;
+  if (reset_trig) HIPCHK(hipMemsetAsync(h->trig.p, 0xFF, sizeof(unsigned long long) * F, s));
+  const uint64_t nchunks = (frame_len + kScChunk - 1) / kScChunk;
+  if (chunk_lo < nchunks) {
+    ScArgs a{};
+    a.iq = iq; a.stride = stride; a.frame_len = frame_len;
+    a.N = h->N; a.M = h->M; a.cp = h->cp;
+    a.thr = h->thr; a.band = 2e-3;
+    a.chunk_lo = chunk_lo; a.chunk_hi = nchunks;
+    a.trig = h->trig.p; a.bits = h->bits.p; a.bit_words = h->cap_words;
+    const uint32_t grid_x = (uint32_t)std::min<uint64_t>(nchunks - chunk_lo, 64);
+    hipEvent_t e = h->timer.begin(s);
+    launch_sc(a, F, grid_x, s);
+    h->timer.end(0, e, s);
+  }
+  PlateauArgs pa{};
+  pa.trig = h->trig.p; pa.bits = h->bits.p; pa.bit_words = h->cap_words;
+  pa.frame_len = frame_len; pa.N = h->N; pa.SL = h->SL; pa.win_len = h->win_len;
+  pa.info = h->info.p;
+  hipEvent_t e = h->timer.begin(s);
+  launch_plateau(pa, F, s);
+  h->timer.end(1, e, s);
+  HIPCHK(hipGetLastError());
+  return MIMO_OK;
+}
+
+int run_estimate(mimo_rx *h, const float2 *iq, uint64_t stride, uint32_t F, uint64_t frame_len,
+                 hipStream_t s) {
+  HIPCHK(hipMemsetAsync(h->keys.p, 0, sizeof(unsigned long long) * F * h->N * h->n_slots, s));
+  SearchArgs sa{};
+  sa.iq = iq; sa.stride = stride; sa.frame_len = frame_len;
+  sa.N = h->N; sa.M = h->M; sa.SL = h->SL; sa.n_slots = h->n_slots;
+  sa.lagc = h->lagc; sa.n_lagc = h->n_lagc;
+  sa.codespec = h->codes.codespec.p; sa.vscale = h->vscale.p;
+  sa.info = h->info.p; sa.keys = h->keys.p; sa.tw = h->tw;
+  hipEvent_t e = h->timer.begin(s);
+  launch_search(sa, h->log2F, F, s);
+  h->timer.end(2, e, s);
+  LsArgs la{};
+  la.iq = iq; la.stride = stride; la.frame_len = frame_len;
+  la.N = h->N; la.M = h->M; la.nac = h->nac; la.n_slots = h->n_slots;
+  la.keys = h->keys.p; la.s1sign = h->s1sign.p; la.occ_index = h->occ.p;
+  la.keep_bias = h->keep_bias; la.scale = h->ls_scale; la.info = h->info.p;
+  la.G = h->G.p; la.nv_part = h->nvp.p; la.tw = h->tw;
+  e = h->timer.begin(s);
+  launch_ls(la, h->log2M, F, s);
+  h->timer.end(3, e, s);
+  WeightArgs wa{};
+  wa.N = h->N; wa.M = h->M; wa.M_occ = h->M_occ; wa.nac = h->nac; wa.SL = h->SL;
+  wa.n_slots = h->n_slots; wa.detector = h->det; wa.noise_var = h->noise_var;
+  wa.nv_norm = h->nv_norm; wa.occ_index = h->occ.p; wa.G = h->G.p; wa.W = h->W.p;
+  wa.gain = h->gain.p; wa.nv_part = h->nvp.p; wa.keys = h->keys.p; wa.win_len = h->win_len;
+  wa.info = h->info.p;
+  e = h->timer.begin(s);
+  launch_weights(wa, F, s);
+  h->timer.end(4, e, s);
+  HIPCHK(hipGetLastError());
+  return MIMO_OK;
+}
+
+int run_decode(mimo_rx *h, const float2 *iq, uint64_t stride, uint32_t F, uint64_t frame_len,
+               uint32_t max_out, float2 *out_sym, uint8_t *out_idx, int ref_mode,
+               const uint8_t *ref_idx, uint64_t ref_seed, uint64_t frame_id0, hipStream_t s) {
+  int rc = ensure_workspace(h, F, 0, (uint64_t)F * max_out * h->N * 3);
+  if (rc) return rc;
+  if (max_out == 0) return MIMO_OK;
+  DecodeArgs d{};
+  d.iq = iq; d.stride = stride; d.frame_len = frame_len;
+  d.N = h->N; d.M = h->M; d.cp = h->cp; d.SL = h->SL; d.M_occ = h->M_occ;
+  d.detector = h->det; d.siso_tx = h->siso_tx; d.siso_rx = h->siso_rx; d.dn = h->dn;
+  d.occ_index = h->occ.p; d.W = h->W.p; d.gain = h->gain.p; d.G = h->G.p; d.info = h->info.p;
+  d.max_out = max_out; d.out_sym = out_sym; d.out_idx = out_idx;
+  d.ref_mode = ref_mode; d.ref_idx = ref_idx; d.ref_seed = ref_seed; d.frame_id0 = frame_id0;
+  d.qam = h->qam; d.evm_part = h->evm_part.p; d.tw = h->tw;
+  hipEvent_t e = h->timer.begin(s);
+  launch_decode(d, h->log2M, F, s);
+  h->timer.end(5, e, s);
+  EvmArgs ea{};
+  ea.N = h->N; ea.max_out = max_out; ea.info = h->info.p; ea.evm_part = h->evm_part.p;
+  ea.evm_out = h->evm_out.p;
+  e = h->timer.begin(s);
+  launch_evm(ea, F, s);
+  h->timer.end(6, e, s);
+  HIPCHK(hipGetLastError());
+  return MIMO_OK;
+}
+
+}  // namespace
+
+// ======================================================================================
+extern "C" {
+
+const char *mimo_last_error(void) { return g_err.c_str(); }
+const char *mimo_version(void) { return "rub_mimo_amd 0.1.0 (gfx950)"; }
+
+int mimo_rx_create(const mimo_rx_config *cfg, void *hip_stream, mimo_rx **out) {
+  if (!cfg || !out || !cfg->p || !cfg->s0_bits || !cfg->s1_bits)
+    return fail(MIMO_ERR_ARG, "mimo_rx_create: null argument");
+  *out = nullptr;
+  const int l2 = ilog2(cfg->M);
+  if (l2 < 6 || l2 > 12) return fail(MIMO_ERR_UNSUPPORTED, "M must be a power of two in [64, 4096]");
+  const uint32_t N = cfg->num_streams;
+  if (!(N == 1 || N == 2 || N == 4 || N == 8))
+    return fail(MIMO_ERR_UNSUPPORTED, "num_streams must be 1, 2, 4 or 8");
+  if (cfg->cp_len == 0 || cfg->cp_len > cfg->M / 2)
+    return fail(MIMO_ERR_ARG, "cp_len must be in [1, M/2]");
+  if (cfg->num_access_codes == 0) return fail(MIMO_ERR_ARG, "num_access_codes must be > 0");
+  if (cfg->detector < 0 || cfg->detector > 3) return fail(MIMO_ERR_ARG, "bad detector");
+  if ((cfg->detector == MIMO_DET_ZF2) && N != 2)
+    return fail(MIMO_ERR_ARG, "the reference invert() is 2x2 only (framing.cc:1346)");
+  if (cfg->detector == MIMO_DET_SISO && (cfg->siso_tx >= N || cfg->siso_rx >= N))
+    return fail(MIMO_ERR_ARG, "siso_tx/siso_rx out of range");
+  const uint32_t q = cfg->qam_order;
+  if (!(q == 4 || q == 16 || q == 64 || q == 256))
+    return fail(MIMO_ERR_ARG, "qam_order must be 4, 16, 64 or 256");
+  mimo_rx *h = new mimo_rx();
+  h->M = cfg->M; h->cp = cfg->cp_len; h->SL = h->M + h->cp; h->N = N;
+  h->nac = cfg->num_access_codes; h->pid = cfg->pid_max;
+  h->log2M = l2;
+  h->p.assign(cfg->p, cfg->p + h->M);
+  int rc = validate_sctype(h->p.data(), h->M, &h->M_null, &h->M_pilot, &h->M_data);
+  if (rc) { delete h; return rc; }
+  h->M_occ = h->M_pilot + h->M_data;
+  if (h->M_occ == 0) { delete h; return fail(MIMO_ERR_SCTYPE, "no occupied subcarriers"); }
+  h->occ_index.resize(h->M);
+  std::vector<int8_t> sign((size_t)N * h->nac * h->M);
+  for (uint32_t i = 0, j = 0; i < h->M; i++) h->occ_index[i] = (h->p[i] != MIMO_SC_NULL) ? (int32_t)j++ : -1;
+  for (uint32_t t = 0; t < N; t++)
+    for (uint32_t c = 0; c < h->nac; c++)
+      for (uint32_t i = 0; i < h->M; i++) {
+        const size_t o = ((size_t)t * h->nac + c) * h->M + i;
+        sign[o] = (h->p[i] == MIMO_SC_NULL) ? 0 : ((cfg->s1_bits[o] & 1) ? 1 : -1);
+      }
+  h->det = cfg->detector;
+  h->noise_var = cfg->noise_var;
+  h->keep_bias = cfg->keep_identity_bias ? 1 : 0;
+  h->siso_tx = cfg->siso_tx; h->siso_rx = cfg->siso_rx;
+  h->thr = cfg->plateau_threshold;
+  h->qam = make_qam(q);
+  h->acb = (uint64_t)h->SL * (h->nac * N + 4);     // framing.cc:284
+  h->txl = (uint64_t)h->pid * h->SL;               // framing.cc:285
+  h->win_len = h->acb + h->txl;
+  h->dn = 1.0f / sqrtf((float)h->M_occ);           // framing.cc:330
+  h->ls_scale = h->dn / (float)h->nac;             // framing.cc:821
+  h->nv_norm = (h->nac >= 2) ? ((double)h->dn * (double)h->dn /
+                                ((double)h->M_occ * N * N * (h->nac - 1)))
+                             : 0.0;
+  // search transform: F >= SL + M - 1 lags+taps, capped at 8192 (then several lag chunks)
+  uint32_t F = 1;
+  while (F < h->SL + h->M - 1) F <<= 1;
+  if (F > 8192) F = 8192;
+  if (F < 2 * h->M) F = 2 * h->M;
+  h->F = F; h->log2F = ilog2(F);
+  h->lagc = F - h->M + 1;
+  h->n_lagc = (h->SL + h->lagc - 1) / h->lagc;
+  h->n_slots = N * h->nac + 1;
+  if (hip_stream) {
+    h->stream = (hipStream_t)hip_stream;
+  } else {
+    if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) {
+      delete h;
+      return fail(MIMO_ERR_HIP, "hipStreamCreate failed");
+    }
+    h->own_stream = true;
+  }
+  rc = get_twiddles(&h->tw);
+  if (!rc) rc = build_codes(h->codes, h->M, N, h->nac, h->p.data(), cfg->s0_bits, cfg->s1_bits,
+                            h->log2F, true, h->stream);
+  if (rc) { mimo_rx_destroy(h); return rc; }
+  uint32_t m_s0 = 0;
+  for (uint32_t i = 0; i < h->M; i += 2) if (h->p[i] != MIMO_SC_NULL) m_s0++;
+  std::vector<float> vs(h->n_slots);
+  const double FF = (double)F * (double)F, MM = (double)h->M * (double)h->M;
+  vs[0] = (float)((double)m_s0 / (MM * FF));
+  for (uint32_t sl = 1; sl < h->n_slots; sl++) vs[sl] = (float)(1.0 / ((double)h->M * FF));
+  if (h->vscale.ensure(h->n_slots) != hipSuccess || h->s1sign.ensure(sign.size()) != hipSuccess ||
+      h->occ.ensure(h->M) != hipSuccess ||
+      hipMemcpy(h->vscale.p, vs.data(), sizeof(float) * vs.size(), hipMemcpyHostToDevice) !=
+          hipSuccess ||
+      hipMemcpy(h->s1sign.p, sign.data(), sign.size(), hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(h->occ.p, h->occ_index.data(), sizeof(int32_t) * h->M, hipMemcpyHostToDevice) !=
+          hipSuccess) {
+    mimo_rx_destroy(h);
+    return fail(MIMO_ERR_HIP, "table upload failed");
+  }
+  *out = h;
+  return MIMO_OK;
+}
+
+int mimo_rx_destroy(mimo_rx *h) {
+  if (!h) return MIMO_OK;
+  if (h->stream) (void)hipStreamSynchronize(h->stream);
+  for (auto &e : h->timer.ev) {
+    (void)hipEventDestroy(e.second.first);
+    (void)hipEventDestroy(e.second.second);
+  }
+  if (h->own_stream && h->stream) (void)hipStreamDestroy(h->stream);
+  delete h;
+  return MIMO_OK;
+}
+
+int mimo_rx_set_callback(mimo_rx *h, mimo_rx_symbol_cb cb, void *user) {
+  if (!h) return fail(MIMO_ERR_ARG, "null handle");
+  h->cb = cb;
+  h->user = user;
+  return MIMO_OK;
+}
+
+int mimo_rx_set_siso(mimo_rx *h, uint32_t tx, uint32_t rx) {
+  if (!h || tx >= h->N || rx >= h->N) return fail(MIMO_ERR_ARG, "siso index out of range");
+  h->siso_tx = tx;
+  h->siso_rx = rx;
+  return MIMO_OK;
+}
+
+// ---------------- streaming framesync::execute ----------------
+static int grow_capture(mimo_rx *h, uint64_t need) {
+  if (need <= h->cap_len && h->capbuf.p) return MIMO_OK;
+  uint64_t nc = std::max<uint64_t>(need, h->cap_len * 2);
+  nc = std::max<uint64_t>(nc, 1 << 16);
+  float2 *np = nullptr;
+  HIPCHK(hipMalloc(&np, sizeof(float2) * nc * h->N));
+  if (h->capbuf.p && h->total) {
+    HIPCHK(hipMemcpy2DAsync(np, sizeof(float2) * nc, h->capbuf.p, sizeof(float2) * h->cap_len,
+                            sizeof(float2) * h->total, h->N, hipMemcpyDeviceToDevice, h->stream));
+  }
+  HIPCHK(hipStreamSynchronize(h->stream));
+  h->capbuf.release();
+  h->capbuf.p = np;
+  h->capbuf.n = nc * h->N;
+  h->cap_len = nc;
+  return MIMO_OK;
+}
+
+static int finish_estimate(mimo_rx *h) {
+  // channel estimate + replay decode of the complete window; callbacks per OFDM symbol
+  const float2 *iq = h->capbuf.p;
+  int rc = run_estimate(h, iq, h->cap_len, 1, h->total, h->stream);
+  if (rc) return rc;
+  HIPCHK(hipMemcpyAsync(&h->sinfo, h->info.p, sizeof(FrameInfo), hipMemcpyDeviceToHost,
+                        h->stream));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  const uint32_t n_sym = h->sinfo.n_sym;
+  const size_t per = (size_t)h->N * h->M_occ;
+  if (n_sym) {
+    HIPCHK(h->symbuf.ensure(per * n_sym));
+    rc = run_decode(h, iq, h->cap_len, 1, h->total, n_sym, h->symbuf.p, nullptr, 0, nullptr, 0,
+                    0, h->stream);
+    if (rc) return rc;
+    h->symhost.resize(per * n_sym);
+    HIPCHK(hipMemcpyAsync(h->symhost.data(), h->symbuf.p, sizeof(float2) * per * n_sym,
+                          hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(hipStreamSynchronize(h->stream));
+  } else {
+    h->symhost.clear();
+  }
+  h->have_est = true;
+  h->last_frames = 1;
+  h->last_max_out = n_sym;
+  if (h->cb) {
+    std::vector<const float *> ptr(h->N);
+    for (uint32_t s = 0; s < n_sym; s++) {
+      for (uint32_t t = 0; t < h->N; t++)
+        ptr[t] = reinterpret_cast<const float *>(h->symhost.data() +
+                                                 ((size_t)t * n_sym + s) * h->M_occ);
+      h->cb(ptr.data(), h->N, h->M_occ, h->user);
+    }
+  }
+  return MIMO_OK;
+}
+
+int mimo_rx_execute(mimo_rx *h, const float *const *iq, uint32_t n_ant, uint64_t n,
+                    int32_t *state_out) {
+  if (!h || (!iq && n)) return fail(MIMO_ERR_ARG, "null argument");
+  if (n_ant != h->N) return fail(MIMO_ERR_ARG, "n_ant must equal num_streams");
+  if (h->state == MIMO_STATE_MIMO) {   // framing.cc:494-503: consume one sample and break
+    if (n) h->nsp += 1;
+    if (state_out) *state_out = h->state;
+    return MIMO_OK;
+  }
+  if (n == 0) {
+    if (state_out) *state_out = h->state;
+    return MIMO_OK;
+  }
+  const uint64_t old_total = h->total;
+  int rc = grow_capture(h, old_total + n);
+  if (rc) return rc;
+  for (uint32_t s = 0; s < h->N; s++)
+    HIPCHK(hipMemcpyAsync(h->capbuf.p + (size_t)s * h->cap_len + old_total, iq[s],
+                          sizeof(float2) * n, hipMemcpyHostToDevice, h->stream));
+  h->total = old_total + n;
+  if (h->state == MIMO_STATE_SEEK_PLATEAU) {
+    if (old_total == 0) {
+      rc = ensure_workspace(h, 1, (h->total + 63) / 64, 0);
+      if (rc) return rc;
+      HIPCHK(hipMemsetAsync(h->trig.p, 0xFF, sizeof(unsigned long long), h->stream));
+    }
+    // re-run the partially filled chunk; earlier chunks are final (y[n] uses x[<=n] only)
+    rc = run_sync(h, h->capbuf.p, h->cap_len, 1, h->total, old_total / kScChunk, false,
+                  h->stream);
+    if (rc) return rc;
+    HIPCHK(hipMemcpyAsync(&h->sinfo, h->info.p, sizeof(FrameInfo), hipMemcpyDeviceToHost,
+                          h->stream));
+    HIPCHK(hipStreamSynchronize(h->stream));
+    if (h->sinfo.status == MIMO_FRAME_NO_SYNC) {
+      h->nsp = h->total;
+    } else {
+      h->have_sync = true;
+      h->state = MIMO_STATE_SAVE_ACCESS_CODES;
+    }
+  } else {
+    // SAVE: refresh completeness against the longer capture
+    rc = run_sync(h, h->capbuf.p, h->cap_len, 1, h->total, ~0ull, false, h->stream);
+    if (rc) return rc;
+    HIPCHK(hipMemcpyAsync(&h->sinfo, h->info.p, sizeof(FrameInfo), hipMemcpyDeviceToHost,
+                          h->stream));
+    HIPCHK(hipStreamSynchronize(h->stream));
+  }
+  if (h->state == MIMO_STATE_SAVE_ACCESS_CODES) {
+    if (h->sinfo.status == MIMO_FRAME_OK) {
+      h->nsp = h->sinfo.nsp;
+      rc = finish_estimate(h);
+      if (rc) return rc;
+      h->state = MIMO_STATE_MIMO;
+    } else {
+      h->nsp = h->total;
+    }
+  }
+  if (state_out) *state_out = h->state;
+  return MIMO_OK;
+}
+
+int mimo_rx_reset(mimo_rx *h) {
+  // framing.cc:461-464 only rewinds the state; here the receiver re-arms on a fresh capture
+  // (documented deviation: the reference keeps stale S&C filter history and accumulates
+  // sync_index across resets).
+  if (!h) return fail(MIMO_ERR_ARG, "null handle");
+  HIPCHK(hipStreamSynchronize(h->stream));
+  h->state = MIMO_STATE_SEEK_PLATEAU;
+  h->total = 0;
+  h->have_sync = false;
+  h->have_est = false;
+  return MIMO_OK;
+}
+
+int mimo_rx_get_state(const mimo_rx *h, int32_t *st) {
+  if (!h || !st) return fail(MIMO_ERR_ARG, "null argument");
+  *st = h->state;
+  return MIMO_OK;
+}
+
+int mimo_rx_get_sync_index(const mimo_rx *h, uint64_t *out) {
+  if (!h || !out) return fail(MIMO_ERR_ARG, "null argument");
+  *out = h->have_sync ? h->sinfo.sync_index : 0;
+  return MIMO_OK;
+}
+
+int mimo_rx_get_num_samples_processed(const mimo_rx *h, uint64_t *out) {
+  if (!h || !out) return fail(MIMO_ERR_ARG, "null argument");
+  *out = h->nsp;
+  return MIMO_OK;
+}
+
+int mimo_rx_get_plateau(const mimo_rx *h, uint32_t s, uint64_t *start, uint64_t *end) {
+  if (!h || s >= h->N) return fail(MIMO_ERR_ARG, "bad stream");
+  if (start) *start = h->have_sync ? h->sinfo.plateau_start[s] : 0;
+  if (end) *end = h->have_sync ? h->sinfo.plateau_end[s] : 0;
+  return MIMO_OK;
+}
+
+int mimo_rx_get_m_occ(const mimo_rx *h, uint32_t *m) {
+  if (!h || !m) return fail(MIMO_ERR_ARG, "null argument");
+  *m = h->M_occ;
+  return MIMO_OK;
+}
+
+int mimo_rx_get_G(mimo_rx *h, float *G) {
+  if (!h || !G) return fail(MIMO_ERR_ARG, "null argument");
+  const size_t n = (size_t)h->M * h->N * h->N;
+  if (!h->have_est) {   // framing.cc:302-319 identity on occupied carriers
+    std::memset(G, 0, sizeof(float2) * n);
+    for (uint32_t k = 0; k < h->M; k++)
+      if (h->p[k] != MIMO_SC_NULL)
+        for (uint32_t r = 0; r < h->N; r++) G[2 * ((k * h->N + r) * h->N + r)] = 1.0f;
+    return MIMO_OK;
+  }
+  HIPCHK(hipMemcpy(G, h->G.p, sizeof(float2) * n, hipMemcpyDeviceToHost));
+  return MIMO_OK;
+}
+
+static int copy_W(mimo_rx *h, uint32_t f, float *W) {
+  const size_t n = (size_t)h->M * h->N * h->N;
+  std::vector<float2> tmp(n);
+  HIPCHK(hipMemcpy(tmp.data(), h->W.p + (size_t)f * n, sizeof(float2) * n,
+                   hipMemcpyDeviceToHost));
+  float2 *o = reinterpret_cast<float2 *>(W);
+  for (uint32_t t = 0; t < h->N; t++)
+    for (uint32_t r = 0; r < h->N; r++)
+      for (uint32_t k = 0; k < h->M; k++)
+        o[((size_t)k * h->N + t) * h->N + r] = tmp[((size_t)t * h->N + r) * h->M + k];
+  return MIMO_OK;
+}
+
+int mimo_rx_get_W(mimo_rx *h, float *W) {
+  if (!h || !W) return fail(MIMO_ERR_ARG, "null argument");
+  if (!h->have_est) return mimo_rx_get_G(h, W);  // W also starts as identity
+  return copy_W(h, 0, W);
+}
+
+int mimo_rx_get_gain(mimo_rx *h, float *gain) {
+  if (!h || !gain) return fail(MIMO_ERR_ARG, "null argument");
+  if (!h->have_est) {
+    for (uint32_t j = 0; j < h->M_occ; j++) gain[j] = 1.0f;
+    return MIMO_OK;
+  }
+  std::vector<float> tmp(h->M);
+  HIPCHK(hipMemcpy(tmp.data(), h->gain.p, sizeof(float) * h->M, hipMemcpyDeviceToHost));
+  for (uint32_t k = 0; k < h->M; k++)
+    if (h->occ_index[k] >= 0) gain[h->occ_index[k]] = tmp[k];
+  return MIMO_OK;
+}
+
+int mimo_rx_get_noise_var(mimo_rx *h, float *out) {
+  if (!h || !out) return fail(MIMO_ERR_ARG, "null argument");
+  *out = h->have_est ? h->sinfo.noise_var : h->noise_var;
+  return MIMO_OK;
+}
+
+static int copy_corr(mimo_rx *h, uint32_t F, uint32_t *corr, uint32_t *s0) {
+  std::vector<unsigned long long> k((size_t)F * h->N * h->n_slots);
+  HIPCHK(hipMemcpy(k.data(), h->keys.p, sizeof(unsigned long long) * k.size(),
+                   hipMemcpyDeviceToHost));
+  auto idx = [](unsigned long long v) -> uint32_t {
+    return v ? (0xFFFFFFFFu - (uint32_t)(v & 0xFFFFFFFFull)) : 0u;
+  };
+  for (uint32_t f = 0; f < F; f++)
+    for (uint32_t r = 0; r < h->N; r++) {
+      const unsigned long long *kk = k.data() + ((size_t)f * h->N + r) * h->n_slots;
+      if (s0) s0[f * h->N + r] = idx(kk[0]);
+      if (corr)
+        for (uint32_t ac = 0; ac + 1 < h->n_slots; ac++)
+          corr[((size_t)f * h->N + r) * (h->n_slots - 1) + ac] = idx(kk[1 + ac]);
+    }
+  return MIMO_OK;
+}
+
+int mimo_rx_get_corr(mimo_rx *h, uint32_t *corr, uint32_t *s0) {
+  if (!h) return fail(MIMO_ERR_ARG, "null handle");
+  if (!h->have_est) {
+    if (corr) std::memset(corr, 0, sizeof(uint32_t) * h->N * (h->n_slots - 1));
+    if (s0) std::memset(s0, 0, sizeof(uint32_t) * h->N);
+    return MIMO_OK;
+  }
+  return copy_corr(h, 1, corr, s0);
+}
+
+// ---------------- batched device frames ----------------
+int mimo_rx_process_batch(mimo_rx *h, const mimo_batch *b, void *hip_stream) {
+  if (!h || !b || !b->d_iq) return fail(MIMO_ERR_ARG, "null argument");
+  if (b->n_frames == 0) return MIMO_OK;
+  if (b->stride < b->frame_len) return fail(MIMO_ERR_ARG, "stride < frame_len");
+  if (b->ref_mode == 1 && !b->d_ref_idx) return fail(MIMO_ERR_ARG, "ref_mode 1 needs d_ref_idx");
+  hipStream_t s = hip_stream ? (hipStream_t)hip_stream : h->stream;
+  const float2 *iq = reinterpret_cast<const float2 *>(b->d_iq);
+  int rc = run_sync(h, iq, b->stride, b->n_frames, b->frame_len, 0, true, s);
+  if (!rc) rc = run_estimate(h, iq, b->stride, b->n_frames, b->frame_len, s);
+  if (!rc)
+    rc = run_decode(h, iq, b->stride, b->n_frames, b->frame_len, b->max_out_syms,
+                    reinterpret_cast<float2 *>(b->d_out_sym),
+                    reinterpret_cast<uint8_t *>(b->d_out_idx), b->ref_mode,
+                    reinterpret_cast<const uint8_t *>(b->d_ref_idx), b->ref_seed, b->frame_id0,
+                    s);
+  if (rc) return rc;
+  h->last_frames = b->n_frames;
+  h->last_max_out = b->max_out_syms;
+  h->last_words = (b->frame_len + 63) / 64;
+  return MIMO_OK;
+}
+
+int mimo_rx_batch_results(mimo_rx *h, mimo_frame_result *out, uint32_t F) {
+  if (!h || !out) return fail(MIMO_ERR_ARG, "null argument");
+  if (F > h->last_frames) return fail(MIMO_ERR_ARG, "more frames than the last batch");
+  std::vector<FrameInfo> inf(F);
+  std::vector<double> ev((size_t)F * h->N * 3);
+  HIPCHK(hipStreamSynchronize(h->stream));
+  HIPCHK(hipDeviceSynchronize());
+  HIPCHK(hipMemcpy(inf.data(), h->info.p, sizeof(FrameInfo) * F, hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(ev.data(), h->evm_out.p, sizeof(double) * ev.size(), hipMemcpyDeviceToHost));
+  for (uint32_t f = 0; f < F; f++) {
+    mimo_frame_result &r = out[f];
+    std::memset(&r, 0, sizeof(r));
+    r.status = inf[f].status;
+    r.n_sym = (inf[f].status == 0) ? inf[f].n_sym : 0;
+    r.trigger = inf[f].trigger;
+    r.sync_index = inf[f].sync_index;
+    r.num_samples_processed = inf[f].nsp;
+    r.noise_var = inf[f].noise_var;
+    for (uint32_t s = 0; s < h->N; s++) {
+      r.plateau_start[s] = inf[f].plateau_start[s];
+      r.plateau_end[s] = inf[f].plateau_end[s];
+      if (inf[f].status == 0) {
+        r.evm_num[s] = ev[((size_t)f * h->N + s) * 3 + 0];
+        r.evm_den[s] = ev[((size_t)f * h->N + s) * 3 + 1];
+        r.errors[s] = (uint64_t)ev[((size_t)f * h->N + s) * 3 + 2];
+      }
+    }
+  }
+  return MIMO_OK;
+}
+
+int mimo_rx_batch_corr(mimo_rx *h, uint32_t *corr, uint32_t *s0, uint32_t F) {
+  if (!h) return fail(MIMO_ERR_ARG, "null handle");
+  if (F > h->last_frames) return fail(MIMO_ERR_ARG, "more frames than the last batch");
+  HIPCHK(hipDeviceSynchronize());
+  return copy_corr(h, F, corr, s0);
+}
+
+int mimo_rx_batch_G(mimo_rx *h, float *G, uint32_t F) {
+  if (!h || !G) return fail(MIMO_ERR_ARG, "null argument");
+  if (F > h->last_frames) return fail(MIMO_ERR_ARG, "more frames than the last batch");
+  HIPCHK(hipDeviceSynchronize());
+  HIPCHK(hipMemcpy(G, h->G.p, sizeof(float2) * (size_t)F * h->M * h->N * h->N,
+                   hipMemcpyDeviceToHost));
+  return MIMO_OK;
+}
+
+int mimo_rx_batch_W(mimo_rx *h, float *W, uint32_t F) {
+  if (!h || !W) return fail(MIMO_ERR_ARG, "null argument");
+  if (F > h->last_frames) return fail(MIMO_ERR_ARG, "more frames than the last batch");
+  HIPCHK(hipDeviceSynchronize());
+  for (uint32_t f = 0; f < F; f++) {
+    int rc = copy_W(h, f, W + (size_t)f * h->M * h->N * h->N * 2);
+    if (rc) return rc;
+  }
+  return MIMO_OK;
+}
+
+int mimo_rx_set_timing(mimo_rx *h, int enable) {
+  if (!h) return fail(MIMO_ERR_ARG, "null handle");
+  h->timer.on = enable != 0;
+  return MIMO_OK;
+}
+
+int mimo_rx_get_stage_times(mimo_rx *h, double *ms, uint32_t *launches) {
+  if (!h) return fail(MIMO_ERR_ARG, "null handle");
+  for (int i = 0; i < MIMO_NUM_STAGES; i++) {
+    if (ms) ms[i] = 0.0;
+    if (launches) launches[i] = 0;
+  }
+  for (auto &e : h->timer.ev) {
+    HIPCHK(hipEventSynchronize(e.second.second));
+    float t = 0.0f;
+    HIPCHK(hipEventElapsedTime(&t, e.second.first, e.second.second));
+    if (ms) ms[e.first] += t;
+    if (launches) launches[e.first] += 1;
+    (void)hipEventDestroy(e.second.first);
+    (void)hipEventDestroy(e.second.second);
+  }
+  h->timer.ev.clear();
+  return MIMO_OK;
+}
+
+// ---------------- transmitter ----------------
+int mimo_tx_create(uint32_t M, uint32_t cp, uint32_t N, uint32_t nac, const uint8_t *p,
+                   const uint8_t *s0_bits, const uint8_t *s1_bits, mimo_tx **out) {
+  if (!p || !s0_bits || !s1_bits || !out) return fail(MIMO_ERR_ARG, "null argument");
+  const int l2 = ilog2(M);
+  if (l2 < 6 || l2 > 12) return fail(MIMO_ERR_UNSUPPORTED, "M must be a power of two in [64, 4096]");
+  if (N == 0 || N > MIMO_MAX_STREAMS || cp == 0 || cp > M / 2 || nac == 0)
+    return fail(MIMO_ERR_ARG, "bad framegen parameters");
+  uint32_t n0, n1, n2;
+  int rc = validate_sctype(p, M, &n0, &n1, &n2);
+  if (rc) return rc;
+  mimo_tx *h = new mimo_tx();
+  h->M = M; h->cp = cp; h->SL = M + cp; h->N = N; h->nac = nac; h->M_occ = n1 + n2;
+  h->log2M = l2;
+  h->dn = 1.0f / sqrtf((float)h->M_occ);   // framing.cc:115
+  if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) {
+    delete h;
+    return fail(MIMO_ERR_HIP, "hipStreamCreate failed");
+  }
+  rc = get_twiddles(&h->tw);
+  if (!rc) rc = build_codes(h->codes, M, N, nac, p, s0_bits, s1_bits, l2 + 1, false, h->stream);
+  if (rc) { mimo_tx_destroy(h); return rc; }
+  const uint32_t n_slots = N * nac + 1;
+  std::vector<float2> all((size_t)n_slots * M);
+  std::vector<int32_t> occ;
+  for (uint32_t i = 0; i < M; i++) if (p[i] != MIMO_SC_NULL) occ.push_back((int32_t)i);
+  if (hipMemcpy(all.data(), h->codes.code_time.p, sizeof(float2) * all.size(),
+                hipMemcpyDeviceToHost) != hipSuccess ||
+      h->occ_list.ensure(occ.size()) != hipSuccess ||
+      hipMemcpy(h->occ_list.p, occ.data(), sizeof(int32_t) * occ.size(),
+                hipMemcpyHostToDevice) != hipSuccess) {
+    mimo_tx_destroy(h);
+    return fail(MIMO_ERR_HIP, "framegen table upload failed");
+  }
+  h->s0.assign(all.begin(), all.begin() + M);
+  // regroup slot-major (slot = 1 + code*N + t) into per-stream [t][code*M + i]
+  h->s1.resize((size_t)N * nac * M);
+  for (uint32_t c = 0; c < nac; c++)
+    for (uint32_t t = 0; t < N; t++)
+      std::memcpy(h->s1.data() + ((size_t)t * nac + c) * M,
+                  all.data() + (size_t)(1 + c * N + t) * M, sizeof(float2) * M);
+  *out = h;
+  return MIMO_OK;
+}
+
+int mimo_tx_destroy(mimo_tx *h) {
+  if (!h) return MIMO_OK;
+  if (h->stream) {
+    (void)hipStreamSynchronize(h->stream);
+    (void)hipStreamDestroy(h->stream);
+  }
+  delete h;
+  return MIMO_OK;
+}
+
+int mimo_tx_get_codes(mimo_tx *h, float *s0, float *s1) {
+  if (!h) return fail(MIMO_ERR_ARG, "null handle");
+  if (s0) std::memcpy(s0, h->s0.data(), sizeof(float2) * h->s0.size());
+  if (s1) std::memcpy(s1, h->s1.data(), sizeof(float2) * h->s1.size());
+  return MIMO_OK;
+}
+
+int mimo_tx_write_sync_words(mimo_tx *h, float *const *tx, uint32_t *n_written) {
+  // framing.cc:169-208: S0 (CP + body) on stream 0, then nac x N TDMA slots of S1
+  if (!h || !tx) return fail(MIMO_ERR_ARG, "null argument");
+  const uint32_t M = h->M, cp = h->cp, total = (h->nac * h->N + 1) * h->SL;
+  for (uint32_t s = 0; s < h->N; s++) std::memset(tx[s], 0, sizeof(float2) * total);
+  uint32_t idx = 0;
+  auto put = [&](uint32_t s, const float2 *code) {
+    std::memcpy(reinterpret_cast<float2 *>(tx[s]) + idx, code + M - cp, sizeof(float2) * cp);
+    idx += cp;
+    std::memcpy(reinterpret_cast<float2 *>(tx[s]) + idx, code, sizeof(float2) * M);
+    idx += M;
+  };
+  put(0, h->s0.data());
+  for (uint32_t ac = 0; ac < h->nac; ac++)
+    for (uint32_t s = 0; s < h->N; s++) put(s, h->s1.data() + ((size_t)s * h->nac + ac) * M);
+  if (n_written) *n_written = idx;
+  return MIMO_OK;
+}
+
+int mimo_tx_assemble_mimo_packet(mimo_tx *h, float *const *tx, const float *const *in,
+                                 uint32_t *n_written) {
+  if (!h || !tx || !in) return fail(MIMO_ERR_ARG, "null argument");
+  const size_t per = h->M_occ;
+  HIPCHK(h->din.ensure(per * h->N));
+  HIPCHK(h->dout.ensure((size_t)h->SL * h->N));
+  for (uint32_t t = 0; t < h->N; t++)
+    HIPCHK(hipMemcpyAsync(h->din.p + t * per, in[t], sizeof(float2) * per, hipMemcpyHostToDevice,
+                          h->stream));
+  TxSymArgs a{};
+  a.N = h->N; a.M = h->M; a.cp = h->cp; a.M_occ = h->M_occ; a.dn = h->dn; a.gain = 1.0f;
+  a.occ_list = h->occ_list.p; a.in = h->din.p; a.n_sym = 1; a.out = h->dout.p; a.tw = h->tw;
+  a.qam = make_qam(4);
+  launch_tx_symbols(a, h->log2M, 1, h->stream);
+  HIPCHK(hipGetLastError());
+  for (uint32_t t = 0; t < h->N; t++)
+    HIPCHK(hipMemcpyAsync(tx[t], h->dout.p + (size_t)t * h->SL, sizeof(float2) * h->SL,
+                          hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  if (n_written) *n_written = h->SL;
+  return MIMO_OK;
+}
+
+// ---------------- synthetic captures ----------------
+static uint64_t synth_offset(const mimo_synth_config *c, uint64_t frame_id) {
+  const uint64_t SL = c->M + c->cp_len;
+  if (c->offset >= 0) return (uint64_t)c->offset;
+  // ref_hash5(seed, DOM_OFFSET, frame, 0, 0) % SL on the host (same mixer as the kernels)
+  auto mix = [](uint64_t z) {
+    z += 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+  };
+  uint64_t hh = mix(c->seed ^ ((uint64_t)DOM_OFFSET * 0xD6E8FEB86659FD93ull));
+  hh = mix(hh ^ frame_id);
+  hh = mix(hh ^ 0ull);
+  hh = mix(hh ^ 0ull);
+  return hh % SL;
+}
+
+int mimo_synth_frame_len(const mimo_synth_config *c, uint64_t frame_id, uint64_t *len) {
+  if (!c || !len) return fail(MIMO_ERR_ARG, "null argument");
+  const uint64_t SL = c->M + c->cp_len;
+  *len = SL * (2ull * c->num_streams * c->num_access_codes + 2 + c->pid + c->tail_syms) +
+         synth_offset(c, frame_id);
+  return MIMO_OK;
+}
+
+int mimo_synth_frames(const mimo_synth_config *c, uint64_t frame_id0, uint32_t n_frames,
+                      void *d_out, uint64_t stride, uint64_t frame_len, void *d_tx_idx,
+                      void *d_H, void *hip_stream) {
+  if (!c || !d_out || !c->p || !c->s0_bits || !c->s1_bits)
+    return fail(MIMO_ERR_ARG, "null argument");
+  const int l2 = ilog2(c->M);
+  if (l2 < 6 || l2 > 12) return fail(MIMO_ERR_UNSUPPORTED, "M must be a power of two in [64, 4096]");
+  const uint32_t N = c->num_streams;
+  if (N == 0 || N > MIMO_MAX_STREAMS) return fail(MIMO_ERR_ARG, "bad num_streams");
+  if (stride < frame_len) return fail(MIMO_ERR_ARG, "stride < frame_len");
+  uint32_t n0, n1, n2;
+  int rc = validate_sctype(c->p, c->M, &n0, &n1, &n2);
+  if (rc) return rc;
+  const uint32_t M_occ = n1 + n2, SL = c->M + c->cp_len;
+  hipStream_t s = hip_stream ? (hipStream_t)hip_stream : nullptr;
+  Codes codes;
+  rc = build_codes(codes, c->M, N, c->num_access_codes, c->p, c->s0_bits, c->s1_bits, l2 + 1,
+                   false, s);
+  if (rc) return rc;
+  float2 *tw = nullptr;
+  rc = get_twiddles(&tw);
+  if (rc) return rc;
+  std::vector<int32_t> occ;
+  for (uint32_t i = 0; i < c->M; i++) if (c->p[i] != MIMO_SC_NULL) occ.push_back((int32_t)i);
+  DevBuf<int32_t> docc;
+  HIPCHK(docc.ensure(occ.size()));
+  HIPCHK(hipMemcpy(docc.p, occ.data(), sizeof(int32_t) * occ.size(), hipMemcpyHostToDevice));
+  // frames in groups so the TX scratch stays bounded (~1 GiB)
+  const uint64_t per_frame = (uint64_t)N * std::max<uint32_t>(c->pid, 1) * SL;
+  uint32_t group = (uint32_t)std::max<uint64_t>(1, (128ull << 20) / per_frame);
+  group = std::min(group, n_frames);
+  DevBuf<float2> scratch;
+  HIPCHK(scratch.ensure(per_frame * group));
+  const Qam qam = make_qam(c->qam_order);
+  const float nstd = (float)std::sqrt(0.0625 * std::pow(10.0, -(double)c->snr_db / 10.0));
+  for (uint32_t f0 = 0; f0 < n_frames; f0 += group) {
+    const uint32_t nf = std::min(group, n_frames - f0);
+    if (c->pid) {
+      TxSymArgs a{};
+      a.N = N; a.M = c->M; a.cp = c->cp_len; a.M_occ = M_occ;
+      a.dn = 1.0f / sqrtf((float)M_occ); a.gain = 0.25f;
+      a.occ_list = docc.p; a.in = nullptr; a.n_sym = c->pid; a.seed = c->seed;
+      a.frame_id0 = frame_id0 + f0; a.qam = qam;
+      a.tx_idx = d_tx_idx ? reinterpret_cast<uint8_t *>(d_tx_idx) + (size_t)f0 * N * c->pid * M_occ
+                          : nullptr;
+      a.out = scratch.p; a.tw = tw;
+      launch_tx_symbols(a, l2, nf, s);
+    }
+    MixArgs m{};
+    m.N = N; m.M = c->M; m.cp = c->cp_len; m.SL = SL; m.nac = c->num_access_codes;
+    m.pid = c->pid; m.seed = c->seed; m.frame_id0 = frame_id0 + f0; m.offset = c->offset;
+    m.identity = c->identity_channel; m.nstd = nstd; m.code_time = codes.code_time.p;
+    m.tx_data = scratch.p;
+    m.out = reinterpret_cast<float2 *>(d_out) + (size_t)f0 * N * stride;
+    m.stride = stride; m.frame_len = frame_len;
+    m.H_out = d_H ? reinterpret_cast<float2 *>(d_H) + (size_t)f0 * N * N : nullptr;
+    launch_mix(m, nf, s);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(s));
+  }
+  return MIMO_OK;
+}
+
+// ---------------- helpers ----------------
+int mimo_sctype_default(uint8_t *p, uint32_t M) {   // framing.cc:949-954
+  if (!p) return fail(MIMO_ERR_ARG, "null argument");
+  for (uint32_t i = 0; i < M; i++) p[i] = MIMO_SC_DATA;
+  return MIMO_OK;
+}
+
+int mimo_sctype_liquid(uint8_t *p, uint32_t M) {    // framing.cc:956-997
+  if (!p) return fail(MIMO_ERR_ARG, "null argument");
+  const uint32_t M2 = M / 2;
+  uint32_t G = std::max<uint32_t>(M / 10, 2);
+  const uint32_t P = (M > 34) ? 8 : 4, P2 = P / 2;
+  for (uint32_t i = 0; i < M; i++) p[i] = MIMO_SC_NULL;
+  for (uint32_t i = 1; i + G < M2; i++) {
+    const uint8_t v = (((i + P2) % P) == 0) ? MIMO_SC_PILOT : MIMO_SC_DATA;
+    p[i] = v;
+    p[M - i] = v;
+  }
+  return MIMO_OK;
+}
+
+int mimo_sctype_validate(const uint8_t *p, uint32_t M, uint32_t *a, uint32_t *b, uint32_t *c) {
+  if (!p || !a || !b || !c) return fail(MIMO_ERR_ARG, "null argument");
+  return validate_sctype(p, M, a, b, c);
+}
+
+int mimo_msequence_draw_bits(uint32_t m, uint32_t g, uint32_t a, uint32_t count, uint8_t *out) {
+  // liquid msequence_create / msequence_generate_symbol(ms,1)
+  if (!out || m < 2 || m > 31) return fail(MIMO_ERR_ARG, "bad msequence parameters");
+  uint32_t gg = g >> 1, v = 0;
+  for (uint32_t i = 0; i < m; i++) { v = (v << 1) | (a & 1u); a >>= 1; }
+  const uint32_t n = (1u << m) - 1u;
+  for (uint32_t i = 0; i < count; i++) {
+    const uint32_t b = (uint32_t)__builtin_parity(v & gg);
+    v = ((v << 1) | b) & n;
+    out[i] = (uint8_t)b;
+  }
+  return MIMO_OK;
+}
+
+float mimo_invert2(float *W, const float *G) {   // framing.cc:1344-1367 on host data
+  const float2 *g = reinterpret_cast<const float2 *>(G);
+  float2 *w = reinterpret_cast<float2 *>(W);
+  auto mul = [](float2 a, float2 b) {
+    return make_float2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
+  };
+  const float2 p0 = mul(g[0], g[3]), p1 = mul(g[1], g[2]);
+  const float2 det = make_float2(p0.x - p1.x, p0.y - p1.y);
+  const float2 di = make_float2(det.x, -det.y), ndi = make_float2(-det.x, det.y);
+  w[0] = mul(di, g[3]);
+  w[3] = mul(di, g[0]);
+  w[2] = mul(ndi, g[2]);
+  w[1] = mul(ndi, g[1]);
+  return 1.0f / (det.x * det.x + det.y * det.y);
+}
+
+int mimo_dev_alloc(void **ptr, size_t bytes) {
+  if (!ptr) return fail(MIMO_ERR_ARG, "null argument");
+  HIPCHK(hipMalloc(ptr, bytes));
+  return MIMO_OK;
+}
+int mimo_dev_free(void *ptr) {
+  HIPCHK(hipFree(ptr));
+  return MIMO_OK;
+}
+int mimo_memcpy_h2d(void *dst, const void *src, size_t bytes, void *s) {
+  HIPCHK(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, (hipStream_t)s));
+  HIPCHK(hipStreamSynchronize((hipStream_t)s));
+  return MIMO_OK;
+}
+int mimo_memcpy_d2h(void *dst, const void *src, size_t bytes, void *s) {
+  HIPCHK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, (hipStream_t)s));
+  HIPCHK(hipStreamSynchronize((hipStream_t)s));
+  return MIMO_OK;
+}
+int mimo_memset_d(void *dst, int value, size_t bytes, void *s) {
+  HIPCHK(hipMemsetAsync(dst, value, bytes, (hipStream_t)s));
+  return MIMO_OK;
+}
+int mimo_stream_sync(void *s) {
+  HIPCHK(hipStreamSynchronize((hipStream_t)s));
+  return MIMO_OK;
+}
+int mimo_device_count(int *n) {
+  if (!n) return fail(MIMO_ERR_ARG, "null argument");
+  HIPCHK(hipGetDeviceCount(n));
+  return MIMO_OK;
+}
+
+}  // extern "C"

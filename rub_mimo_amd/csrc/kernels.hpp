@@ -1,0 +1,162 @@
+// rub_mimo_amd/csrc/kernels.hpp -- launch interfaces of the gfx950 kernels (host side).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "common.hpp"
+
+namespace mimo {
+
+// Schmidl-Cox metric + plateau rule, framing.cc:591-637 (see sync_kernels.hip)
+struct ScArgs {
+  const float2 *iq;
+  uint64_t stride;          // complex samples between antenna arrays
+  uint64_t frame_len;
+  uint32_t N, M, cp;
+  double thr, band;
+  uint64_t chunk_lo, chunk_hi;
+  unsigned long long *trig; // [F], min trigger sample (UINT64_MAX = none yet)
+  uint64_t *bits;           // [F][N][bit_words] y > thr bitmask
+  uint64_t bit_words;
+};
+constexpr int kScChunk = 8192;   // output samples per chunk (multiple of 64 and of M/2)
+void launch_sc(const ScArgs &a, uint32_t n_frames, uint32_t grid_x, hipStream_t s);
+
+struct PlateauArgs {
+  const unsigned long long *trig;
+  const uint64_t *bits;
+  uint64_t bit_words;
+  uint64_t frame_len;
+  uint32_t N, SL;
+  uint64_t win_len;         // ACB + TX (framing.cc:284-285, 387-388)
+  FrameInfo *info;
+};
+void launch_plateau(const PlateauArgs &a, uint32_t n_frames, hipStream_t s);
+
+// access-code search, framing.cc:702-744 (est_kernels.hip)
+struct SearchArgs {
+  const float2 *iq;
+  uint64_t stride, frame_len;
+  uint32_t N, M, SL, n_slots;      // n_slots = N*nac + 1 (slot 0 = S0)
+  uint32_t lagc, n_lagc;           // lags per transform, transforms per slot
+  const float2 *codespec;          // [n_slots][F]
+  const float *vscale;             // [n_slots]
+  const FrameInfo *info;
+  unsigned long long *keys;        // [F][N][n_slots] packed (value, ~index)
+  const float2 *tw;
+};
+void launch_search(const SearchArgs &a, int log2F, uint32_t n_frames, hipStream_t s);
+
+// LS estimate, framing.cc:797-824 (+ training residual noise variance)
+struct LsArgs {
+  const float2 *iq;
+  uint64_t stride, frame_len;
+  uint32_t N, M, nac, n_slots;
+  const unsigned long long *keys;
+  const int8_t *s1sign;            // [N][nac][M]
+  const int32_t *occ_index;        // [M] -> j or -1
+  int keep_bias;
+  float scale;                     // dft_normalizer / float(nac) (framing.cc:821)
+  const FrameInfo *info;
+  float2 *G;                       // [F][M][N][N]
+  double *nv_part;                 // [F][N*N]
+  const float2 *tw;
+};
+void launch_ls(const LsArgs &a, int log2M, uint32_t n_frames, hipStream_t s);
+
+// per-subcarrier weights, framing.cc:826-831 -> 1344-1367 (+ NxN ZF/MMSE)
+struct WeightArgs {
+  uint32_t N, M, M_occ, nac, SL, n_slots;
+  int detector;
+  float noise_var;                 // < 0: estimate
+  double nv_norm;                  // dn^2 / (M_occ*N*N*(nac-1)), 0 if nac < 2
+  const int32_t *occ_index;
+  const float2 *G;
+  float2 *W;                       // [F][N(out)][N(rx)][M]
+  float *gain;                     // [F][M]
+  const double *nv_part;
+  const unsigned long long *keys;
+  uint64_t win_len;
+  FrameInfo *info;
+};
+void launch_weights(const WeightArgs &a, uint32_t n_frames, hipStream_t s);
+
+// replay decode, framing.cc:535-589 / 508-533 fused with square-QAM demap + EVM
+struct DecodeArgs {
+  const float2 *iq;
+  uint64_t stride, frame_len;
+  uint32_t N, M, cp, SL, M_occ;
+  int detector;
+  uint32_t siso_tx, siso_rx;
+  float dn;                        // 1/sqrtf(M_occ) (framing.cc:330)
+  const int32_t *occ_index;
+  const float2 *W;
+  const float *gain;
+  const float2 *G;
+  const FrameInfo *info;
+  uint32_t max_out;
+  float2 *out_sym;                 // [F][N][max_out][M_occ] or null
+  uint8_t *out_idx;                // same layout or null
+  int ref_mode;
+  const uint8_t *ref_idx;
+  uint64_t ref_seed, frame_id0;
+  Qam qam;
+  double *evm_part;                // [F][max_out][N][3]
+  const float2 *tw;
+};
+void launch_decode(const DecodeArgs &a, int log2M, uint32_t n_frames, hipStream_t s);
+
+struct EvmArgs {
+  uint32_t N, max_out;
+  const FrameInfo *info;
+  const double *evm_part;
+  double *evm_out;                 // [F][N][3]
+};
+void launch_evm(const EvmArgs &a, uint32_t n_frames, hipStream_t s);
+
+// code tables: S0/S1 -> IFFT*dn (framing.cc:1054-1111, 1214-1262) -> zero-pad FFT_F
+struct CodesArgs {
+  uint32_t M, N, nac, n_slots;
+  const uint8_t *p;                // [M]
+  const uint8_t *s0_bits;          // [M]
+  const uint8_t *s1_bits;          // [N][nac*M]
+  float dn_s0, dn_s1;
+  float2 *code_time;               // [n_slots][M]
+  float2 *codespec;                // [n_slots][F] (null: skip)
+  const float2 *tw;
+};
+void launch_codes(const CodesArgs &a, int log2M, int log2F, hipStream_t s);
+
+// transmitter: assemble_mimo_packet (framing.cc:210-235) for many symbols
+struct TxSymArgs {
+  uint32_t N, M, cp, M_occ;
+  float dn;                        // 1/sqrtf(M_pilot+M_data) (framing.cc:115)
+  float gain;                      // baseband gain (1 for framegen, 0.25 in tx_worker)
+  const int32_t *occ_list;         // [M_occ] -> sc
+  // symbol source: explicit (in != null) [N][n_sym][M_occ] or hashed QAM
+  const float2 *in;
+  uint32_t n_sym;
+  uint64_t seed, frame_id0;
+  Qam qam;
+  uint8_t *tx_idx;                 // hashed mode: [F][N][n_sym][M_occ] or null
+  float2 *out;                     // [F][N][n_sym][SL]
+  const float2 *tw;
+};
+void launch_tx_symbols(const TxSymArgs &a, int log2M, uint32_t n_frames, hipStream_t s);
+
+struct MixArgs {
+  uint32_t N, M, cp, SL, nac, pid;
+  uint64_t seed, frame_id0;
+  int32_t offset;                  // < 0: per-frame hashed offset
+  int identity;
+  float nstd;
+  const float2 *code_time;         // [n_slots][M]
+  const float2 *tx_data;           // [F][N][pid][SL]
+  float2 *out;                     // [F][N][stride]
+  uint64_t stride, frame_len;
+  float2 *H_out;                   // [F][N][N] or null
+};
+void launch_mix(const MixArgs &a, uint32_t n_frames, hipStream_t s);
+
+}  // namespace mimo

@@ -1,0 +1,331 @@
+// rub_mimo_amd/csrc/sync_kernels.hip -- Schmidl-Cox timing metric and plateau rule on gfx950.
+//
+// Reference: framesync::execute_sc_sync (framing.cc:591-637), a per-sample state machine:
+//   p[n] = conj(x[n-M/2]) x[n]  (wdelaycf read-before-push, lag M/2)
+//   P[n] = -sum_{M/2} p          (firfilt_crcf, taps -1)
+//   R[n] = 0.5 sum_M |x|^2       (firfilt_rrrf, taps 0.5)
+//   y[n] = |P|^2 / R^2 ;  plateau: y > 0.95 run with end - start > cp on every antenna.
+//
+// GPU form. A workgroup owns one 8192-sample chunk of one frame and walks it antenna by
+// antenna in rows of M/2 samples; thread t owns fixed columns, so x[n-M/2] is the same
+// thread's value one row up and the windowed sums are row-prefix differences:
+//   P[n] = RP_r[c] + (RT_{r-1} - RP_{r-1}[c]),  R[n] = RPz_r[c] + RTz_{r-1} + RTz_{r-2} - RPz_{r-2}[c]
+// with one block scan per row, all in fp64 (error ~1e-13, far below the decision band).
+// Samples whose fp64 metric lies within kBand of the threshold are recomputed exactly as the
+// CPU oracle does (sequential fp32 sums oldest->newest, no FMA: this file is compiled with
+// -ffp-contract=off). A sequential fp32 sum of M terms is within (M-1)u of the exact value,
+// so |y32 - y_exact| <= ~4e-4 for M <= 2048; kBand = 2e-3 keeps every plateau
+// decision, hence plateau start/end and sync_index, bit-identical to the oracle.
+//
+// Plateau runs become 64-bit words; "run of cp+2 ones ending at n" is a last-zero prefix max
+// over words; the first n where every antenna qualifies is atomicMin'ed into trig[frame].
+// Chunks beyond the current trigger exit early (results never depend on dispatch order:
+// a chunk is skipped only when a smaller trigger already exists).
+#include "kernels.hpp"
+
+#pragma clang fp contract(off)
+
+namespace mimo {
+
+constexpr int kScT = 256;
+constexpr int kBfMax = 12864;  // >= chunk + cp + 2*(M/2) + 64 for M <= 4096
+
+MIMO_DEV int64_t floordiv(int64_t a, int64_t b) {
+  int64_t q = a / b;
+  return (q * b > a) ? q - 1 : q;
+}
+
+// exact restatement of framing.cc:626-637 under the pinned liquid semantics
+__device__ __noinline__ float sc_exact(const float2 *__restrict__ x, int64_t n, int64_t M) {
+  const int64_t M2 = M / 2;
+  float Pr = 0.0f, Pi = 0.0f, R = 0.0f;
+  for (int64_t k = n - M2 + 1; k <= n; k++) {
+    float2 d = (k - M2 >= 0) ? x[k - M2] : make_float2(0.0f, 0.0f);
+    float2 v = (k >= 0) ? x[k] : make_float2(0.0f, 0.0f);
+    float pr = d.x * v.x - (-d.y) * v.y;
+    float pi = d.x * v.y + (-d.y) * v.x;
+    Pr = Pr + (-1.0f) * pr;
+    Pi = Pi + (-1.0f) * pi;
+  }
+  for (int64_t k = n - M + 1; k <= n; k++) {
+    float2 v = (k >= 0) ? x[k] : make_float2(0.0f, 0.0f);
+    float z = v.x * v.x + v.y * v.y;
+    R = R + 0.5f * z;
+  }
+  return (Pr * Pr + Pi * Pi) / (R * R);
+}
+
+// block-wide exclusive scan of three doubles; also returns the block totals
+MIMO_DEV void block_scan3(double &a, double &b, double &c, double &ta, double &tb, double &tc,
+                          double (*wsum)[kScT / 64]) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  double ia = a, ib = b, ic = c;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    double xa = __shfl_up(ia, off), xb = __shfl_up(ib, off), xc = __shfl_up(ic, off);
+    if (lane >= off) { ia += xa; ib += xb; ic += xc; }
+  }
+  if (lane == 63) { wsum[0][wv] = ia; wsum[1][wv] = ib; wsum[2][wv] = ic; }
+  __syncthreads();
+  double oa = 0.0, ob = 0.0, oc = 0.0;
+  ta = 0.0; tb = 0.0; tc = 0.0;
+#pragma unroll
+  for (int w = 0; w < kScT / 64; w++) {
+    if (w < wv) { oa += wsum[0][w]; ob += wsum[1][w]; oc += wsum[2][w]; }
+    ta += wsum[0][w]; tb += wsum[1][w]; tc += wsum[2][w];
+  }
+  __syncthreads();
+  a = oa + ia - a;
+  b = ob + ib - b;
+  c = oc + ic - c;
+}
+
+template <int CPT>
+__global__ __launch_bounds__(kScT) void sc_kernel(ScArgs a) {
+  __shared__ __attribute__((aligned(16))) uint8_t bflag[kBfMax];
+  __shared__ uint64_t words[kBfMax / 64];
+  __shared__ long long lzp[kBfMax / 64];
+  __shared__ uint64_t allcond[kScChunk / 64];
+  __shared__ double wsum[3][kScT / 64];
+  __shared__ unsigned long long s_trig, s_min;
+
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const uint32_t f = blockIdx.y;
+  const int64_t RL = a.M / 2;
+  const int64_t L = (int64_t)a.frame_len;
+  const int64_t cp = a.cp;
+
+  for (uint64_t chunk = a.chunk_lo + blockIdx.x; chunk < a.chunk_hi; chunk += gridDim.x) {
+    const int64_t c0 = (int64_t)chunk * kScChunk;
+    if (c0 >= L) break;
+    if (tid == 0) {
+      s_trig = __hip_atomic_load(&a.trig[f], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      s_min = ~0ull;
+    }
+    for (int i = tid; i < kScChunk / 64; i += kScT) allcond[i] = ~0ull;
+    __syncthreads();
+    if (s_trig < (unsigned long long)c0) break;  // an earlier trigger exists
+
+    const int64_t row_lo = floordiv(c0 - cp - 1, RL);
+    const int64_t row_hi = (c0 + kScChunk - 1) / RL;
+    const int64_t wb0 = floordiv(row_lo * RL, 64) * 64;
+    const int nbytes = (int)((row_hi + 1) * RL - wb0);
+    const int nwords = (nbytes + 63) / 64;
+    const int64_t wofs = (c0 - wb0) / 64;
+
+    for (uint32_t s = 0; s < a.N; s++) {
+      const float2 *__restrict__ x = a.iq + ((uint64_t)f * a.N + s) * a.stride;
+      for (int i = tid; i < nwords * 64; i += kScT) bflag[i] = 0;
+      __syncthreads();
+
+      float2 xprev[CPT];
+      double rpp_re[CPT], rpp_im[CPT], rpz1[CPT], rpz2[CPT];
+#pragma unroll
+      for (int q = 0; q < CPT; q++) {
+        xprev[q] = make_float2(0.0f, 0.0f);
+        rpp_re[q] = rpp_im[q] = rpz1[q] = rpz2[q] = 0.0;
+      }
+      double rtp_re = 0.0, rtp_im = 0.0, rtz1 = 0.0, rtz2 = 0.0;
+
+      for (int64_t rw = row_lo - 2; rw <= row_hi; rw++) {
+        float2 xc[CPT];
+        double lre[CPT], lim[CPT], lz[CPT];
+        double are = 0.0, aim = 0.0, az = 0.0;
+#pragma unroll
+        for (int q = 0; q < CPT; q++) {
+          const int64_t col = (int64_t)tid * CPT + q;
+          const int64_t n = rw * RL + col;
+          xc[q] = (col < RL && n >= 0 && n < L) ? x[n] : make_float2(0.0f, 0.0f);
+          const float2 d = xprev[q];
+          float pr = d.x * xc[q].x - (-d.y) * xc[q].y;  // conj(x[n-M/2]) * x[n]
+          float pi = d.x * xc[q].y + (-d.y) * xc[q].x;
+          float z = xc[q].x * xc[q].x + xc[q].y * xc[q].y;
+          are += (double)pr; aim += (double)pi; az += (double)z;
+          lre[q] = are; lim[q] = aim; lz[q] = az;
+        }
+        double tre, tim, tz;
+        double ore = are, oim = aim, oz = az;
+        block_scan3(ore, oim, oz, tre, tim, tz, wsum);
+        double rp_re[CPT], rp_im[CPT], rp_z[CPT];
+#pragma unroll
+        for (int q = 0; q < CPT; q++) {
+          rp_re[q] = ore + lre[q];
+          rp_im[q] = oim + lim[q];
+          rp_z[q] = oz + lz[q];
+        }
+        if (rw >= row_lo) {
+#pragma unroll
+          for (int q = 0; q < CPT; q++) {
+            const int64_t col = (int64_t)tid * CPT + q;
+            if (col >= RL) continue;
+            const int64_t n = rw * RL + col;
+            const double Pre = rp_re[q] + (rtp_re - rpp_re[q]);
+            const double Pim = rp_im[q] + (rtp_im - rpp_im[q]);
+            const double R = 0.5 * (rp_z[q] + rtz1 + (rtz2 - rpz2[q]));
+            bool b = false;
+            if (n >= 0 && n < L && R > 0.0) {
+              const double y = (Pre * Pre + Pim * Pim) / (R * R);
+              if (fabs(y - a.thr) <= a.band) b = (double)sc_exact(x, n, a.M) > a.thr;
+              else b = y > a.thr;
+            }
+            bflag[n - wb0] = b ? 1 : 0;
+          }
+        }
+#pragma unroll
+        for (int q = 0; q < CPT; q++) {
+          rpz2[q] = rpz1[q];
+          rpz1[q] = rp_z[q];
+          rpp_re[q] = rp_re[q];
+          rpp_im[q] = rp_im[q];
+          xprev[q] = xc[q];
+        }
+        rtz2 = rtz1; rtz1 = tz; rtp_re = tre; rtp_im = tim;
+      }
+      __syncthreads();
+      for (int w = tid; w < nwords; w += kScT) {
+        uint64_t v = 0;
+        const uint32_t *bw = reinterpret_cast<const uint32_t *>(bflag + w * 64);
+#pragma unroll
+        for (int i = 0; i < 16; i++) {
+          uint32_t q4 = bw[i];  // four 0/1 bytes
+          v |= (uint64_t)((q4 & 1u) | ((q4 >> 7) & 2u) | ((q4 >> 14) & 4u) | ((q4 >> 21) & 8u))
+               << (4 * i);
+        }
+        words[w] = v;
+      }
+      __syncthreads();
+      // publish this chunk's plateau bits for the start-of-run scan (plateau_kernel)
+      uint64_t *gbits = a.bits + ((uint64_t)f * a.N + s) * a.bit_words;
+      for (int i = tid; i < kScChunk / 64; i += kScT) {
+        const uint64_t gw = (uint64_t)c0 / 64 + i;
+        if (gw < a.bit_words) gbits[gw] = words[wofs + i];
+      }
+      // last-zero prefix max over words (wave 0)
+      if (wv == 0) {
+        const int per = (nwords + 63) / 64;
+        long long run = -1;
+        for (int k = 0; k < per; k++) {
+          const int w = lane * per + k;
+          if (w < nwords) {
+            const uint64_t inv = ~words[w];
+            const long long lzw = inv ? (long long)(wb0 + 64 * w + 63 - __clzll(inv)) : -1;
+            run = lzw > run ? lzw : run;
+            lzp[w] = run;
+          }
+        }
+        long long inc = run;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+          long long o = __shfl_up(inc, off);
+          if (lane >= off && o > inc) inc = o;
+        }
+        long long excl = __shfl_up(inc, 1);
+        if (lane == 0) excl = -1;
+        for (int k = 0; k < per; k++) {
+          const int w = lane * per + k;
+          if (w < nwords && excl > lzp[w]) lzp[w] = excl;
+        }
+      }
+      __syncthreads();
+      for (int ow = tid; ow < kScChunk / 64; ow += kScT) {
+        const int64_t wn = wofs + ow;
+        const uint64_t word = words[wn];
+        const long long prevlz = (wn > 0) ? lzp[wn - 1] : -1;
+        uint64_t cw = 0;
+        for (int i = 0; i < 64; i++) {
+          const int64_t n = c0 + 64 * ow + i;
+          const uint64_t m = ~word & ((2ull << i) - 1ull);
+          const long long lz = m ? (long long)(wb0 + 64 * wn + 63 - __clzll(m)) : prevlz;
+          if (n < L && lz <= n - cp - 2) cw |= 1ull << i;
+        }
+        allcond[ow] &= cw;
+      }
+      __syncthreads();
+    }
+    for (int ow = tid; ow < kScChunk / 64; ow += kScT) {
+      const uint64_t v = allcond[ow];
+      if (v) atomicMin(&s_min, (unsigned long long)(c0 + 64 * ow + __ffsll((long long)v) - 1));
+    }
+    __syncthreads();
+    if (tid == 0 && s_min != ~0ull) atomicMin(&a.trig[f], s_min);
+    __syncthreads();
+  }
+}
+
+// start of the run containing the trigger, per antenna; sync index; completeness
+__global__ __launch_bounds__(64) void plateau_kernel(PlateauArgs a) {
+  const uint32_t f = blockIdx.x;
+  const int lane = threadIdx.x;
+  FrameInfo &I = a.info[f];
+  const unsigned long long n = a.trig[f];
+  const int64_t L = (int64_t)a.frame_len;
+  if (n == ~0ull) {
+    if (lane == 0) {
+      I.status = 1;  // MIMO_FRAME_NO_SYNC
+      I.trigger = n;
+      I.nsp = (uint64_t)L;
+      I.n_sym = 0;
+      I.sync_index = 0;
+      I.base = 0;
+    }
+    return;
+  }
+  uint64_t sum = 0;
+  for (uint32_t s = 0; s < a.N; s++) {
+    const uint64_t *b = a.bits + ((uint64_t)f * a.N + s) * a.bit_words;
+    const int64_t w = (int64_t)(n / 64);
+    const uint64_t m = ~b[w] & ((1ull << (n % 64)) - 1ull);
+    int64_t start = 0;
+    if (m) {
+      start = w * 64 + 63 - __clzll(m) + 1;
+    } else {
+      for (int64_t wb = w - 1; wb >= 0; wb -= 64) {
+        const int64_t ww = wb - lane;
+        const uint64_t inv = (ww >= 0) ? ~b[ww] : 0ull;
+        const unsigned long long bal = __ballot(inv != 0ull);
+        if (bal) {
+          const int l = __ffsll((long long)bal) - 1;
+          const int64_t wz = wb - l;
+          start = wz * 64 + 63 - __clzll(~b[wz]) + 1;
+          break;
+        }
+      }
+    }
+    if (lane == 0) {
+      I.plateau_start[s] = (uint64_t)start;
+      I.plateau_end[s] = n;
+    }
+    sum += (uint64_t)start;
+  }
+  if (lane == 0) {
+    const uint64_t sync = sum / a.N;                 // framing.cc:618-620
+    const int64_t base = (int64_t)sync - a.SL;       // window start
+    const int64_t n_e = base + (int64_t)a.win_len;   // estimate_channel runs at this sample
+    I.trigger = n;
+    I.sync_index = sync;
+    I.base = base;
+    if (n_e < L) {
+      I.status = 0;
+      I.nsp = (uint64_t)((n_e + 1 < L) ? n_e + 2 : n_e + 1);
+    } else {
+      I.status = 2;  // MIMO_FRAME_INCOMPLETE: still saving access codes
+      I.nsp = (uint64_t)L;
+      I.n_sym = 0;
+    }
+  }
+}
+
+void launch_sc(const ScArgs &a, uint32_t n_frames, uint32_t grid_x, hipStream_t s) {
+  dim3 grid(grid_x, n_frames);
+  const uint32_t RL = a.M / 2;
+  if (RL <= 256) hipLaunchKernelGGL(sc_kernel<1>, grid, dim3(kScT), 0, s, a);
+  else if (RL <= 512) hipLaunchKernelGGL(sc_kernel<2>, grid, dim3(kScT), 0, s, a);
+  else if (RL <= 1024) hipLaunchKernelGGL(sc_kernel<4>, grid, dim3(kScT), 0, s, a);
+  else hipLaunchKernelGGL(sc_kernel<8>, grid, dim3(kScT), 0, s, a);
+}
+
+void launch_plateau(const PlateauArgs &a, uint32_t n_frames, hipStream_t s) {
+  hipLaunchKernelGGL(plateau_kernel, dim3(n_frames), dim3(64), 0, s, a);
+}
+
+}  // namespace mimo

@@ -1,0 +1,197 @@
+"""Batched device-resident receiver and GPU frame synthesiser (the bench's hot path).
+
+`Receiver.process(iq_ptr, ...)` runs the whole receive chain of include/mimo_rx.h's
+mimo_rx_process_batch over n_frames captures already in HBM: Schmidl-Cox + plateau,
+access-code search, LS estimate, detector weights, replay decode, demap and EVM, all HIP
+kernels on one stream with no host synchronisation.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass, field
+
+import numpy as np
+
+from . import _lib
+from ._lib import check, lib
+from .framing import LFSR_LARGE_LENGTH, LFSR_SMALL_0_GEN_POLY, LFSR_SMALL_LENGTH, msequence, \
+    ofdmframe_init_default_sctype, ofdmframe_validate_sctype, s1_polynomials
+
+
+@dataclass
+class RxParams:
+    M: int = 2048
+    cp_len: int = 152
+    num_streams: int = 4
+    num_access_codes: int = 20
+    pid_max: int = 1000
+    detector: int = _lib.DET_MMSE
+    noise_var: float = -1.0
+    keep_identity_bias: bool = True
+    siso_tx: int = 0
+    siso_rx: int = 0
+    plateau_threshold: float = 0.95
+    qam_order: int = 64
+    p: np.ndarray = field(default=None)
+
+    @property
+    def SL(self):
+        return self.M + self.cp_len
+
+    def sctype(self):
+        return ofdmframe_init_default_sctype(self.M) if self.p is None else \
+            np.ascontiguousarray(self.p, np.uint8)
+
+    def m_occ(self):
+        _, a, b = ofdmframe_validate_sctype(self.sctype())
+        return a + b
+
+
+def code_bits(M, N, nac):
+    """Fresh-generator msequence draws for S0 and the per-stream S1 codes."""
+    b0 = msequence(LFSR_SMALL_LENGTH, LFSR_SMALL_0_GEN_POLY, 1).draw_bits(M)
+    b1 = np.concatenate([msequence(LFSR_LARGE_LENGTH, g, 1).draw_bits(nac * M)
+                         for g in s1_polynomials(N)])
+    return b0, b1
+
+
+def _ptr(x):
+    """Device address of a torch tensor, a DeviceBuffer or an int."""
+    if x is None:
+        return None
+    if isinstance(x, int):
+        return x
+    if hasattr(x, "data_ptr"):
+        return x.data_ptr()
+    if hasattr(x, "addr"):
+        return x.addr
+    raise TypeError("expected a device pointer")
+
+
+class Receiver:
+    def __init__(self, params: RxParams, stream=None):
+        self.params = params
+        P = params
+        p = P.sctype()
+        self.p = p
+        b0, b1 = code_bits(P.M, P.num_streams, P.num_access_codes)
+        cfg = _lib.RxConfig(P.M, P.cp_len, P.num_streams, P.num_access_codes, P.pid_max,
+                            p.ctypes.data, b0.ctypes.data, b1.ctypes.data, P.detector,
+                            P.noise_var, 1 if P.keep_identity_bias else 0, P.siso_tx, P.siso_rx,
+                            P.plateau_threshold, P.qam_order)
+        h = C.c_void_p()
+        check(lib().mimo_rx_create(C.byref(cfg), stream, C.byref(h)), "mimo_rx_create")
+        self._h = h
+        self.M_occ = P.m_occ()
+        self._last = 0
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            lib().mimo_rx_destroy(self._h)
+            self._h = None
+
+    def process(self, iq, stride, frame_len, n_frames, max_out=None, out_sym=None, out_idx=None,
+                ref_mode=0, ref_idx=None, ref_seed=0, frame_id0=0, stream=None):
+        P = self.params
+        b = _lib.Batch(_ptr(iq), stride, frame_len, n_frames,
+                       P.pid_max if max_out is None else max_out, _ptr(out_sym), _ptr(out_idx),
+                       ref_mode, _ptr(ref_idx), ref_seed, frame_id0)
+        check(lib().mimo_rx_process_batch(self._h, C.byref(b), stream), "process_batch")
+        self._last = n_frames
+
+    def results(self, n_frames=None):
+        n = self._last if n_frames is None else n_frames
+        arr = (_lib.FrameResult * n)()
+        check(lib().mimo_rx_batch_results(self._h, arr, n), "batch_results")
+        N = self.params.num_streams
+        out = []
+        for r in arr:
+            out.append(dict(
+                status=r.status, n_sym=r.n_sym, trigger=r.trigger, sync_index=r.sync_index,
+                num_samples_processed=r.num_samples_processed,
+                plateau_start=list(r.plateau_start)[:N], plateau_end=list(r.plateau_end)[:N],
+                noise_var=r.noise_var, evm_num=np.array(r.evm_num[:N]),
+                evm_den=np.array(r.evm_den[:N]), errors=np.array(r.errors[:N], np.int64)))
+        return out
+
+    def corr(self, n_frames=None):
+        n = self._last if n_frames is None else n_frames
+        N, nac = self.params.num_streams, self.params.num_access_codes
+        ci = np.zeros((n, N, N * nac), np.uint32)
+        si = np.zeros((n, N), np.uint32)
+        check(lib().mimo_rx_batch_corr(self._h, ci.ctypes.data, si.ctypes.data, n), "batch_corr")
+        return ci, si
+
+    def G(self, n_frames=None):
+        n = self._last if n_frames is None else n_frames
+        P = self.params
+        G = np.zeros((n, P.M, P.num_streams, P.num_streams), np.complex64)
+        check(lib().mimo_rx_batch_G(self._h, G.ctypes.data, n), "batch_G")
+        return G
+
+    def W(self, n_frames=None):
+        n = self._last if n_frames is None else n_frames
+        P = self.params
+        W = np.zeros((n, P.M, P.num_streams, P.num_streams), np.complex64)
+        check(lib().mimo_rx_batch_W(self._h, W.ctypes.data, n), "batch_W")
+        return W
+
+    def set_timing(self, on):
+        check(lib().mimo_rx_set_timing(self._h, 1 if on else 0), "set_timing")
+
+    def stage_times(self):
+        ms = (C.c_double * _lib.NUM_STAGES)()
+        cnt = (C.c_uint32 * _lib.NUM_STAGES)()
+        check(lib().mimo_rx_get_stage_times(self._h, ms, cnt), "stage_times")
+        return {n: (ms[i], cnt[i]) for i, n in enumerate(_lib.STAGE_NAMES)}
+
+
+@dataclass
+class SynthParams:
+    M: int = 2048
+    cp_len: int = 152
+    num_streams: int = 4
+    num_access_codes: int = 20
+    pid: int = 1000
+    qam_order: int = 64
+    seed: int = 1
+    snr_db: float = 30.0
+    tail_syms: int = 3
+    identity_channel: bool = False
+    offset: int = -1
+    p: np.ndarray = field(default=None)
+
+    @property
+    def SL(self):
+        return self.M + self.cp_len
+
+    def max_frame_len(self):
+        """Uniform capture length that holds any offset u in [0, SL)."""
+        SL = self.SL
+        return SL * (2 * self.num_streams * self.num_access_codes + 2 + self.pid +
+                     self.tail_syms) + SL
+
+
+class Synthesizer:
+    """GPU synthetic captures in the reference tx_worker layout (mimo_synth_frames)."""
+
+    def __init__(self, params: SynthParams):
+        self.params = params
+        P = params
+        self.p = ofdmframe_init_default_sctype(P.M) if P.p is None else \
+            np.ascontiguousarray(P.p, np.uint8)
+        self.b0, self.b1 = code_bits(P.M, P.num_streams, P.num_access_codes)
+        self._cfg = _lib.SynthConfig(P.M, P.cp_len, P.num_streams, P.num_access_codes, P.pid,
+                                     P.qam_order, P.seed, P.snr_db, P.tail_syms,
+                                     1 if P.identity_channel else 0, P.offset,
+                                     self.p.ctypes.data, self.b0.ctypes.data, self.b1.ctypes.data)
+
+    def frame_len(self, frame_id):
+        v = C.c_uint64()
+        check(lib().mimo_synth_frame_len(C.byref(self._cfg), frame_id, C.byref(v)), "frame_len")
+        return v.value
+
+    def generate(self, out, stride, frame_len, n_frames, frame_id0=0, tx_idx=None, H=None,
+                 stream=None):
+        check(lib().mimo_synth_frames(C.byref(self._cfg), frame_id0, n_frames, _ptr(out), stride,
+                                      frame_len, _ptr(tx_idx), _ptr(H), stream), "synth_frames")
