@@ -105,6 +105,7 @@ def main():
     t1 = time.perf_counter()
     rx.set_timing(False)
     stages = rx.stage_times()
+    n_exact = rx.sc_exact_count()
     elapsed = t1 - t0
     res = rx.results(F)
     ok = sum(1 for r in res if r["status"] == _lib.FRAME_OK)
@@ -186,6 +187,7 @@ def main():
         "pipeline_hbm_gbs": bytes_alg / elapsed / 1e9,
         "stages_ms_per_step": {k: v[0] / max(args.steps, 1) for k, v in stages.items()},
         "frames_ok": int(ok), "frames": int(F * world),
+        "sc_exact_recomputes_per_step": n_exact / max(args.steps + args.warmup, 1),
         "evm_db": 10 * np.log10(evm_num / evm_den) if evm_den > 0 else None,
         "symbol_errors_last_step": int(errors),
     }

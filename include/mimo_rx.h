@@ -152,6 +152,9 @@ int mimo_rx_batch_W(mimo_rx *h, float *W, uint32_t n_frames);
 int mimo_rx_set_timing(mimo_rx *h, int enable);
 /* sums of stage durations (ms) and launch counts since the last call; synchronises */
 int mimo_rx_get_stage_times(mimo_rx *h, double *ms, uint32_t *launches);
+/* S&C samples whose fp64 metric fell within the decision band and were recomputed with the
+ * oracle's exact fp32 order, since the last call (diagnostic; synchronises) */
+int mimo_rx_get_sc_exact_count(mimo_rx *h, uint64_t *out);
 
 /* ---------------- transmitter: framegen (framing.h:42-103) ---------------- */
 typedef struct mimo_tx mimo_tx;

@@ -151,18 +151,27 @@ __global__ __launch_bounds__(T) void decode_kernel(DecodeArgs a) {
   }
 }
 
-__global__ void evm_kernel(EvmArgs a) {
-  const uint32_t f = blockIdx.x, t = threadIdx.x;
-  if (t >= a.N) return;
+// per-frame EVM / symbol-error totals: fixed-order strided partial sums + LDS tree, so the
+// result is bitwise reproducible run to run
+__global__ __launch_bounds__(256) void evm_kernel(EvmArgs a) {
+  __shared__ double red[256];
+  const uint32_t f = blockIdx.x, tid = threadIdx.x;
   const FrameInfo &I = a.info[f];
   const uint32_t n_out = (I.status == 0) ? min(I.n_sym, a.max_out) : 0u;
-  double v0 = 0.0, v1 = 0.0, v2 = 0.0;
-  for (uint32_t s = 0; s < n_out; s++) {
-    const double *ep = a.evm_part + (((uint64_t)f * a.max_out + s) * a.N + t) * 3;
-    v0 += ep[0]; v1 += ep[1]; v2 += ep[2];
+  const uint32_t per = a.N * 3;
+  for (uint32_t c = 0; c < per; c++) {
+    double v = 0.0;
+    for (uint32_t s = tid; s < n_out; s += 256)
+      v += a.evm_part[((uint64_t)f * a.max_out + s) * per + c];
+    red[tid] = v;
+    __syncthreads();
+    for (uint32_t w = 128; w > 0; w >>= 1) {
+      if (tid < w) red[tid] += red[tid + w];
+      __syncthreads();
+    }
+    if (tid == 0) a.evm_out[(uint64_t)f * per + c] = red[0];
+    __syncthreads();
   }
-  double *o = a.evm_out + ((uint64_t)f * a.N + t) * 3;
-  o[0] = v0; o[1] = v1; o[2] = v2;
 }
 
 // ------------------------------------------------------------------------------------
@@ -202,7 +211,7 @@ void launch_decode(const DecodeArgs &a, int log2M, uint32_t n_frames, hipStream_
 }
 
 void launch_evm(const EvmArgs &a, uint32_t n_frames, hipStream_t s) {
-  hipLaunchKernelGGL(evm_kernel, dim3(n_frames), dim3(64), 0, s, a);
+  hipLaunchKernelGGL(evm_kernel, dim3(n_frames), dim3(256), 0, s, a);
 }
 
 }  // namespace mimo

@@ -216,6 +216,7 @@ struct mimo_rx {
   DevBuf<float2> G, W;
   DevBuf<float> gain;
   DevBuf<double> nvp, evm_part, evm_out;
+  DevBuf<unsigned long long> n_exact;   // S&C exact fp32 recomputes (diagnostic)
   uint32_t last_frames = 0, last_max_out = 0;
   uint64_t last_words = 0;
   // streaming state (facade)
@@ -298,6 +299,11 @@ int run_sync(mimo_rx *h, const float2 *iq, uint64_t stride, uint32_t F, uint64_t
     a.thr = h->thr; a.band = 2e-3;
     a.chunk_lo = chunk_lo; a.chunk_hi = nchunks;
     a.trig = h->trig.p; a.bits = h->bits.p; a.bit_words = h->cap_words;
+    if (!h->n_exact.p) {
+      HIPCHK(h->n_exact.ensure(1));
+      HIPCHK(hipMemsetAsync(h->n_exact.p, 0, sizeof(unsigned long long), s));
+    }
+    a.n_exact = h->n_exact.p;
     const uint32_t grid_x = (uint32_t)std::min<uint64_t>(nchunks - chunk_lo, 64);
     hipEvent_t e = h->timer.begin(s);
     launch_sc(a, F, grid_x, s);
@@ -828,6 +834,19 @@ int mimo_rx_batch_W(mimo_rx *h, float *W, uint32_t F) {
 int mimo_rx_set_timing(mimo_rx *h, int enable) {
   if (!h) return fail(MIMO_ERR_ARG, "null handle");
   h->timer.on = enable != 0;
+  return MIMO_OK;
+}
+
+int mimo_rx_get_sc_exact_count(mimo_rx *h, uint64_t *out) {
+  if (!h || !out) return fail(MIMO_ERR_ARG, "null argument");
+  *out = 0;
+  if (!h->n_exact.p) return MIMO_OK;
+  unsigned long long v = 0;
+  HIPCHK(hipStreamSynchronize(h->stream));
+  HIPCHK(hipDeviceSynchronize());
+  HIPCHK(hipMemcpy(&v, h->n_exact.p, sizeof(v), hipMemcpyDeviceToHost));
+  HIPCHK(hipMemset(h->n_exact.p, 0, sizeof(v)));
+  *out = v;
   return MIMO_OK;
 }
 

@@ -19,6 +19,7 @@ struct ScArgs {
   unsigned long long *trig; // [F], min trigger sample (UINT64_MAX = none yet)
   uint64_t *bits;           // [F][N][bit_words] y > thr bitmask
   uint64_t bit_words;
+  unsigned long long *n_exact;  // count of exact fp32 recomputes (null: not counted)
 };
 constexpr int kScChunk = 8192;   // output samples per chunk (multiple of 64 and of M/2)
 void launch_sc(const ScArgs &a, uint32_t n_frames, uint32_t grid_x, hipStream_t s);

@@ -29,13 +29,35 @@ namespace mimo {
 
 constexpr int kScT = 256;
 constexpr int kBfMax = 12864;  // >= chunk + cp + 2*(M/2) + 64 for M <= 4096
+constexpr int kAmbMax = 128;   // near-threshold samples resolved cooperatively per row
 
 MIMO_DEV int64_t floordiv(int64_t a, int64_t b) {
   int64_t q = a / b;
   return (q * b > a) ? q - 1 : q;
 }
 
-// exact restatement of framing.cc:626-637 under the pinned liquid semantics
+// exact restatement of framing.cc:626-637 under the pinned liquid semantics, on the M
+// samples s[i] = x[n - M + 1 + i] staged in LDS by the whole workgroup (one lane sums)
+MIMO_DEV float sc_exact_lds(const float2 *s, int M) {
+  // the three accumulation chains are interleaved for latency, each in its own order
+  const int M2 = M / 2;
+  float Pr = 0.0f, Pi = 0.0f, R = 0.0f;
+  for (int j = 0; j < M2; j++) {       // P: k = n - M/2 + 1 + j, oldest -> newest
+    const float2 d = s[j], v = s[M2 + j];
+    float pr = d.x * v.x - (-d.y) * v.y;
+    float pi = d.x * v.y + (-d.y) * v.x;
+    Pr = Pr + (-1.0f) * pr;
+    Pi = Pi + (-1.0f) * pi;
+    const float2 u0 = s[2 * j], u1 = s[2 * j + 1];   // R: i = 2j, 2j+1, oldest -> newest
+    float z0 = u0.x * u0.x + u0.y * u0.y;
+    R = R + 0.5f * z0;
+    float z1 = u1.x * u1.x + u1.y * u1.y;
+    R = R + 0.5f * z1;
+  }
+  return (Pr * Pr + Pi * Pi) / (R * R);
+}
+
+// the same from global memory, one lane alone (only if a row overflows the LDS list)
 __device__ __noinline__ float sc_exact(const float2 *__restrict__ x, int64_t n, int64_t M) {
   const int64_t M2 = M / 2;
   float Pr = 0.0f, Pi = 0.0f, R = 0.0f;
@@ -88,8 +110,14 @@ __global__ __launch_bounds__(kScT) void sc_kernel(ScArgs a) {
   __shared__ uint64_t allcond[kScChunk / 64];
   __shared__ double wsum[3][kScT / 64];
   __shared__ unsigned long long s_trig, s_min;
+  __shared__ float2 stage[6144];          // union of the M-sample windows of a row's
+                                           // near-threshold samples (<= M + M/2)
+  __shared__ long long amb_n[kAmbMax];     // near-threshold samples of the current row
+  __shared__ int s_namb;
+  __shared__ unsigned long long s_nmin, s_nmax;
 
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  if (tid == 0) { s_namb = 0; s_nmin = ~0ull; s_nmax = 0ull; }
   const uint32_t f = blockIdx.y;
   const int64_t RL = a.M / 2;
   const int64_t L = (int64_t)a.frame_len;
@@ -127,15 +155,28 @@ __global__ __launch_bounds__(kScT) void sc_kernel(ScArgs a) {
       }
       double rtp_re = 0.0, rtp_im = 0.0, rtz1 = 0.0, rtz2 = 0.0;
 
+      // software pipeline: the next row's samples are in flight while this row scans
+      float2 xnext[CPT];
+#pragma unroll
+      for (int q = 0; q < CPT; q++) {
+        const int64_t col = (int64_t)tid * CPT + q;
+        const int64_t n = (row_lo - 2) * RL + col;
+        xnext[q] = (col < RL && n >= 0 && n < L) ? x[n] : make_float2(0.0f, 0.0f);
+      }
       for (int64_t rw = row_lo - 2; rw <= row_hi; rw++) {
         float2 xc[CPT];
         double lre[CPT], lim[CPT], lz[CPT];
         double are = 0.0, aim = 0.0, az = 0.0;
 #pragma unroll
         for (int q = 0; q < CPT; q++) {
+          xc[q] = xnext[q];
           const int64_t col = (int64_t)tid * CPT + q;
-          const int64_t n = rw * RL + col;
-          xc[q] = (col < RL && n >= 0 && n < L) ? x[n] : make_float2(0.0f, 0.0f);
+          const int64_t n1 = (rw + 1) * RL + col;
+          xnext[q] = (rw < row_hi && col < RL && n1 >= 0 && n1 < L) ? x[n1]
+                                                                     : make_float2(0.0f, 0.0f);
+        }
+#pragma unroll
+        for (int q = 0; q < CPT; q++) {
           const float2 d = xprev[q];
           float pr = d.x * xc[q].x - (-d.y) * xc[q].y;  // conj(x[n-M/2]) * x[n]
           float pi = d.x * xc[q].y + (-d.y) * xc[q].x;
@@ -165,12 +206,43 @@ __global__ __launch_bounds__(kScT) void sc_kernel(ScArgs a) {
             bool b = false;
             if (n >= 0 && n < L && R > 0.0) {
               const double y = (Pre * Pre + Pim * Pim) / (R * R);
-              if (fabs(y - a.thr) <= a.band) b = (double)sc_exact(x, n, a.M) > a.thr;
-              else b = y > a.thr;
+              if (fabs(y - a.thr) <= a.band) {
+                // near the threshold: defer to the exact fp32 recompute below
+                const int slot = atomicAdd(&s_namb, 1);
+                if (slot < kAmbMax) {
+                  amb_n[slot] = n;
+                  atomicMin(&s_nmin, (unsigned long long)n);
+                  atomicMax(&s_nmax, (unsigned long long)n);
+                } else {
+                  b = (double)sc_exact(x, n, a.M) > a.thr;   // overflow: lane alone
+                }
+              } else {
+                b = y > a.thr;
+              }
             }
             bflag[n - wb0] = b ? 1 : 0;
           }
         }
+        __syncthreads();
+        const int namb = s_namb < kAmbMax ? s_namb : kAmbMax;
+        if (namb > 0) {   // block-uniform: stage the union of the windows, one lane each
+          const int64_t nmin = (int64_t)s_nmin;
+          const int64_t w0 = nmin - (int64_t)a.M + 1;
+          const int W = (int)((int64_t)s_nmax - nmin) + (int)a.M;
+          for (int i = tid; i < W; i += kScT) {
+            const int64_t k = w0 + i;
+            stage[i] = (k >= 0 && k < L) ? x[k] : make_float2(0.0f, 0.0f);
+          }
+          __syncthreads();
+          if (tid < namb) {
+            const int64_t n = amb_n[tid];
+            const float y32 = sc_exact_lds(stage + (n - nmin), (int)a.M);
+            bflag[n - wb0] = ((double)y32 > a.thr) ? 1 : 0;
+          }
+          if (tid == 0 && a.n_exact) atomicAdd(a.n_exact, (unsigned long long)namb);
+          __syncthreads();
+        }
+        if (tid == 0) { s_namb = 0; s_nmin = ~0ull; s_nmax = 0ull; }
 #pragma unroll
         for (int q = 0; q < CPT; q++) {
           rpz2[q] = rpz1[q];

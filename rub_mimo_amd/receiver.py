@@ -139,6 +139,11 @@ class Receiver:
     def set_timing(self, on):
         check(lib().mimo_rx_set_timing(self._h, 1 if on else 0), "set_timing")
 
+    def sc_exact_count(self):
+        v = C.c_uint64()
+        check(lib().mimo_rx_get_sc_exact_count(self._h, C.byref(v)), "sc_exact_count")
+        return v.value
+
     def stage_times(self):
         ms = (C.c_double * _lib.NUM_STAGES)()
         cnt = (C.c_uint32 * _lib.NUM_STAGES)()

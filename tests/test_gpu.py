@@ -320,7 +320,7 @@ def test_c4_batched_full_size_properties():
     M, cp, N, nac, pid, qam, F = 4096, 304, 8, 20, 1000, 256, 2
     S = Synthesizer(SynthParams(M=M, cp_len=cp, num_streams=N, num_access_codes=nac, pid=pid,
                                 qam_order=qam, seed=51, snr_db=35.0))
-    L = S.max_frame_len()
+    L = S.params.max_frame_len()
     out = _lib.DeviceBuffer(F * N * L * 8)
     S.generate(out, L, L, F)
     rxo = Receiver(RxParams(M=M, cp_len=cp, num_streams=N, num_access_codes=nac, pid_max=pid,
