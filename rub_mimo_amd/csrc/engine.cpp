@@ -208,10 +208,10 @@ struct mimo_rx {
   DevBuf<int32_t> occ;
   // workspace
   uint32_t cap_frames = 0;
-  uint64_t cap_words = 0;
+  uint64_t cap_chunks = 0;
   uint64_t cap_evm = 0;
   DevBuf<unsigned long long> trig, keys;
-  DevBuf<uint64_t> bits;
+  DevBuf<ScRecord> rec;
   DevBuf<FrameInfo> info;
   DevBuf<float2> G, W;
   DevBuf<float> gain;
@@ -247,10 +247,10 @@ struct mimo_tx {
 
 namespace {
 
-// Per-frame arrays grow with F; the plateau bitmask grows with F * words. A growing
-// single-frame bitmask (streaming capture) keeps its earlier words: chunks already final
-// are never recomputed, and trig[] is untouched when only the capture length grows.
-int ensure_workspace(mimo_rx *h, uint32_t F, uint64_t words, uint64_t evm_entries) {
+// Per-frame arrays grow with F; the per-chunk trigger records grow with F * chunks. A
+// growing single-frame record array (streaming capture) keeps its earlier records: chunks
+// already final are never recomputed, and trig[] is untouched when only the capture grows.
+int ensure_workspace(mimo_rx *h, uint32_t F, uint64_t chunks, uint64_t evm_entries) {
   if (F > h->cap_frames) {
     const uint32_t nf = F;
     HIPCHK(h->trig.ensure(nf));
@@ -262,20 +262,18 @@ int ensure_workspace(mimo_rx *h, uint32_t F, uint64_t words, uint64_t evm_entrie
     HIPCHK(h->nvp.ensure((size_t)nf * h->N * h->N));
     HIPCHK(h->evm_out.ensure((size_t)nf * h->N * 3));
     h->cap_frames = nf;
-    HIPCHK(h->bits.ensure((size_t)nf * h->N * h->cap_words));
+    HIPCHK(h->rec.ensure((size_t)nf * h->cap_chunks));
   }
-  if (words > h->cap_words) {
-    const uint64_t nw = std::max<uint64_t>(words, h->cap_words * 2);
-    uint64_t *np = nullptr;
-    HIPCHK(hipMalloc(&np, sizeof(uint64_t) * (size_t)h->cap_frames * h->N * nw));
-    if (h->bits.p && h->cap_words && h->cap_frames == 1) {
-      HIPCHK(hipMemcpy2D(np, sizeof(uint64_t) * nw, h->bits.p, sizeof(uint64_t) * h->cap_words,
-                         sizeof(uint64_t) * h->cap_words, h->N, hipMemcpyDeviceToDevice));
-    }
-    h->bits.release();
-    h->bits.p = np;
-    h->bits.n = (size_t)h->cap_frames * h->N * nw;
-    h->cap_words = nw;
+  if (chunks > h->cap_chunks) {
+    const uint64_t nc = std::max<uint64_t>(chunks, h->cap_chunks * 2);
+    ScRecord *np = nullptr;
+    HIPCHK(hipMalloc(&np, sizeof(ScRecord) * (size_t)h->cap_frames * nc));
+    if (h->rec.p && h->cap_chunks && h->cap_frames == 1)
+      HIPCHK(hipMemcpy(np, h->rec.p, sizeof(ScRecord) * h->cap_chunks, hipMemcpyDeviceToDevice));
+    h->rec.release();
+    h->rec.p = np;
+    h->rec.n = (size_t)h->cap_frames * nc;
+    h->cap_chunks = nc;
   }
   if (evm_entries > h->cap_evm) {
     HIPCHK(h->evm_part.ensure(evm_entries));
@@ -287,18 +285,17 @@ int ensure_workspace(mimo_rx *h, uint32_t F, uint64_t words, uint64_t evm_entrie
 // S&C + plateau over chunks [chunk_lo, end) of every frame
 int run_sync(mimo_rx *h, const float2 *iq, uint64_t stride, uint32_t F, uint64_t frame_len,
              uint64_t chunk_lo, bool reset_trig, hipStream_t s) {
-  const uint64_t words = (frame_len + 63) / 64;
-  int rc = ensure_workspace(h, F, words, 0);
+  const uint64_t nchunks = (frame_len + kScChunk - 1) / kScChunk;
+  int rc = ensure_workspace(h, F, nchunks, 0);
   if (rc) return rc;
   if (reset_trig) HIPCHK(hipMemsetAsync(h->trig.p, 0xFF, sizeof(unsigned long long) * F, s));
-  const uint64_t nchunks = (frame_len + kScChunk - 1) / kScChunk;
   if (chunk_lo < nchunks) {
     ScArgs a{};
     a.iq = iq; a.stride = stride; a.frame_len = frame_len;
     a.N = h->N; a.M = h->M; a.cp = h->cp;
     a.thr = h->thr; a.band = 2e-3;
     a.chunk_lo = chunk_lo; a.chunk_hi = nchunks;
-    a.trig = h->trig.p; a.bits = h->bits.p; a.bit_words = h->cap_words;
+    a.trig = h->trig.p; a.rec = h->rec.p; a.rec_stride = h->cap_chunks;
     if (!h->n_exact.p) {
       HIPCHK(h->n_exact.ensure(1));
       HIPCHK(hipMemsetAsync(h->n_exact.p, 0, sizeof(unsigned long long), s));
@@ -310,8 +307,9 @@ int run_sync(mimo_rx *h, const float2 *iq, uint64_t stride, uint32_t F, uint64_t
     h->timer.end(0, e, s);
   }
   PlateauArgs pa{};
-  pa.trig = h->trig.p; pa.bits = h->bits.p; pa.bit_words = h->cap_words;
-  pa.frame_len = frame_len; pa.N = h->N; pa.SL = h->SL; pa.win_len = h->win_len;
+  pa.trig = h->trig.p; pa.rec = h->rec.p; pa.rec_stride = h->cap_chunks;
+  pa.iq = iq; pa.stride = stride; pa.frame_len = frame_len;
+  pa.N = h->N; pa.M = h->M; pa.SL = h->SL; pa.thr = h->thr; pa.win_len = h->win_len;
   pa.info = h->info.p;
   hipEvent_t e = h->timer.begin(s);
   launch_plateau(pa, F, s);
@@ -587,7 +585,7 @@ int mimo_rx_execute(mimo_rx *h, const float *const *iq, uint32_t n_ant, uint64_t
   h->total = old_total + n;
   if (h->state == MIMO_STATE_SEEK_PLATEAU) {
     if (old_total == 0) {
-      rc = ensure_workspace(h, 1, (h->total + 63) / 64, 0);
+      rc = ensure_workspace(h, 1, (h->total + kScChunk - 1) / kScChunk, 0);
       if (rc) return rc;
       HIPCHK(hipMemsetAsync(h->trig.p, 0xFF, sizeof(unsigned long long), h->stream));
     }
@@ -769,7 +767,7 @@ int mimo_rx_process_batch(mimo_rx *h, const mimo_batch *b, void *hip_stream) {
   if (rc) return rc;
   h->last_frames = b->n_frames;
   h->last_max_out = b->max_out_syms;
-  h->last_words = (b->frame_len + 63) / 64;
+  h->last_words = (b->frame_len + kScChunk - 1) / kScChunk;
   return MIMO_OK;
 }
 

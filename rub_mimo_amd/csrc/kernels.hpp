@@ -9,6 +9,13 @@
 namespace mimo {
 
 // Schmidl-Cox metric + plateau rule, framing.cc:591-637 (see sync_kernels.hip)
+struct ScRecord {             // a chunk's trigger candidate and the run starts it saw
+  unsigned long long n_cand;
+  unsigned long long start[kMaxStreams];
+  long long pos0;             // first sample the chunk computed
+  uint32_t found;             // bit s: start[s] is final (a zero bit inside the chunk)
+  uint32_t pad;
+};
 struct ScArgs {
   const float2 *iq;
   uint64_t stride;          // complex samples between antenna arrays
@@ -17,8 +24,8 @@ struct ScArgs {
   double thr, band;
   uint64_t chunk_lo, chunk_hi;
   unsigned long long *trig; // [F], min trigger sample (UINT64_MAX = none yet)
-  uint64_t *bits;           // [F][N][bit_words] y > thr bitmask
-  uint64_t bit_words;
+  ScRecord *rec;            // [F][rec_stride] per-chunk candidates
+  uint64_t rec_stride;
   unsigned long long *n_exact;  // count of exact fp32 recomputes (null: not counted)
 };
 constexpr int kScChunk = 8192;   // output samples per chunk (multiple of 64 and of M/2)
@@ -26,10 +33,12 @@ void launch_sc(const ScArgs &a, uint32_t n_frames, uint32_t grid_x, hipStream_t 
 
 struct PlateauArgs {
   const unsigned long long *trig;
-  const uint64_t *bits;
-  uint64_t bit_words;
-  uint64_t frame_len;
-  uint32_t N, SL;
+  const ScRecord *rec;
+  uint64_t rec_stride;
+  const float2 *iq;
+  uint64_t stride, frame_len;
+  uint32_t N, M, SL;
+  double thr;
   uint64_t win_len;         // ACB + TX (framing.cc:284-285, 387-388)
   FrameInfo *info;
 };

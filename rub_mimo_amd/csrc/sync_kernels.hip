@@ -4,7 +4,8 @@
 //   p[n] = conj(x[n-M/2]) x[n]  (wdelaycf read-before-push, lag M/2)
 //   P[n] = -sum_{M/2} p          (firfilt_crcf, taps -1)
 //   R[n] = 0.5 sum_M |x|^2       (firfilt_rrrf, taps 0.5)
-//   y[n] = |P|^2 / R^2 ;  plateau: y > 0.95 run with end - start > cp on every antenna.
+//   y[n] = |P|^2 / R^2 ;  plateau: y > 0.95 run with end - start > cp on every antenna;
+//   sync_index = floor(sum of run starts / N).
 //
 // GPU form. A workgroup owns one 8192-sample chunk of one frame and walks it antenna by
 // antenna in rows of M/2 samples; thread t owns fixed columns, so x[n-M/2] is the same
@@ -13,14 +14,19 @@
 // with one block scan per row, all in fp64 (error ~1e-13, far below the decision band).
 // Samples whose fp64 metric lies within kBand of the threshold are recomputed exactly as the
 // CPU oracle does (sequential fp32 sums oldest->newest, no FMA: this file is compiled with
-// -ffp-contract=off). A sequential fp32 sum of M terms is within (M-1)u of the exact value,
-// so |y32 - y_exact| <= ~4e-4 for M <= 2048; kBand = 2e-3 keeps every plateau
-// decision, hence plateau start/end and sync_index, bit-identical to the oracle.
+// -ffp-contract=off), one lane per sample over an LDS-staged window. A sequential fp32 sum of
+// M terms is within (M-1)u of the exact value, so |y32 - y_exact| <= ~4e-4 for M <= 2048
+// (DESIGN.md); a 2e-3 band keeps every plateau decision -- hence plateau start/end and
+// sync_index -- bit-identical to the oracle.
 //
 // Plateau runs become 64-bit words; "run of cp+2 ones ending at n" is a last-zero prefix max
-// over words; the first n where every antenna qualifies is atomicMin'ed into trig[frame].
-// Chunks beyond the current trigger exit early (results never depend on dispatch order:
-// a chunk is skipped only when a smaller trigger already exists).
+// over words. Antennas are processed in order and the chunk stops as soon as no sample can
+// still qualify on every antenna (noise and data regions cost one antenna, not N). The first
+// qualifying n is atomicMin'ed into trig[frame]; the chunk also records each antenna's run
+// start from its LDS bits, which plateau_kernel completes with an exact backward scan only
+// when a run began before the chunk's halo. Chunks beyond the current trigger exit early;
+// results never depend on dispatch order (a chunk is skipped only when a smaller trigger
+// already exists, and the kept candidate is the global minimum).
 #include "kernels.hpp"
 
 #pragma clang fp contract(off)
@@ -29,6 +35,7 @@ namespace mimo {
 
 constexpr int kScT = 256;
 constexpr int kBfMax = 12864;  // >= chunk + cp + 2*(M/2) + 64 for M <= 4096
+constexpr int kBfW = kBfMax / 64;
 constexpr int kAmbMax = 128;   // near-threshold samples resolved cooperatively per row
 
 MIMO_DEV int64_t floordiv(int64_t a, int64_t b) {
@@ -37,18 +44,18 @@ MIMO_DEV int64_t floordiv(int64_t a, int64_t b) {
 }
 
 // exact restatement of framing.cc:626-637 under the pinned liquid semantics, on the M
-// samples s[i] = x[n - M + 1 + i] staged in LDS by the whole workgroup (one lane sums)
+// samples s[i] = x[n - M + 1 + i] (LDS). The three accumulation chains are interleaved for
+// latency; each keeps its own oldest -> newest order.
 MIMO_DEV float sc_exact_lds(const float2 *s, int M) {
-  // the three accumulation chains are interleaved for latency, each in its own order
   const int M2 = M / 2;
   float Pr = 0.0f, Pi = 0.0f, R = 0.0f;
-  for (int j = 0; j < M2; j++) {       // P: k = n - M/2 + 1 + j, oldest -> newest
+  for (int j = 0; j < M2; j++) {       // P: k = n - M/2 + 1 + j
     const float2 d = s[j], v = s[M2 + j];
     float pr = d.x * v.x - (-d.y) * v.y;
     float pi = d.x * v.y + (-d.y) * v.x;
     Pr = Pr + (-1.0f) * pr;
     Pi = Pi + (-1.0f) * pi;
-    const float2 u0 = s[2 * j], u1 = s[2 * j + 1];   // R: i = 2j, 2j+1, oldest -> newest
+    const float2 u0 = s[2 * j], u1 = s[2 * j + 1];   // R: i = 2j, 2j+1
     float z0 = u0.x * u0.x + u0.y * u0.y;
     R = R + 0.5f * z0;
     float z1 = u1.x * u1.x + u1.y * u1.y;
@@ -57,7 +64,7 @@ MIMO_DEV float sc_exact_lds(const float2 *s, int M) {
   return (Pr * Pr + Pi * Pi) / (R * R);
 }
 
-// the same from global memory, one lane alone (only if a row overflows the LDS list)
+// the same straight from global memory (one lane; overflow rows and the rare backward scan)
 __device__ __noinline__ float sc_exact(const float2 *__restrict__ x, int64_t n, int64_t M) {
   const int64_t M2 = M / 2;
   float Pr = 0.0f, Pi = 0.0f, R = 0.0f;
@@ -77,7 +84,8 @@ __device__ __noinline__ float sc_exact(const float2 *__restrict__ x, int64_t n, 
   return (Pr * Pr + Pi * Pi) / (R * R);
 }
 
-// block-wide exclusive scan of three doubles; also returns the block totals
+// block-wide exclusive scan of three doubles plus block totals; wsum is double-buffered by
+// the caller (alternate rows), so one barrier per scan suffices
 MIMO_DEV void block_scan3(double &a, double &b, double &c, double &ta, double &tb, double &tc,
                           double (*wsum)[kScT / 64]) {
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -96,7 +104,6 @@ MIMO_DEV void block_scan3(double &a, double &b, double &c, double &ta, double &t
     if (w < wv) { oa += wsum[0][w]; ob += wsum[1][w]; oc += wsum[2][w]; }
     ta += wsum[0][w]; tb += wsum[1][w]; tc += wsum[2][w];
   }
-  __syncthreads();
   a = oa + ia - a;
   b = ob + ib - b;
   c = oc + ic - c;
@@ -105,14 +112,13 @@ MIMO_DEV void block_scan3(double &a, double &b, double &c, double &ta, double &t
 template <int CPT>
 __global__ __launch_bounds__(kScT) void sc_kernel(ScArgs a) {
   __shared__ __attribute__((aligned(16))) uint8_t bflag[kBfMax];
-  __shared__ uint64_t words[kBfMax / 64];
-  __shared__ long long lzp[kBfMax / 64];
+  __shared__ uint64_t words[kMaxStreams][kBfW];
+  __shared__ long long lzp[kBfW];
   __shared__ uint64_t allcond[kScChunk / 64];
-  __shared__ double wsum[3][kScT / 64];
+  __shared__ double wsum[2][3][kScT / 64];
   __shared__ unsigned long long s_trig, s_min;
-  __shared__ float2 stage[6144];          // union of the M-sample windows of a row's
-                                           // near-threshold samples (<= M + M/2)
-  __shared__ long long amb_n[kAmbMax];     // near-threshold samples of the current row
+  __shared__ float2 stage[768 * CPT];      // union of a row's near-threshold windows (1.5 M)
+  __shared__ long long amb_n[kAmbMax];
   __shared__ int s_namb;
   __shared__ unsigned long long s_nmin, s_nmax;
 
@@ -136,15 +142,16 @@ __global__ __launch_bounds__(kScT) void sc_kernel(ScArgs a) {
 
     const int64_t row_lo = floordiv(c0 - cp - 1, RL);
     const int64_t row_hi = (c0 + kScChunk - 1) / RL;
-    const int64_t wb0 = floordiv(row_lo * RL, 64) * 64;
+    const int64_t pos0 = row_lo * RL;               // first computed sample
+    const int64_t wb0 = floordiv(pos0, 64) * 64;
     const int nbytes = (int)((row_hi + 1) * RL - wb0);
     const int nwords = (nbytes + 63) / 64;
     const int64_t wofs = (c0 - wb0) / 64;
+    int any = 1;
 
-    for (uint32_t s = 0; s < a.N; s++) {
+    for (uint32_t s = 0; s < a.N && any; s++) {
       const float2 *__restrict__ x = a.iq + ((uint64_t)f * a.N + s) * a.stride;
       for (int i = tid; i < nwords * 64; i += kScT) bflag[i] = 0;
-      __syncthreads();
 
       float2 xprev[CPT];
       double rpp_re[CPT], rpp_im[CPT], rpz1[CPT], rpz2[CPT];
@@ -154,7 +161,6 @@ __global__ __launch_bounds__(kScT) void sc_kernel(ScArgs a) {
         rpp_re[q] = rpp_im[q] = rpz1[q] = rpz2[q] = 0.0;
       }
       double rtp_re = 0.0, rtp_im = 0.0, rtz1 = 0.0, rtz2 = 0.0;
-
       // software pipeline: the next row's samples are in flight while this row scans
       float2 xnext[CPT];
 #pragma unroll
@@ -163,6 +169,8 @@ __global__ __launch_bounds__(kScT) void sc_kernel(ScArgs a) {
         const int64_t n = (row_lo - 2) * RL + col;
         xnext[q] = (col < RL && n >= 0 && n < L) ? x[n] : make_float2(0.0f, 0.0f);
       }
+      __syncthreads();   // bflag cleared
+
       for (int64_t rw = row_lo - 2; rw <= row_hi; rw++) {
         float2 xc[CPT];
         double lre[CPT], lim[CPT], lz[CPT];
@@ -186,7 +194,7 @@ __global__ __launch_bounds__(kScT) void sc_kernel(ScArgs a) {
         }
         double tre, tim, tz;
         double ore = are, oim = aim, oz = az;
-        block_scan3(ore, oim, oz, tre, tim, tz, wsum);
+        block_scan3(ore, oim, oz, tre, tim, tz, wsum[rw & 1]);
         double rp_re[CPT], rp_im[CPT], rp_z[CPT];
 #pragma unroll
         for (int q = 0; q < CPT; q++) {
@@ -194,6 +202,7 @@ __global__ __launch_bounds__(kScT) void sc_kernel(ScArgs a) {
           rp_im[q] = oim + lim[q];
           rp_z[q] = oz + lz[q];
         }
+        int has_amb = 0;
         if (rw >= row_lo) {
 #pragma unroll
           for (int q = 0; q < CPT; q++) {
@@ -206,13 +215,13 @@ __global__ __launch_bounds__(kScT) void sc_kernel(ScArgs a) {
             bool b = false;
             if (n >= 0 && n < L && R > 0.0) {
               const double y = (Pre * Pre + Pim * Pim) / (R * R);
-              if (fabs(y - a.thr) <= a.band) {
-                // near the threshold: defer to the exact fp32 recompute below
+              if (fabs(y - a.thr) <= a.band) {   // defer to the exact fp32 recompute
                 const int slot = atomicAdd(&s_namb, 1);
                 if (slot < kAmbMax) {
                   amb_n[slot] = n;
                   atomicMin(&s_nmin, (unsigned long long)n);
                   atomicMax(&s_nmax, (unsigned long long)n);
+                  has_amb = 1;
                 } else {
                   b = (double)sc_exact(x, n, a.M) > a.thr;   // overflow: lane alone
                 }
@@ -223,9 +232,8 @@ __global__ __launch_bounds__(kScT) void sc_kernel(ScArgs a) {
             bflag[n - wb0] = b ? 1 : 0;
           }
         }
-        __syncthreads();
-        const int namb = s_namb < kAmbMax ? s_namb : kAmbMax;
-        if (namb > 0) {   // block-uniform: stage the union of the windows, one lane each
+        if (__syncthreads_or(has_amb)) {   // block-uniform
+          const int namb = s_namb < kAmbMax ? s_namb : kAmbMax;
           const int64_t nmin = (int64_t)s_nmin;
           const int64_t w0 = nmin - (int64_t)a.M + 1;
           const int W = (int)((int64_t)s_nmax - nmin) + (int)a.M;
@@ -241,8 +249,8 @@ __global__ __launch_bounds__(kScT) void sc_kernel(ScArgs a) {
           }
           if (tid == 0 && a.n_exact) atomicAdd(a.n_exact, (unsigned long long)namb);
           __syncthreads();
+          if (tid == 0) { s_namb = 0; s_nmin = ~0ull; s_nmax = 0ull; }
         }
-        if (tid == 0) { s_namb = 0; s_nmin = ~0ull; s_nmax = 0ull; }
 #pragma unroll
         for (int q = 0; q < CPT; q++) {
           rpz2[q] = rpz1[q];
@@ -263,23 +271,17 @@ __global__ __launch_bounds__(kScT) void sc_kernel(ScArgs a) {
           v |= (uint64_t)((q4 & 1u) | ((q4 >> 7) & 2u) | ((q4 >> 14) & 4u) | ((q4 >> 21) & 8u))
                << (4 * i);
         }
-        words[w] = v;
+        words[s][w] = v;
       }
       __syncthreads();
-      // publish this chunk's plateau bits for the start-of-run scan (plateau_kernel)
-      uint64_t *gbits = a.bits + ((uint64_t)f * a.N + s) * a.bit_words;
-      for (int i = tid; i < kScChunk / 64; i += kScT) {
-        const uint64_t gw = (uint64_t)c0 / 64 + i;
-        if (gw < a.bit_words) gbits[gw] = words[wofs + i];
-      }
-      // last-zero prefix max over words (wave 0)
+      // last-zero prefix max over words (wave 0); positions before pos0 read as zero
       if (wv == 0) {
         const int per = (nwords + 63) / 64;
         long long run = -1;
         for (int k = 0; k < per; k++) {
           const int w = lane * per + k;
           if (w < nwords) {
-            const uint64_t inv = ~words[w];
+            const uint64_t inv = ~words[s][w];
             const long long lzw = inv ? (long long)(wb0 + 64 * w + 63 - __clzll(inv)) : -1;
             run = lzw > run ? lzw : run;
             lzp[w] = run;
@@ -299,32 +301,62 @@ __global__ __launch_bounds__(kScT) void sc_kernel(ScArgs a) {
         }
       }
       __syncthreads();
+      int nz = 0;
       for (int ow = tid; ow < kScChunk / 64; ow += kScT) {
         const int64_t wn = wofs + ow;
-        const uint64_t word = words[wn];
+        const uint64_t word = words[s][wn];
         const long long prevlz = (wn > 0) ? lzp[wn - 1] : -1;
         uint64_t cw = 0;
         for (int i = 0; i < 64; i++) {
           const int64_t n = c0 + 64 * ow + i;
           const uint64_t m = ~word & ((2ull << i) - 1ull);
-          const long long lz = m ? (long long)(wb0 + 64 * wn + 63 - __clzll(m)) : prevlz;
-          if (n < L && lz <= n - cp - 2) cw |= 1ull << i;
+          const long long lzv = m ? (long long)(wb0 + 64 * wn + 63 - __clzll(m)) : prevlz;
+          if (n < L && lzv <= n - cp - 2) cw |= 1ull << i;
         }
-        allcond[ow] &= cw;
+        const uint64_t v = allcond[ow] & cw;
+        allcond[ow] = v;
+        nz |= (v != 0ull);
+      }
+      any = __syncthreads_or(nz);   // no qualifying sample left: skip remaining antennas
+    }
+    if (any) {
+      for (int ow = tid; ow < kScChunk / 64; ow += kScT) {
+        const uint64_t v = allcond[ow];
+        if (v) atomicMin(&s_min, (unsigned long long)(c0 + 64 * ow + __ffsll((long long)v) - 1));
       }
       __syncthreads();
+      const unsigned long long cand = s_min;
+      if (cand != ~0ull) {
+        ScRecord *rec = a.rec + (uint64_t)f * a.rec_stride + chunk;
+        if (wv == 0) {   // run start: one past the last zero below the candidate
+          bool found = false;
+          if (lane < (int)a.N) {
+            const int s = lane;
+            const int64_t n = (int64_t)cand;
+            int64_t wn = (n - wb0) / 64;
+            const int64_t i = (n - wb0) % 64;
+            uint64_t m = ~words[s][wn] & ((1ull << i) - 1ull);
+            while (!m && wn > 0) m = ~words[s][--wn];   // rare: only for a candidate chunk
+            const long long lzv = m ? (long long)(wb0 + 64 * wn + 63 - __clzll(m)) : -1;
+            found = lzv >= pos0;    // a computed zero, not the halo padding
+            rec->start[s] = found ? (unsigned long long)(lzv + 1) : 0ull;
+          }
+          const unsigned long long fm = __ballot(found);
+          if (lane == 0) {
+            rec->found = (uint32_t)fm;
+            rec->n_cand = cand;
+            rec->pos0 = pos0;
+            atomicMin(&a.trig[f], cand);
+          }
+        }
+      }
     }
-    for (int ow = tid; ow < kScChunk / 64; ow += kScT) {
-      const uint64_t v = allcond[ow];
-      if (v) atomicMin(&s_min, (unsigned long long)(c0 + 64 * ow + __ffsll((long long)v) - 1));
-    }
-    __syncthreads();
-    if (tid == 0 && s_min != ~0ull) atomicMin(&a.trig[f], s_min);
     __syncthreads();
   }
 }
 
-// start of the run containing the trigger, per antenna; sync index; completeness
+// run starts (from the trigger chunk's record, exact backward scan where the run began
+// before that chunk's halo), sync index, completeness
 __global__ __launch_bounds__(64) void plateau_kernel(PlateauArgs a) {
   const uint32_t f = blockIdx.x;
   const int lane = threadIdx.x;
@@ -342,23 +374,29 @@ __global__ __launch_bounds__(64) void plateau_kernel(PlateauArgs a) {
     }
     return;
   }
+  const ScRecord &rec = a.rec[(uint64_t)f * a.rec_stride + n / kScChunk];
   uint64_t sum = 0;
   for (uint32_t s = 0; s < a.N; s++) {
-    const uint64_t *b = a.bits + ((uint64_t)f * a.N + s) * a.bit_words;
-    const int64_t w = (int64_t)(n / 64);
-    const uint64_t m = ~b[w] & ((1ull << (n % 64)) - 1ull);
     int64_t start = 0;
-    if (m) {
-      start = w * 64 + 63 - __clzll(m) + 1;
+    if (rec.found & (1u << s)) {
+      start = (int64_t)rec.start[s];
     } else {
-      for (int64_t wb = w - 1; wb >= 0; wb -= 64) {
-        const int64_t ww = wb - lane;
-        const uint64_t inv = (ww >= 0) ? ~b[ww] : 0ull;
-        const unsigned long long bal = __ballot(inv != 0ull);
+      // every computed sample of the chunk's range is in the run: walk back exactly
+      const float2 *__restrict__ x = a.iq + ((uint64_t)f * a.N + s) * a.stride;
+      start = 0;
+      for (int64_t q0 = rec.pos0 - 1; q0 >= 0; q0 -= 64) {
+        const int64_t q = q0 - lane;
+        bool zero = true;
+        if (q >= 0) {
+          const float y = sc_exact(x, q, a.M);
+          zero = !((double)y > a.thr);
+        } else {
+          zero = false;
+        }
+        const unsigned long long bal = __ballot(zero);
         if (bal) {
-          const int l = __ffsll((long long)bal) - 1;
-          const int64_t wz = wb - l;
-          start = wz * 64 + 63 - __clzll(~b[wz]) + 1;
+          const int l = __ffsll((long long)bal) - 1;   // lowest lane = highest position
+          start = q0 - l + 1;
           break;
         }
       }
