@@ -13,6 +13,8 @@
 // W is stored [t][r][k] so every weight read is coalesced and L2-resident per frame; the
 // demap, EVM partials and the equalised symbol + uint8 index stores are fused into the same
 // pass. Algorithmic HBM traffic per symbol: N*M*8 read + N*M_occ*9 written.
+#include <algorithm>
+
 #include "fft.hpp"
 #include "kernels.hpp"
 
@@ -151,6 +153,186 @@ __global__ __launch_bounds__(T) void decode_kernel(DecodeArgs a) {
   }
 }
 
+// Persistent form for configurations whose N antennas fit one LDS batch (C1-C3): a grid of
+// ~2 workgroups per CU walks the (frame, symbol) items; the next item's N x M input is
+// loaded into registers (16-byte loads) while the current item is transformed, so HBM
+// reads overlap the FFT and the NxN apply. Each thread owns 4 consecutive subcarriers per
+// group, so weights, gains, equalised symbols and indices move as 16-byte / 4-byte vectors.
+template <int LOG2M, int NA, int T>
+__global__ __launch_bounds__(T) void decode_persistent_kernel(DecodeArgs a) {
+  constexpr int M = 1 << LOG2M, PB = lds_padded_len(M);
+  constexpr int NPAIR = M / 2;                 // complex pairs per antenna body
+  constexpr int NIN = NPAIR / T;               // 16-byte loads per thread per antenna
+  constexpr int G4 = M / (4 * T);              // 4-subcarrier groups per thread
+  static_assert(NIN >= 1 && G4 >= 1, "decode_persistent_kernel needs M >= 4T");
+  extern __shared__ __attribute__((aligned(16))) float2 lds[];
+  __shared__ double red[3][NA][T / 64];
+  const int tid = threadIdx.x;
+  const uint32_t total = a.n_frames * a.max_out;
+  const bool siso = (a.detector == 3);
+
+  float4 pre[NA][NIN];
+  // issue the loads of one item into pre[] (zeros for items without a decodable symbol)
+  auto fetch = [&](uint32_t item) {
+    bool ok = false;
+    int64_t abs0 = 0;
+    uint32_t f = 0;
+    if (item < total) {
+      f = item / a.max_out;
+      const uint32_t s = item % a.max_out;
+      const FrameInfo &I = a.info[f];
+      const uint32_t n_out = (I.status == 0) ? min(I.n_sym, a.max_out) : 0u;
+      if (s < n_out) {
+        abs0 = I.base + (int64_t)I.i0 + (int64_t)s * a.SL + a.cp;
+        ok = abs0 >= 0 && abs0 + M <= (int64_t)a.frame_len;
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < NA; r++) {
+      const float2 *__restrict__ x = a.iq + ((uint64_t)f * NA + r) * a.stride + abs0;
+#pragma unroll
+      for (int u = 0; u < NIN; u++) {
+        const int i2 = tid + u * T;
+        if (!ok) {
+          pre[r][u] = make_float4(0.f, 0.f, 0.f, 0.f);
+        } else if ((abs0 & 1) == 0) {
+          pre[r][u] = reinterpret_cast<const float4 *>(x)[i2];
+        } else {
+          const float2 v0 = x[2 * i2], v1 = x[2 * i2 + 1];
+          pre[r][u] = make_float4(v0.x, v0.y, v1.x, v1.y);
+        }
+      }
+    }
+  };
+
+  uint32_t item = blockIdx.x;
+  fetch(item);
+  for (; item < total; item += gridDim.x) {
+    const uint32_t f = item / a.max_out, s = item % a.max_out;
+    const FrameInfo &I = a.info[f];
+    const uint32_t n_out = (I.status == 0) ? min(I.n_sym, a.max_out) : 0u;
+    double *ep = a.evm_part + (((uint64_t)f * a.max_out + s) * NA) * 3;
+    __syncthreads();   // the previous item's LDS reads are done
+#pragma unroll
+    for (int r = 0; r < NA; r++)
+#pragma unroll
+      for (int u = 0; u < NIN; u++) {
+        const int i = 2 * (tid + u * T);
+        lds[r * PB + lds_pad(i)] = make_float2(pre[r][u].x, pre[r][u].y);
+        lds[r * PB + lds_pad(i + 1)] = make_float2(pre[r][u].z, pre[r][u].w);
+      }
+    fetch(item + gridDim.x);   // next item's input in flight during this item's compute
+    if (s >= n_out) {          // block-uniform
+      if (tid < NA * 3) ep[tid] = 0.0;
+      continue;
+    }
+    __syncthreads();
+    fft_lds<LOG2M, T, NA, false>(lds, a.tw);
+
+    // per-thread partials over <= 4*G4 subcarriers stay fp32; waves and items sum in fp64
+    float e_num[NA], e_den[NA], e_err[NA];
+#pragma unroll
+    for (int t = 0; t < NA; t++) e_num[t] = e_den[t] = e_err[t] = 0.0f;
+    const uint64_t frame_id = a.frame_id0 + f;
+    const float2 *__restrict__ Wf = a.W + (uint64_t)f * NA * NA * M;
+    const float *__restrict__ gf = a.gain + (uint64_t)f * M;
+#pragma unroll
+    for (int g = 0; g < G4; g++) {
+      const int k0 = 4 * (tid + g * T);
+      float2 X[NA][4];
+#pragma unroll
+      for (int r = 0; r < NA; r++)
+#pragma unroll
+        for (int e = 0; e < 4; e++) {
+          const float2 v = lds[r * PB + lds_pad(k0 + e)];
+          X[r][e] = make_float2(v.x * a.dn, v.y * a.dn);   // (:561) x dft_normalizer
+        }
+      float gn[4] = {1.0f, 1.0f, 1.0f, 1.0f};
+      if (!siso) {
+        const float4 g4 = *reinterpret_cast<const float4 *>(gf + k0);
+        gn[0] = g4.x; gn[1] = g4.y; gn[2] = g4.z; gn[3] = g4.w;
+      }
+#pragma unroll
+      for (int t = 0; t < NA; t++) {
+        float2 y[4];
+        if (siso) {
+#pragma unroll
+          for (int e = 0; e < 4; e++) {
+            y[e] = make_float2(0.0f, 0.0f);
+            if (t == (int)a.siso_rx) {
+              const float2 gg =
+                  a.G[(((uint64_t)f * M + k0 + e) * NA + a.siso_rx) * NA + a.siso_tx];
+              y[e] = cdiv(X[t][e], gg);
+            }
+          }
+        } else {
+#pragma unroll
+          for (int r = 0; r < NA; r++) {
+            const float4 *wp = reinterpret_cast<const float4 *>(Wf + ((uint64_t)t * NA + r) * M + k0);
+            const float4 w01 = wp[0], w23 = wp[1];
+            const float2 w[4] = {make_float2(w01.x, w01.y), make_float2(w01.z, w01.w),
+                                 make_float2(w23.x, w23.y), make_float2(w23.z, w23.w)};
+#pragma unroll
+            for (int e = 0; e < 4; e++)
+              y[e] = (r == 0) ? cmul(w[e], X[r][e]) : cadd(y[e], cmul(w[e], X[r][e]));
+          }
+#pragma unroll
+          for (int e = 0; e < 4; e++) y[e] = make_float2(y[e].x * gn[e], y[e].y * gn[e]);
+        }
+        uint32_t packed = 0;
+#pragma unroll
+        for (int e = 0; e < 4; e++) {
+          const int k = k0 + e;
+          const uint32_t d = qam_demap(y[e], a.qam);
+          uint32_t refi = d;
+          if (a.ref_mode == 1)
+            refi = a.ref_idx[(((uint64_t)f * NA + t) * a.max_out + s) * a.M_occ + k];
+          else if (a.ref_mode == 2)
+            refi = (uint32_t)(hash5(a.ref_seed, DOM_DATA, frame_id, t,
+                                    (uint64_t)s * a.M_occ + k) &
+                              (uint64_t)(a.qam.L * a.qam.L - 1));
+          const float2 sp = qam_point(refi, a.qam);
+          const float er = y[e].x - sp.x, ei = y[e].y - sp.y;
+          e_num[t] += er * er + ei * ei;
+          e_den[t] += sp.x * sp.x + sp.y * sp.y;
+          e_err[t] += (d != refi) ? 1.0f : 0.0f;
+          packed |= d << (8 * e);
+        }
+        const uint64_t o = (((uint64_t)f * NA + t) * a.max_out + s) * a.M_occ + k0;
+        if (a.out_sym) {
+          float4 *op = reinterpret_cast<float4 *>(a.out_sym + o);
+          op[0] = make_float4(y[0].x, y[0].y, y[1].x, y[1].y);
+          op[1] = make_float4(y[2].x, y[2].y, y[3].x, y[3].y);
+        }
+        if (a.out_idx) *reinterpret_cast<uint32_t *>(a.out_idx + o) = packed;
+        __builtin_amdgcn_sched_barrier(0);   // keep stream t+1's W loads after stream t
+      }
+    }
+#pragma unroll
+    for (int t = 0; t < NA; t++) {
+      double vn = e_num[t], vd = e_den[t], ve = e_err[t];
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) {
+        vn += __shfl_xor(vn, off);
+        vd += __shfl_xor(vd, off);
+        ve += __shfl_xor(ve, off);
+      }
+      if ((tid & 63) == 0) {
+        red[0][t][tid >> 6] = vn;
+        red[1][t][tid >> 6] = vd;
+        red[2][t][tid >> 6] = ve;
+      }
+    }
+    __syncthreads();
+    if (tid < NA * 3) {
+      const int t = tid / 3, c = tid % 3;
+      double v = 0.0;
+      for (int w = 0; w < T / 64; w++) v += red[c][t][w];
+      ep[t * 3 + c] = v;
+    }
+  }
+}
+
 // per-frame EVM / symbol-error totals: fixed-order strided partial sums + LDS tree, so the
 // result is bitwise reproducible run to run
 __global__ __launch_bounds__(256) void evm_kernel(EvmArgs a) {
@@ -183,6 +365,22 @@ static void decode_launch_na(const DecodeArgs &a, uint32_t nf, hipStream_t s) {
   constexpr int TW = (M * NA / 32) < 64 ? 64 : ((M * NA / 32) > 1024 ? 1024 : (M * NA / 32));
   constexpr int T0 = TW < 256 ? 256 : TW;
   constexpr int T = T0 > M ? M : T0;
+  // persistent kernel: 16 complex per thread per item (4 antennas x 4 subcarriers at C3)
+  constexpr int TP0 = (NA * M / 16) < 64 ? 64 : ((NA * M / 16) > 1024 ? 1024 : (NA * M / 16));
+  constexpr int TP = TP0 > M / 4 ? M / 4 : TP0;
+  if constexpr (GA == NA && TP >= 64) {
+    if (a.all_occ) {
+      const size_t shm = sizeof(float2) * lds_padded_len(M) * NA;
+      (void)hipFuncSetAttribute((const void *)decode_persistent_kernel<LOG2M, NA, TP>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
+      const uint32_t per_cu = (uint32_t)std::max<size_t>(1, (160u * 1024u) / (shm + 2048));
+      const uint32_t total = nf * a.max_out;
+      const uint32_t grid = std::min<uint32_t>(total, a.n_cu * std::min<uint32_t>(per_cu, 4));
+      hipLaunchKernelGGL((decode_persistent_kernel<LOG2M, NA, TP>), dim3(grid), dim3(TP), shm,
+                         s, a);
+      return;
+    }
+  }
   const size_t shm = sizeof(float2) * lds_padded_len(M) * GA;
   (void)hipFuncSetAttribute((const void *)decode_kernel<LOG2M, NA, GA, T>,
                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);

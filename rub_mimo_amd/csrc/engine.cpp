@@ -13,6 +13,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -187,6 +188,7 @@ struct mimo_rx {
   uint32_t M_null = 0, M_pilot = 0, M_data = 0, M_occ = 0;
   int log2M = 0, log2F = 0;
   uint32_t F = 0, lagc = 0, n_lagc = 0, n_slots = 0;
+  uint32_t n_cu = 256;
   int det = 0;
   float noise_var = -1.0f;
   int keep_bias = 1;
@@ -366,6 +368,10 @@ int run_decode(mimo_rx *h, const float2 *iq, uint64_t stride, uint32_t F, uint64
   d.max_out = max_out; d.out_sym = out_sym; d.out_idx = out_idx;
   d.ref_mode = ref_mode; d.ref_idx = ref_idx; d.ref_seed = ref_seed; d.frame_id0 = frame_id0;
   d.qam = h->qam; d.evm_part = h->evm_part.p; d.tw = h->tw;
+  d.n_frames = F; d.n_cu = h->n_cu;
+  // RMIMO_DECODE_GRID=1 forces the one-workgroup-per-symbol grid (A/B against the persistent form)
+  static const bool grid_only = [] { const char *e = getenv("RMIMO_DECODE_GRID"); return e && e[0] == '1'; }();
+  d.all_occ = (h->M_occ == h->M && !grid_only) ? 1 : 0;
   hipEvent_t e = h->timer.begin(s);
   launch_decode(d, h->log2M, F, s);
   h->timer.end(5, e, s);
@@ -456,6 +462,13 @@ int mimo_rx_create(const mimo_rx_config *cfg, void *hip_stream, mimo_rx **out) {
       return fail(MIMO_ERR_HIP, "hipStreamCreate failed");
     }
     h->own_stream = true;
+  }
+  {
+    int dev = 0, ncu = 0;
+    if (hipGetDevice(&dev) == hipSuccess &&
+        hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
+        ncu > 0)
+      h->n_cu = (uint32_t)ncu;
   }
   rc = get_twiddles(&h->tw);
   if (!rc) rc = build_codes(h->codes, h->M, N, h->nac, h->p.data(), cfg->s0_bits, cfg->s1_bits,

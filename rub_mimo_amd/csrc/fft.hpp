@@ -84,10 +84,24 @@ MIMO_DEV void fft_pass(float2 *buf, const float2 *__restrict__ tw) {
 #pragma unroll
       for (int r = 0; r < R; r++) a[q][r] = base[lds_pad(j + r * NB)];
       if constexpr (NS > 1) {
+        // one table read per butterfly; the other R-2 twiddles are products of it
+        // (<= 3 roundings deep, well inside the fp32 FFT error budget)
         const int k = j % NS;
         constexpr int STEP = kTwN / (NS * R);
+        float2 w[R];
+        w[1] = twiddle<INV>(tw, k * STEP);
+        if constexpr (R >= 4) {
+          w[2] = cmul(w[1], w[1]);
+          w[3] = cmul(w[2], w[1]);
+        }
+        if constexpr (R == 8) {
+          w[4] = cmul(w[2], w[2]);
+          w[5] = cmul(w[4], w[1]);
+          w[6] = cmul(w[3], w[3]);
+          w[7] = cmul(w[4], w[3]);
+        }
 #pragma unroll
-        for (int r = 1; r < R; r++) a[q][r] = cmul(a[q][r], twiddle<INV>(tw, r * k * STEP));
+        for (int r = 1; r < R; r++) a[q][r] = cmul(a[q][r], w[r]);
       }
       dft_small<R, INV>(a[q]);
     }

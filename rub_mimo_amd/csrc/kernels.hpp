@@ -114,6 +114,9 @@ struct DecodeArgs {
   Qam qam;
   double *evm_part;                // [F][max_out][N][3]
   const float2 *tw;
+  uint32_t n_frames;
+  int all_occ;                     // every subcarrier occupied (j == k): vector stores
+  uint32_t n_cu;                   // compute units (persistent grid size)
 };
 void launch_decode(const DecodeArgs &a, int log2M, uint32_t n_frames, hipStream_t s);
 
