@@ -13,6 +13,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
@@ -219,8 +220,9 @@ struct mimo_rx {
   DevBuf<float> gain;
   DevBuf<double> nvp, evm_part, evm_out;
   DevBuf<unsigned long long> n_exact;   // S&C exact fp32 recomputes (diagnostic)
+  DevBuf<uint32_t> queue;               // S&C work-queue head
+  DevBuf<unsigned long long> sc_prof;   // RMIMO_SC_PROF=1 cycle counters
   uint32_t last_frames = 0, last_max_out = 0;
-  uint64_t last_words = 0;
   // streaming state (facade)
   DevBuf<float2> capbuf;
   uint64_t cap_len = 0, total = 0;
@@ -287,7 +289,8 @@ int ensure_workspace(mimo_rx *h, uint32_t F, uint64_t chunks, uint64_t evm_entri
 // S&C + plateau over chunks [chunk_lo, end) of every frame
 int run_sync(mimo_rx *h, const float2 *iq, uint64_t stride, uint32_t F, uint64_t frame_len,
              uint64_t chunk_lo, bool reset_trig, hipStream_t s) {
-  const uint64_t nchunks = (frame_len + kScChunk - 1) / kScChunk;
+  const uint64_t K = sc_chunk_len(h->cp);
+  const uint64_t nchunks = (frame_len + K - 1) / K;
   int rc = ensure_workspace(h, F, nchunks, 0);
   if (rc) return rc;
   if (reset_trig) HIPCHK(hipMemsetAsync(h->trig.p, 0xFF, sizeof(unsigned long long) * F, s));
@@ -295,21 +298,46 @@ int run_sync(mimo_rx *h, const float2 *iq, uint64_t stride, uint32_t F, uint64_t
     ScArgs a{};
     a.iq = iq; a.stride = stride; a.frame_len = frame_len;
     a.N = h->N; a.M = h->M; a.cp = h->cp;
-    a.thr = h->thr; a.band = 2e-3;
-    a.chunk_lo = chunk_lo; a.chunk_hi = nchunks;
+    // diagnostics only: RMIMO_SC_BAND overrides the exact-recompute band (a band below the
+    // fp32 error bound breaks parity)
+    static const double band_env = [] { const char *e = getenv("RMIMO_SC_BAND"); return e ? atof(e) : 2e-3; }();
+    a.thr = h->thr; a.band = band_env;
+    a.chunk_len = K; a.chunk_lo = chunk_lo; a.chunk_hi = nchunks;
     a.trig = h->trig.p; a.rec = h->rec.p; a.rec_stride = h->cap_chunks;
     if (!h->n_exact.p) {
       HIPCHK(h->n_exact.ensure(1));
       HIPCHK(hipMemsetAsync(h->n_exact.p, 0, sizeof(unsigned long long), s));
     }
     a.n_exact = h->n_exact.p;
-    const uint32_t grid_x = (uint32_t)std::min<uint64_t>(nchunks - chunk_lo, 64);
+    if (!h->queue.p) HIPCHK(h->queue.ensure(1));
+    HIPCHK(hipMemsetAsync(h->queue.p, 0, sizeof(uint32_t), s));
+    a.queue = h->queue.p;
+    static const bool prof_env = [] { const char *e = getenv("RMIMO_SC_PROF"); return e && e[0] == '1'; }();
+    if (prof_env) {
+      if (!h->sc_prof.p) HIPCHK(h->sc_prof.ensure(17));
+      HIPCHK(hipMemsetAsync(h->sc_prof.p, 0, 17 * sizeof(unsigned long long), s));
+      HIPCHK(hipMemsetAsync(h->sc_prof.p + 8, 0xFF, sizeof(unsigned long long), s));
+      a.prof = h->sc_prof.p;
+    }
     hipEvent_t e = h->timer.begin(s);
-    launch_sc(a, F, grid_x, s);
+    launch_sc(a, F, h->n_cu, s);
     h->timer.end(0, e, s);
+    if (prof_env) {   // diagnostics: per-item cycle split of the S&C kernel
+      unsigned long long v[17];
+      HIPCHK(hipMemcpyAsync(v, h->sc_prof.p, sizeof(v), hipMemcpyDeviceToHost, s));
+      HIPCHK(hipStreamSynchronize(s));
+      const double it = v[0] ? (double)v[0] : 1.0;
+      fprintf(stderr, "sc_prof items %llu skipped %llu antenna_passes %llu cycles/item rows %.0f "
+              "words %.0f resolve %.0f total %.0f wall_us/item %.2f span_us %.2f max_item_us %.2f "
+              "last_start_us %.2f\n", v[0], v[6], v[1],
+              v[2] / it, v[3] / it, v[4] / it, v[5] / it, v[7] / it / 100.0,
+              (double)(v[9] - v[8]) / 100.0, v[10] / 100.0, (double)(v[11] - v[8]) / 100.0);
+      fprintf(stderr, "sc_prof phases/item warm %.0f A %.0f scan %.0f B %.0f run %.0f\n",
+              v[12] / it, v[13] / it, v[14] / it, v[15] / it, v[16] / it);
+    }
   }
   PlateauArgs pa{};
-  pa.trig = h->trig.p; pa.rec = h->rec.p; pa.rec_stride = h->cap_chunks;
+  pa.trig = h->trig.p; pa.rec = h->rec.p; pa.rec_stride = h->cap_chunks; pa.chunk_len = K;
   pa.iq = iq; pa.stride = stride; pa.frame_len = frame_len;
   pa.N = h->N; pa.M = h->M; pa.SL = h->SL; pa.thr = h->thr; pa.win_len = h->win_len;
   pa.info = h->info.p;
@@ -598,12 +626,13 @@ int mimo_rx_execute(mimo_rx *h, const float *const *iq, uint32_t n_ant, uint64_t
   h->total = old_total + n;
   if (h->state == MIMO_STATE_SEEK_PLATEAU) {
     if (old_total == 0) {
-      rc = ensure_workspace(h, 1, (h->total + kScChunk - 1) / kScChunk, 0);
+      const uint64_t K = sc_chunk_len(h->cp);
+      rc = ensure_workspace(h, 1, (h->total + K - 1) / K, 0);
       if (rc) return rc;
       HIPCHK(hipMemsetAsync(h->trig.p, 0xFF, sizeof(unsigned long long), h->stream));
     }
     // re-run the partially filled chunk; earlier chunks are final (y[n] uses x[<=n] only)
-    rc = run_sync(h, h->capbuf.p, h->cap_len, 1, h->total, old_total / kScChunk, false,
+    rc = run_sync(h, h->capbuf.p, h->cap_len, 1, h->total, old_total / sc_chunk_len(h->cp), false,
                   h->stream);
     if (rc) return rc;
     HIPCHK(hipMemcpyAsync(&h->sinfo, h->info.p, sizeof(FrameInfo), hipMemcpyDeviceToHost,
@@ -780,7 +809,6 @@ int mimo_rx_process_batch(mimo_rx *h, const mimo_batch *b, void *hip_stream) {
   if (rc) return rc;
   h->last_frames = b->n_frames;
   h->last_max_out = b->max_out_syms;
-  h->last_words = (b->frame_len + kScChunk - 1) / kScChunk;
   return MIMO_OK;
 }
 

@@ -22,19 +22,28 @@ struct ScArgs {
   uint64_t frame_len;
   uint32_t N, M, cp;
   double thr, band;
+  uint64_t chunk_len;        // candidate positions per chunk (sc_chunk_len)
   uint64_t chunk_lo, chunk_hi;
   unsigned long long *trig; // [F], min trigger sample (UINT64_MAX = none yet)
   ScRecord *rec;            // [F][rec_stride] per-chunk candidates
   uint64_t rec_stride;
   unsigned long long *n_exact;  // count of exact fp32 recomputes (null: not counted)
+  uint32_t *queue;          // work-queue head, zeroed before each launch
+  unsigned long long *prof; // diagnostics: [items, antenna passes, row, words, resolve, total
+                            // cycles, skipped items] (null: off)
 };
-constexpr int kScChunk = 8192;   // output samples per chunk (multiple of 64 and of M/2)
-void launch_sc(const ScArgs &a, uint32_t n_frames, uint32_t grid_x, hipStream_t s);
+// an S&C work item spans kScSpan positions: a halo of >= cp+2 (run history, multiple of 16)
+// and the chunk's candidate positions
+constexpr int kScSpan = 16384;
+inline uint64_t sc_chunk_len(uint32_t cp) { return kScSpan - ((uint64_t)cp + 2 + 15) / 16 * 16; }
+size_t sc_lds_bytes(uint32_t M, uint32_t N);
+// persistent grid of n_cu x (resident blocks per CU) over the F x chunks items
+void launch_sc(const ScArgs &a, uint32_t n_frames, uint32_t n_cu, hipStream_t s);
 
 struct PlateauArgs {
   const unsigned long long *trig;
   const ScRecord *rec;
-  uint64_t rec_stride;
+  uint64_t rec_stride, chunk_len;
   const float2 *iq;
   uint64_t stride, frame_len;
   uint32_t N, M, SL;

@@ -7,65 +7,98 @@
 //   y[n] = |P|^2 / R^2 ;  plateau: y > 0.95 run with end - start > cp on every antenna;
 //   sync_index = floor(sum of run starts / N).
 //
-// GPU form. A workgroup owns one 8192-sample chunk of one frame and walks it antenna by
-// antenna in rows of M/2 samples; thread t owns fixed columns, so x[n-M/2] is the same
-// thread's value one row up and the windowed sums are row-prefix differences:
-//   P[n] = RP_r[c] + (RT_{r-1} - RP_{r-1}[c]),  R[n] = RPz_r[c] + RTz_{r-1} + RTz_{r-2} - RPz_{r-2}[c]
-// with one block scan per row, all in fp64 (error ~1e-13, far below the decision band).
-// Samples whose fp64 metric lies within kBand of the threshold are recomputed exactly as the
-// CPU oracle does (sequential fp32 sums oldest->newest, no FMA: this file is compiled with
-// -ffp-contract=off), one lane per sample over an LDS-staged window. A sequential fp32 sum of
-// M terms is within (M-1)u of the exact value, so |y32 - y_exact| <= ~4e-4 for M <= 2048
-// (DESIGN.md); a 2e-3 band keeps every plateau decision -- hence plateau start/end and
-// sync_index -- bit-identical to the oracle.
+// GPU form (throughput, not a per-sample scan). A persistent grid pulls (frame, chunk) items
+// from a queue in chunk-major order. An item is kScSpan = 16384 positions: a halo of
+// H >= cp+2 positions (run history) and K = kScSpan - H candidate positions. For each antenna
+// the workgroup streams the item through an LDS ring of M + 4096 samples (coalesced 16-byte
+// loads, the next 4096 samples in flight while the current ones are processed); thread t
+// owns 16 consecutive positions per 4096-sample iteration. With the window sums written as
+// running differences,
+//   P[n] = P[n-1] + p[n] - p[n-M/2],   2R[n] = 2R[n-1] + |x[n]|^2 - |x[n-M]|^2,
+// each thread sums its segment's differences, one block scan (fp64) gives every segment its
+// starting sums, and the thread walks its 16 positions. The decision is division-free:
+// |P|^2 - thr R^2 against band * R^2.
 //
-// Plateau runs become 64-bit words; "run of cp+2 ones ending at n" is a last-zero prefix max
-// over words. Antennas are processed in order and the chunk stops as soon as no sample can
-// still qualify on every antenna (noise and data regions cost one antenna, not N). The first
-// qualifying n is atomicMin'ed into trig[frame]; the chunk also records each antenna's run
-// start from its LDS bits, which plateau_kernel completes with an exact backward scan only
-// when a run began before the chunk's halo. Chunks beyond the current trigger exit early;
-// results never depend on dispatch order (a chunk is skipped only when a smaller trigger
-// already exists, and the kept candidate is the global minimum).
+// Exactness. Samples whose fp64 metric lies within the band of the threshold -- or whose
+// window energy is tiny next to the energy streamed so far, where fp64 cancellation could
+// matter -- are provisionally 1 and recomputed exactly as the CPU oracle does (sequential fp32
+// sums oldest->newest, no FMA: this file is compiled with -ffp-contract=off) once the item
+// still has a candidate. A sequential fp32 sum of M terms is within (M-1)u of the exact
+// value, so |y32 - y_exact| <= ~4e-4 for M <= 2048; a 2e-3 band keeps every
+// plateau decision -- hence plateau start/end and sync_index -- bit-identical to the oracle.
+// An all-zero window (R = 0, the oracle's 0/0) is tracked exactly with a nonzero count.
+//
+// "Run of cp+2 ones ending at n" is a last-zero prefix max (block scan per iteration).
+// Antennas are processed in order and the item stops as soon as no position can still
+// qualify on every antenna (provisional ones only enlarge that set, so the early-out is
+// safe); noise and data regions cost one antenna, not N. The first qualifying n is
+// atomicMin'ed into trig[frame] and the item records each antenna's run start from its LDS
+// bits; plateau_kernel completes a run that began before the halo with an exact backward
+// scan. Items beyond a frame's current trigger are skipped; results never depend on
+// dispatch order (an item is skipped only when a smaller trigger already exists, and the
+// kept candidate is the global minimum).
+#include <algorithm>
+#include <cstdio>
+
 #include "kernels.hpp"
 
 #pragma clang fp contract(off)
 
 namespace mimo {
 
-constexpr int kScT = 256;
-constexpr int kBfMax = 12864;  // >= chunk + cp + 2*(M/2) + 64 for M <= 4096
-constexpr int kBfW = kBfMax / 64;
-constexpr int kAmbMax = 128;   // near-threshold samples resolved cooperatively per row
+constexpr int kScT = 256;               // threads per workgroup
+constexpr int kScS = 16;                // consecutive positions per thread per iteration
+constexpr int kScIt = kScT * kScS;      // 4096 positions per iteration
+constexpr int kScIters = kScSpan / kScIt;
+constexpr int kAmbMax = 256;            // provisional samples per item
+constexpr int kResGroup = kScT / 2;     // samples per resolve pass (two lanes each)
+static_assert(kScSpan % kScIt == 0, "item span");
 
-MIMO_DEV int64_t floordiv(int64_t a, int64_t b) {
-  int64_t q = a / b;
-  return (q * b > a) ? q - 1 : q;
-}
+// LDS ring slot -> padded float2 index: 2 float2 of padding per 32 keeps the 16-byte reads
+// of 16 consecutive threads (16 positions apart) on distinct banks
+MIMO_DEV int ring_pad(int i) { return i + ((i >> 5) << 1); }
 
 // exact restatement of framing.cc:626-637 under the pinned liquid semantics, on the M
 // samples s[i] = x[n - M + 1 + i] (LDS). The three accumulation chains are interleaved for
 // latency; each keeps its own oldest -> newest order.
 MIMO_DEV float sc_exact_lds(const float2 *s, int M) {
+  constexpr int U = 8;                 // M/2 is a multiple of 32 for every supported M
   const int M2 = M / 2;
   float Pr = 0.0f, Pi = 0.0f, R = 0.0f;
-  for (int j = 0; j < M2; j++) {       // P: k = n - M/2 + 1 + j
-    const float2 d = s[j], v = s[M2 + j];
-    float pr = d.x * v.x - (-d.y) * v.y;
-    float pi = d.x * v.y + (-d.y) * v.x;
-    Pr = Pr + (-1.0f) * pr;
-    Pi = Pi + (-1.0f) * pi;
-    const float2 u0 = s[2 * j], u1 = s[2 * j + 1];   // R: i = 2j, 2j+1
-    float z0 = u0.x * u0.x + u0.y * u0.y;
-    R = R + 0.5f * z0;
-    float z1 = u1.x * u1.x + u1.y * u1.y;
-    R = R + 0.5f * z1;
+  float2 d[U], v[U], u[2 * U];         // the next block's operands load while this one sums
+#pragma unroll
+  for (int k = 0; k < U; k++) { d[k] = s[k]; v[k] = s[M2 + k]; }
+#pragma unroll
+  for (int k = 0; k < 2 * U; k++) u[k] = s[k];
+  for (int j = 0; j < M2; j += U) {
+    float2 dc[U], vc[U], uc[2 * U];
+#pragma unroll
+    for (int k = 0; k < U; k++) { dc[k] = d[k]; vc[k] = v[k]; }
+#pragma unroll
+    for (int k = 0; k < 2 * U; k++) uc[k] = u[k];
+    if (j + U < M2) {
+#pragma unroll
+      for (int k = 0; k < U; k++) { d[k] = s[j + U + k]; v[k] = s[M2 + j + U + k]; }
+#pragma unroll
+      for (int k = 0; k < 2 * U; k++) u[k] = s[2 * (j + U) + k];
+    }
+#pragma unroll
+    for (int k = 0; k < U; k++) {      // P: k' = n - M/2 + 1 + j + k
+      float pr = dc[k].x * vc[k].x - (-dc[k].y) * vc[k].y;
+      float pi = dc[k].x * vc[k].y + (-dc[k].y) * vc[k].x;
+      Pr = Pr + (-1.0f) * pr;
+      Pi = Pi + (-1.0f) * pi;
+      float z0 = uc[2 * k].x * uc[2 * k].x + uc[2 * k].y * uc[2 * k].y;   // R: i = 2(j+k)
+      R = R + 0.5f * z0;
+      float z1 = uc[2 * k + 1].x * uc[2 * k + 1].x + uc[2 * k + 1].y * uc[2 * k + 1].y;
+      R = R + 0.5f * z1;
+    }
   }
   return (Pr * Pr + Pi * Pi) / (R * R);
 }
 
-// the same straight from global memory (one lane; overflow rows and the rare backward scan)
-__device__ __noinline__ float sc_exact(const float2 *__restrict__ x, int64_t n, int64_t M) {
+// the same straight from global memory (one lane; list overflow and the rare backward scan)
+MIMO_DEV float sc_exact(const float2 *__restrict__ x, int64_t n, int64_t M) {
   const int64_t M2 = M / 2;
   float Pr = 0.0f, Pi = 0.0f, R = 0.0f;
   for (int64_t k = n - M2 + 1; k <= n; k++) {
@@ -84,245 +117,466 @@ __device__ __noinline__ float sc_exact(const float2 *__restrict__ x, int64_t n, 
   return (Pr * Pr + Pi * Pi) / (R * R);
 }
 
-// block-wide exclusive scan of three doubles plus block totals; wsum is double-buffered by
-// the caller (alternate rows), so one barrier per scan suffices
-MIMO_DEV void block_scan3(double &a, double &b, double &c, double &ta, double &tb, double &tc,
-                          double (*wsum)[kScT / 64]) {
+
+// block-wide exclusive scan of NV doubles plus the block totals (one barrier; the caller
+// alternates ws between consecutive scans)
+template <int NV>
+MIMO_DEV void block_scan(double (&v)[NV], double (&tot)[NV], double (*ws)[kScT / 64]) {
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  double ia = a, ib = b, ic = c;
+  double inc[NV];
+#pragma unroll
+  for (int k = 0; k < NV; k++) inc[k] = v[k];
 #pragma unroll
   for (int off = 1; off < 64; off <<= 1) {
-    double xa = __shfl_up(ia, off), xb = __shfl_up(ib, off), xc = __shfl_up(ic, off);
-    if (lane >= off) { ia += xa; ib += xb; ic += xc; }
-  }
-  if (lane == 63) { wsum[0][wv] = ia; wsum[1][wv] = ib; wsum[2][wv] = ic; }
-  __syncthreads();
-  double oa = 0.0, ob = 0.0, oc = 0.0;
-  ta = 0.0; tb = 0.0; tc = 0.0;
 #pragma unroll
-  for (int w = 0; w < kScT / 64; w++) {
-    if (w < wv) { oa += wsum[0][w]; ob += wsum[1][w]; oc += wsum[2][w]; }
-    ta += wsum[0][w]; tb += wsum[1][w]; tc += wsum[2][w];
+    for (int k = 0; k < NV; k++) {
+      const double o = __shfl_up(inc[k], off);
+      if (lane >= off) inc[k] += o;
+    }
   }
-  a = oa + ia - a;
-  b = ob + ib - b;
-  c = oc + ic - c;
+  if (lane == 63) {
+#pragma unroll
+    for (int k = 0; k < NV; k++) ws[k][wv] = inc[k];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < NV; k++) {
+    double o = 0.0, t = 0.0;
+#pragma unroll
+    for (int w = 0; w < kScT / 64; w++) {
+      const double u = ws[k][w];
+      if (w < wv) o += u;
+      t += u;
+    }
+    v[k] = o + (inc[k] - v[k]);
+    tot[k] = t;
+  }
 }
 
-template <int CPT>
-__global__ __launch_bounds__(kScT) void sc_kernel(ScArgs a) {
-  __shared__ __attribute__((aligned(16))) uint8_t bflag[kBfMax];
-  __shared__ uint64_t words[kMaxStreams][kBfW];
-  __shared__ long long lzp[kBfW];
-  __shared__ uint64_t allcond[kScChunk / 64];
-  __shared__ double wsum[2][3][kScT / 64];
-  __shared__ unsigned long long s_trig, s_min;
-  __shared__ float2 stage[768 * CPT];      // union of a row's near-threshold windows (1.5 M)
-  __shared__ long long amb_n[kAmbMax];
-  __shared__ int s_namb;
-  __shared__ unsigned long long s_nmin, s_nmax;
+// "run of cp+2 ones ends at n" for the 16 positions sb..sb+15 of this thread. carry is the
+// last zero before the iteration (block-uniform, updated to the last zero through it).
+MIMO_DEV uint32_t run_cond(uint32_t bits, int64_t sb, long long &carry, int64_t cp,
+                           long long *red) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const uint32_t inv = ~bits & 0xFFFFu;
+  const long long lz = inv ? (long long)(sb + 31 - __clz(inv)) : -1;
+  long long inc = lz;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const long long o = __shfl_up(inc, off);
+    if (lane >= off && o > inc) inc = o;
+  }
+  long long ex = __shfl_up(inc, 1);
+  if (lane == 0) ex = -1;
+  if (lane == 63) red[wv] = inc;
+  __syncthreads();
+  long long before = carry, all = carry;
+#pragma unroll
+  for (int w = 0; w < kScT / 64; w++) {
+    const long long u = red[w];
+    if (w < wv && u > before) before = u;
+    if (u > all) all = u;
+  }
+  if (ex > before) before = ex;
+  uint32_t cond = 0;
+  if (cp + 2 > kScS) {
+    // a zero inside the segment is < cp+2 positions back, so only the leading run of ones
+    // (bits 0..i all set) can qualify, and only where the last zero before it is old enough
+    const uint32_t lead = bits & ~(bits + 1u) & 0xFFFFu;
+    const long long i0 = before + cp + 2 - sb;
+    cond = i0 <= 0 ? lead : (i0 >= kScS ? 0u : lead & ~((1u << i0) - 1u));
+  } else {
+#pragma unroll
+    for (int i = 0; i < kScS; i++) {
+      const uint32_t m = inv & ((2u << i) - 1u);
+      const long long lzv = m ? (long long)(sb + 31 - __clz(m)) : before;
+      if (lzv <= sb + i - cp - 2) cond |= 1u << i;
+    }
+  }
+  carry = all;
+  return cond;
+}
+
+// two consecutive samples (q even), zero outside [0, L)
+MIMO_DEV float4 ld_pair(const float2 *__restrict__ x, int64_t q, int64_t L, bool vec) {
+  if (vec && q >= 0 && q + 1 < L) return *reinterpret_cast<const float4 *>(x + q);
+  const float2 v0 = (q >= 0 && q < L) ? x[q] : make_float2(0.0f, 0.0f);
+  const float2 v1 = (q + 1 >= 0 && q + 1 < L) ? x[q + 1] : make_float2(0.0f, 0.0f);
+  return make_float4(v0.x, v0.y, v1.x, v1.y);
+}
+
+// one iteration's 4096 samples from q0 into registers, 16 bytes per lane, when the block is
+// inside [0, L) (block-uniform); otherwise false and the ring is filled by guarded loads
+MIMO_DEV bool fetch_block(float4 (&pre)[kScIt / (2 * kScT)], const float2 *__restrict__ x,
+                          int64_t q0, int64_t L, bool vec) {
+  const bool ok = vec && q0 >= 0 && q0 + kScIt <= L;
+  const float4 *p = reinterpret_cast<const float4 *>(x + (ok ? q0 : 0)) + threadIdx.x;
+#pragma unroll
+  for (int j = 0; j < kScIt / (2 * kScT); j++)
+    pre[j] = ok ? p[kScT * j] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+  return ok;
+}
+
+// conj(d) * v, the oracle's operation order
+MIMO_DEV float2 cj_mul(float2 d, float2 v) {
+  return make_float2(d.x * v.x - (-d.y) * v.y, d.x * v.y + (-d.y) * v.x);
+}
+
+__global__ __launch_bounds__(kScT) void sc_kernel(ScArgs a, uint32_t n_frames) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char sc_dyn[];
+  const int M = (int)a.M, RL = M / 2, RING = M + kScIt;
+  float2 *ring = reinterpret_cast<float2 *>(sc_dyn);
+  // provisional plateau bits, [antenna][iteration][thread] x 16
+  uint16_t *wbits = reinterpret_cast<uint16_t *>(sc_dyn + sizeof(float2) * ring_pad(RING));
+  __shared__ uint16_t acond[kScIters][kScT];
+  __shared__ double scan_ws[2][5][kScT / 64];
+  __shared__ long long run_ws[2][kScT / 64];
+  __shared__ unsigned long long s_trig, s_min, s_key;
+  __shared__ uint32_t s_item;
+  __shared__ long long amb_n[kAmbMax];     // -1 once taken by a resolve pass
+  __shared__ long long amb_pos[kAmbMax];
+  __shared__ uint8_t amb_s[kAmbMax];
+  __shared__ int s_namb, s_ng;
+  __shared__ int res_i[kResGroup];
+  __shared__ float res_v[3][kResGroup];
+  auto amb_n_val = [&](int i) { return amb_pos[i]; };
 
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  if (tid == 0) { s_namb = 0; s_nmin = ~0ull; s_nmax = 0ull; }
-  const uint32_t f = blockIdx.y;
-  const int64_t RL = a.M / 2;
-  const int64_t L = (int64_t)a.frame_len;
-  const int64_t cp = a.cp;
+  const int64_t L = (int64_t)a.frame_len, cp = a.cp;
+  const int64_t K = (int64_t)a.chunk_len, H = (int64_t)kScSpan - K;
+  const uint64_t total = (a.chunk_hi - a.chunk_lo) * n_frames;
+  int par = 0;
+  if (a.prof && tid == 0) atomicMin(&a.prof[8], (unsigned long long)wall_clock64());
 
-  for (uint64_t chunk = a.chunk_lo + blockIdx.x; chunk < a.chunk_hi; chunk += gridDim.x) {
-    const int64_t c0 = (int64_t)chunk * kScChunk;
-    if (c0 >= L) break;
+  for (;;) {
+    if (tid == 0) s_item = atomicAdd(a.queue, 1u);
+    __syncthreads();
+    const uint64_t item = s_item;
+    if (item >= total) {
+      if (a.prof && tid == 0) atomicMax(&a.prof[9], (unsigned long long)wall_clock64());
+      break;
+    }
+    const uint32_t f = (uint32_t)(item % n_frames);
+    const uint64_t chunk = a.chunk_lo + item / n_frames;
+    const int64_t c0 = (int64_t)chunk * K;
     if (tid == 0) {
       s_trig = __hip_atomic_load(&a.trig[f], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       s_min = ~0ull;
+      s_namb = 0;
     }
-    for (int i = tid; i < kScChunk / 64; i += kScT) allcond[i] = ~0ull;
+#pragma unroll
+    for (int it = 0; it < kScIters; it++) acond[it][tid] = 0xFFFFu;
     __syncthreads();
-    if (s_trig < (unsigned long long)c0) break;  // an earlier trigger exists
-
-    const int64_t row_lo = floordiv(c0 - cp - 1, RL);
-    const int64_t row_hi = (c0 + kScChunk - 1) / RL;
-    const int64_t pos0 = row_lo * RL;               // first computed sample
-    const int64_t wb0 = floordiv(pos0, 64) * 64;
-    const int nbytes = (int)((row_hi + 1) * RL - wb0);
-    const int nwords = (nbytes + 63) / 64;
-    const int64_t wofs = (c0 - wb0) / 64;
+    if (c0 >= L || s_trig < (unsigned long long)c0) {  // an earlier trigger exists
+      if (a.prof && tid == 0) atomicAdd(&a.prof[6], 1ull);
+      continue;
+    }
+    const long long t_item = clock64();
+    const long long w_item = wall_clock64();
+    long long t_rows = 0, t_words = 0, t_ph[5] = {0, 0, 0, 0, 0};
+    const int64_t w0 = c0 - H;                 // first evaluated position
+    const int64_t org = w0 - M;                // ring slot 0 at the start of the item
+    const int64_t cend = std::min<int64_t>(c0 + K, L);
     int any = 1;
+    uint32_t n_done = 0;
 
     for (uint32_t s = 0; s < a.N && any; s++) {
+      const long long t_r0 = clock64();
       const float2 *__restrict__ x = a.iq + ((uint64_t)f * a.N + s) * a.stride;
-      for (int i = tid; i < nwords * 64; i += kScT) bflag[i] = 0;
-
-      float2 xprev[CPT];
-      double rpp_re[CPT], rpp_im[CPT], rpz1[CPT], rpz2[CPT];
-#pragma unroll
-      for (int q = 0; q < CPT; q++) {
-        xprev[q] = make_float2(0.0f, 0.0f);
-        rpp_re[q] = rpp_im[q] = rpz1[q] = rpz2[q] = 0.0;
+      const bool vec = ((uintptr_t)x & 15u) == 0;
+      // history [org, w0) -> slots [0, M); iteration 0's block in flight behind it
+      for (int j = tid; 2 * j < M; j += kScT)
+        *reinterpret_cast<float4 *>(ring + ring_pad(2 * j)) = ld_pair(x, org + 2 * j, L, vec);
+      float4 pre[kScIt / (2 * kScT)];
+      bool pf = fetch_block(pre, x, w0, L, vec);
+      __syncthreads();
+      // window sums ending at w0 - 1: P over [w0-RL, w0), 2R and the nonzero count over [org, w0)
+      double c[4] = {0.0, 0.0, 0.0, 0.0}, t4[4], tot[5];
+      for (int k = tid; k < M; k += kScT) {
+        const float2 v = ring[ring_pad(k)];
+        const float z = v.x * v.x + v.y * v.y;
+        c[2] += (double)z;
+        c[3] += (z != 0.0f) ? 1.0 : 0.0;
+        if (k >= RL) {
+          const float2 pp = cj_mul(ring[ring_pad(k - RL)], v);
+          c[0] += (double)pp.x;
+          c[1] += (double)pp.y;
+        }
       }
-      double rtp_re = 0.0, rtp_im = 0.0, rtz1 = 0.0, rtz2 = 0.0;
-      // software pipeline: the next row's samples are in flight while this row scans
-      float2 xnext[CPT];
-#pragma unroll
-      for (int q = 0; q < CPT; q++) {
-        const int64_t col = (int64_t)tid * CPT + q;
-        const int64_t n = (row_lo - 2) * RL + col;
-        xnext[q] = (col < RL && n >= 0 && n < L) ? x[n] : make_float2(0.0f, 0.0f);
-      }
-      __syncthreads();   // bflag cleared
+      block_scan<4>(c, t4, scan_ws[par]);
+      long long t_m = clock64();
+      t_ph[0] += t_m - t_r0;
+      par ^= 1;
+      double Pc_re = t4[0], Pc_im = t4[1], Zc = t4[2], Cc = t4[3], Ac = t4[2];
+      long long carry = w0 - 1;                // the halo boundary reads as a zero
 
-      for (int64_t rw = row_lo - 2; rw <= row_hi; rw++) {
-        float2 xc[CPT];
-        double lre[CPT], lim[CPT], lz[CPT];
-        double are = 0.0, aim = 0.0, az = 0.0;
+#pragma unroll 1
+      for (int it = 0; it < kScIters; it++) {
+        const int64_t ib = w0 + (int64_t)it * kScIt;
+        {
+          const int slot = (M + it * kScIt) % RING + 2 * tid;
+          if (pf) {
 #pragma unroll
-        for (int q = 0; q < CPT; q++) {
-          xc[q] = xnext[q];
-          const int64_t col = (int64_t)tid * CPT + q;
-          const int64_t n1 = (rw + 1) * RL + col;
-          xnext[q] = (rw < row_hi && col < RL && n1 >= 0 && n1 < L) ? x[n1]
-                                                                     : make_float2(0.0f, 0.0f);
+            for (int j = 0; j < kScIt / (2 * kScT); j++) {
+              int sl = slot + 2 * kScT * j;
+              if (sl >= RING) sl -= RING;
+              *reinterpret_cast<float4 *>(ring + ring_pad(sl)) = pre[j];
+            }
+          } else {   // frame edges: guarded loads straight into the ring
+#pragma unroll 1
+            for (int j = 0; j < kScIt / (2 * kScT); j++) {
+              int sl = slot + 2 * kScT * j;
+              if (sl >= RING) sl -= RING;
+              *reinterpret_cast<float4 *>(ring + ring_pad(sl)) =
+                  ld_pair(x, ib + 2 * (tid + kScT * j), L, vec);
+            }
+          }
         }
+        __syncthreads();
+        if (it + 1 < kScIters) pf = fetch_block(pre, x, ib + kScIt, L, vec);
+        const float2 *xn = ring + ring_pad((M + it * kScIt + kScS * tid) % RING);
+        const float2 *xr = ring + ring_pad((RL + it * kScIt + kScS * tid) % RING);
+        const float2 *xm = ring + ring_pad((it * kScIt + kScS * tid) % RING);
+        // phase A: this segment's sum of window differences
+        // (plus |dP| and lagged-energy sums that bound y over the segment)
+        double d[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
+        float bp = 0.0f, bz = 0.0f;
+        int dc = 0;
+#pragma unroll 2
+        for (int i = 0; i < kScS; i += 2) {
+          const float4 vn = *reinterpret_cast<const float4 *>(xn + i);
+          const float4 vr = *reinterpret_cast<const float4 *>(xr + i);
+          const float4 vm = *reinterpret_cast<const float4 *>(xm + i);
 #pragma unroll
-        for (int q = 0; q < CPT; q++) {
-          const float2 d = xprev[q];
-          float pr = d.x * xc[q].x - (-d.y) * xc[q].y;  // conj(x[n-M/2]) * x[n]
-          float pi = d.x * xc[q].y + (-d.y) * xc[q].x;
-          float z = xc[q].x * xc[q].x + xc[q].y * xc[q].y;
-          are += (double)pr; aim += (double)pi; az += (double)z;
-          lre[q] = are; lim[q] = aim; lz[q] = az;
+          for (int h = 0; h < 2; h++) {
+            const float2 n_ = h ? make_float2(vn.z, vn.w) : make_float2(vn.x, vn.y);
+            const float2 r_ = h ? make_float2(vr.z, vr.w) : make_float2(vr.x, vr.y);
+            const float2 m_ = h ? make_float2(vm.z, vm.w) : make_float2(vm.x, vm.y);
+            const float2 pn = cj_mul(r_, n_), pl = cj_mul(m_, r_);
+            const float zn = n_.x * n_.x + n_.y * n_.y, zl = m_.x * m_.x + m_.y * m_.y;
+            const double zn64 = (double)zn;
+            d[0] += (double)pn.x - (double)pl.x;
+            d[1] += (double)pn.y - (double)pl.y;
+            d[2] += zn64 - (double)zl;
+            d[4] += zn64;
+            dc += (zn != 0.0f ? 1 : 0) - (zl != 0.0f ? 1 : 0);
+            bp += (fabsf(pn.x) + fabsf(pn.y)) + (fabsf(pl.x) + fabsf(pl.y));
+            bz += zl;
+          }
         }
-        double tre, tim, tz;
-        double ore = are, oim = aim, oz = az;
-        block_scan3(ore, oim, oz, tre, tim, tz, wsum[rw & 1]);
-        double rp_re[CPT], rp_im[CPT], rp_z[CPT];
-#pragma unroll
-        for (int q = 0; q < CPT; q++) {
-          rp_re[q] = ore + lre[q];
-          rp_im[q] = oim + lim[q];
-          rp_z[q] = oz + lz[q];
+        d[3] = (double)dc;
+        { const long long t2 = clock64(); t_ph[1] += t2 - t_m; t_m = t2; }
+        block_scan<5>(d, tot, scan_ws[par]);
+        { const long long t2 = clock64(); t_ph[2] += t2 - t_m; t_m = t2; }
+        par ^= 1;
+        // phase B: walk the segment
+        double Pre = Pc_re + d[0], Pim = Pc_im + d[1], Z = Zc + d[2], C = Cc + d[3];
+        const double Aend = Ac + tot[4];       // energy streamed through this iteration
+        const double zfloor = 1e-6 * Aend;
+        const int64_t sb = ib + kScS * tid;
+        uint32_t bits = 0, ovf = 0;
+        // Every n of the segment has |P[n]| <= |P_s| + bp and 2R[n] >= Z_s - bz. If that bound
+        // keeps y below thr - 2*band everywhere (and the fp64 sums are far from cancellation),
+        // all 16 decisions are 0 and the walk is skipped -- the common case away from a sync.
+        bool walk = true;
+        {
+          const double pmax = sqrt(Pre * Pre + Pim * Pim) + 1.001 * (double)bp;
+          const double rmin = 0.5 * (Z - 1.001 * (double)bz);
+          if (rmin > 0.0 && Z > 16.0 * zfloor && pmax * pmax < (a.thr - 2.0 * a.band) * (rmin * rmin))
+            walk = false;
         }
-        int has_amb = 0;
-        if (rw >= row_lo) {
+#pragma unroll 2
+        for (int i = 0; walk && i < kScS; i += 2) {
+          const float4 vn = *reinterpret_cast<const float4 *>(xn + i);
+          const float4 vr = *reinterpret_cast<const float4 *>(xr + i);
+          const float4 vm = *reinterpret_cast<const float4 *>(xm + i);
 #pragma unroll
-          for (int q = 0; q < CPT; q++) {
-            const int64_t col = (int64_t)tid * CPT + q;
-            if (col >= RL) continue;
-            const int64_t n = rw * RL + col;
-            const double Pre = rp_re[q] + (rtp_re - rpp_re[q]);
-            const double Pim = rp_im[q] + (rtp_im - rpp_im[q]);
-            const double R = 0.5 * (rp_z[q] + rtz1 + (rtz2 - rpz2[q]));
+          for (int h = 0; h < 2; h++) {
+            const float2 n_ = h ? make_float2(vn.z, vn.w) : make_float2(vn.x, vn.y);
+            const float2 r_ = h ? make_float2(vr.z, vr.w) : make_float2(vr.x, vr.y);
+            const float2 m_ = h ? make_float2(vm.z, vm.w) : make_float2(vm.x, vm.y);
+            const float2 pn = cj_mul(r_, n_), pl = cj_mul(m_, r_);
+            const float zn = n_.x * n_.x + n_.y * n_.y, zl = m_.x * m_.x + m_.y * m_.y;
+            Pre += (double)pn.x - (double)pl.x;
+            Pim += (double)pn.y - (double)pl.y;
+            Z += (double)zn - (double)zl;
+            C += ((zn != 0.0f) ? 1.0 : 0.0) - ((zl != 0.0f) ? 1.0 : 0.0);
+            const int64_t n = sb + i + h;
             bool b = false;
-            if (n >= 0 && n < L && R > 0.0) {
-              const double y = (Pre * Pre + Pim * Pim) / (R * R);
-              if (fabs(y - a.thr) <= a.band) {   // defer to the exact fp32 recompute
+            if (n >= 0 && n < L && C > 0.5) {
+              const double R = 0.5 * Z, R2 = R * R;
+              const double q = Pre * Pre + Pim * Pim - a.thr * R2;
+              if (fabs(q) <= a.band * R2 || Z <= zfloor) {
                 const int slot = atomicAdd(&s_namb, 1);
                 if (slot < kAmbMax) {
                   amb_n[slot] = n;
-                  atomicMin(&s_nmin, (unsigned long long)n);
-                  atomicMax(&s_nmax, (unsigned long long)n);
-                  has_amb = 1;
+                  amb_pos[slot] = n;
+                  amb_s[slot] = (uint8_t)s;
+                  b = true;
                 } else {
-                  b = (double)sc_exact(x, n, a.M) > a.thr;   // overflow: lane alone
+                  ovf |= 1u << (i + h);   // list full: this lane recomputes it below
                 }
               } else {
-                b = y > a.thr;
+                b = q > 0.0;
               }
             }
-            bflag[n - wb0] = b ? 1 : 0;
+            bits |= (b ? 1u : 0u) << (i + h);
           }
         }
-        if (__syncthreads_or(has_amb)) {   // block-uniform
-          const int namb = s_namb < kAmbMax ? s_namb : kAmbMax;
-          const int64_t nmin = (int64_t)s_nmin;
-          const int64_t w0 = nmin - (int64_t)a.M + 1;
-          const int W = (int)((int64_t)s_nmax - nmin) + (int)a.M;
-          for (int i = tid; i < W; i += kScT) {
-            const int64_t k = w0 + i;
-            stage[i] = (k >= 0 && k < L) ? x[k] : make_float2(0.0f, 0.0f);
-          }
-          __syncthreads();
-          if (tid < namb) {
-            const int64_t n = amb_n[tid];
-            const float y32 = sc_exact_lds(stage + (n - nmin), (int)a.M);
-            bflag[n - wb0] = ((double)y32 > a.thr) ? 1 : 0;
-          }
-          if (tid == 0 && a.n_exact) atomicAdd(a.n_exact, (unsigned long long)namb);
-          __syncthreads();
-          if (tid == 0) { s_namb = 0; s_nmin = ~0ull; s_nmax = 0ull; }
+        while (ovf) {   // overflow of the provisional list (pathological input): exact here
+          const int i = __ffs((int)ovf) - 1;
+          ovf &= ovf - 1u;
+          if (!((double)sc_exact(x, sb + i, a.M) > a.thr)) bits &= ~(1u << i);
+          if (a.n_exact) atomicAdd(a.n_exact, 1ull);
         }
+        Pc_re += tot[0]; Pc_im += tot[1]; Zc += tot[2]; Cc += tot[3]; Ac = Aend;
+        wbits[((int)s * kScIters + it) * kScT + tid] = (uint16_t)bits;
+        { const long long t2 = clock64(); t_ph[3] += t2 - t_m; t_m = t2; }
+        const uint32_t cond = run_cond(bits, sb, carry, cp, run_ws[par]);
+        // candidates only inside [c0, cend)
+        const int64_t lo = c0 - sb, hi = cend - sb;
+        uint32_t mask = 0;
+        if (hi > 0 && lo < kScS) {
+          const int l = lo < 0 ? 0 : (int)lo, u = hi > kScS ? kScS : (int)hi;
+          mask = ((1u << u) - 1u) & ~((1u << l) - 1u);
+        }
+        acond[it][tid] = (uint16_t)(acond[it][tid] & cond & mask);
+        { const long long t2 = clock64(); t_ph[4] += t2 - t_m; t_m = t2; }
+      }
+      const long long t_r1 = clock64();
+      t_rows += t_r1 - t_r0;
+      int surv = 0;
 #pragma unroll
-        for (int q = 0; q < CPT; q++) {
-          rpz2[q] = rpz1[q];
-          rpz1[q] = rp_z[q];
-          rpp_re[q] = rp_re[q];
-          rpp_im[q] = rp_im[q];
-          xprev[q] = xc[q];
+      for (int it = 0; it < kScIters; it++) surv |= (acond[it][tid] != 0);
+      any = __syncthreads_or(surv);
+      n_done = s + 1;
+      t_words += clock64() - t_r1;
+    }
+
+    const int namb = s_namb < kAmbMax ? s_namb : kAmbMax;
+    const long long t_res0 = clock64();
+    if (any && namb > 0) {
+      // exact fp32 recompute of the provisional bits, a batch per (antenna, LDS window). The
+      // oracle's per-sample terms -pr, -pi (P taps -1) and 0.5|x|^2 (R taps 0.5) are tabled
+      // once per window (the same fp32 operations); each sample's three sequential sums then
+      // run on two lanes (R; Pr+Pi interleaved), oldest -> newest exactly as framing.cc does.
+      if (a.n_exact && tid == 0) atomicAdd(a.n_exact, (unsigned long long)namb);
+      const int WCAP = (int)((sizeof(float2) * ring_pad(RING)) / 12) & ~3;
+      float *tz = reinterpret_cast<float *>(sc_dyn);
+      float2 *tp = reinterpret_cast<float2 *>(sc_dyn + sizeof(float) * WCAP);
+      for (;;) {
+        if (tid == 0) { s_key = ~0ull; s_ng = 0; }
+        __syncthreads();
+        for (int i = tid; i < namb; i += kScT)
+          if (amb_n[i] >= 0)
+            atomicMin(&s_key, ((unsigned long long)amb_s[i] << 48) | (unsigned long long)amb_n[i]);
+        __syncthreads();
+        const unsigned long long key = s_key;
+        if (key == ~0ull) break;   // block-uniform
+        const int s = (int)(key >> 48);
+        const int64_t nmin = (int64_t)(key & ((1ull << 48) - 1));
+        const int64_t q0 = nmin - M + 1;       // table index i <-> sample q0 + i
+        const float2 *__restrict__ x = a.iq + ((uint64_t)f * a.N + s) * a.stride;
+        for (int i = tid; i < WCAP; i += kScT) {
+          const int64_t k = q0 + i;
+          const float2 v = (k >= 0 && k < L) ? x[k] : make_float2(0.0f, 0.0f);
+          const float2 dd = (k - RL >= 0 && k - RL < L) ? x[k - RL] : make_float2(0.0f, 0.0f);
+          float z = v.x * v.x + v.y * v.y;
+          tz[i] = 0.5f * z;
+          const float2 pp = cj_mul(dd, v);
+          tp[i] = make_float2((-1.0f) * pp.x, (-1.0f) * pp.y);
         }
-        rtz2 = rtz1; rtz1 = tz; rtp_re = tre; rtp_im = tim;
-      }
-      __syncthreads();
-      for (int w = tid; w < nwords; w += kScT) {
-        uint64_t v = 0;
-        const uint32_t *bw = reinterpret_cast<const uint32_t *>(bflag + w * 64);
-#pragma unroll
-        for (int i = 0; i < 16; i++) {
-          uint32_t q4 = bw[i];  // four 0/1 bytes
-          v |= (uint64_t)((q4 & 1u) | ((q4 >> 7) & 2u) | ((q4 >> 14) & 4u) | ((q4 >> 21) & 8u))
-               << (4 * i);
-        }
-        words[s][w] = v;
-      }
-      __syncthreads();
-      // last-zero prefix max over words (wave 0); positions before pos0 read as zero
-      if (wv == 0) {
-        const int per = (nwords + 63) / 64;
-        long long run = -1;
-        for (int k = 0; k < per; k++) {
-          const int w = lane * per + k;
-          if (w < nwords) {
-            const uint64_t inv = ~words[s][w];
-            const long long lzw = inv ? (long long)(wb0 + 64 * w + 63 - __clzll(inv)) : -1;
-            run = lzw > run ? lzw : run;
-            lzp[w] = run;
+        // this window's samples (at most kResGroup per pass; the rest wait for the next pass)
+        for (int i = tid; i < namb; i += kScT) {
+          const int64_t n = amb_n[i];
+          if (n >= 0 && amb_s[i] == s && n - nmin <= WCAP - M) {
+            const int g = atomicAdd(&s_ng, 1);
+            if (g < kResGroup) { res_i[g] = i; amb_n[i] = -1; }
           }
         }
-        long long inc = run;
+        __syncthreads();
+        const int ng = s_ng < kResGroup ? s_ng : kResGroup;
+        {
+          const int g = lane + 64 * (wv >> 1);
+          if (g < ng) {
+            const int r = (int)(amb_n_val(res_i[g]) - nmin);
+            if ((wv & 1) == 0) {          // R over i = r .. r + M - 1
+              const float *q = tz + r;
+              float R = 0.0f;
+#pragma unroll 8
+              for (int k = 0; k < M; k++) R = R + q[k];
+              res_v[0][g] = R;
+            } else {                      // P over i = r + M/2 .. r + M - 1
+              const float2 *q = tp + r + RL;
+              float Pr = 0.0f, Pi = 0.0f;
+#pragma unroll 8
+              for (int k = 0; k < RL; k++) { const float2 t = q[k]; Pr = Pr + t.x; Pi = Pi + t.y; }
+              res_v[1][g] = Pr;
+              res_v[2][g] = Pi;
+            }
+          }
+        }
+        __syncthreads();
+        if (tid < ng) {
+          const float Pr = res_v[1][tid], Pi = res_v[2][tid], R = res_v[0][tid];
+          const float y32 = (Pr * Pr + Pi * Pi) / (R * R);
+          if (!((double)y32 > a.thr)) {
+            const int64_t o = amb_n_val(res_i[tid]) - w0;
+            const int it = (int)(o / kScIt), t = (int)((o % kScIt) / kScS);
+            const int bit = (int)(o % kScS) + 16 * (t & 1);
+            uint32_t *w32 = reinterpret_cast<uint32_t *>(wbits) +
+                            ((s * kScIters + it) * kScT + t) / 2;
+            atomicAnd(w32, ~(1u << bit));
+          }
+        }
+        __syncthreads();
+      }
+      // plateau rule again from the corrected bits
 #pragma unroll
-        for (int off = 1; off < 64; off <<= 1) {
-          long long o = __shfl_up(inc, off);
-          if (lane >= off && o > inc) inc = o;
-        }
-        long long excl = __shfl_up(inc, 1);
-        if (lane == 0) excl = -1;
-        for (int k = 0; k < per; k++) {
-          const int w = lane * per + k;
-          if (w < nwords && excl > lzp[w]) lzp[w] = excl;
+      for (int it = 0; it < kScIters; it++) acond[it][tid] = 0xFFFFu;
+      for (uint32_t s = 0; s < n_done; s++) {
+        long long carry = w0 - 1;
+#pragma unroll 1
+        for (int it = 0; it < kScIters; it++) {
+          const int64_t sb = w0 + (int64_t)it * kScIt + kScS * tid;
+          const uint32_t bits = wbits[((int)s * kScIters + it) * kScT + tid];
+          par ^= 1;
+          const uint32_t cond = run_cond(bits, sb, carry, cp, run_ws[par]);
+          const int64_t lo = c0 - sb, hi = cend - sb;
+          uint32_t mask = 0;
+          if (hi > 0 && lo < kScS) {
+            const int l = lo < 0 ? 0 : (int)lo, u = hi > kScS ? kScS : (int)hi;
+            mask = ((1u << u) - 1u) & ~((1u << l) - 1u);
+          }
+          acond[it][tid] = (uint16_t)(acond[it][tid] & cond & mask);
         }
       }
-      __syncthreads();
-      int nz = 0;
-      for (int ow = tid; ow < kScChunk / 64; ow += kScT) {
-        const int64_t wn = wofs + ow;
-        const uint64_t word = words[s][wn];
-        const long long prevlz = (wn > 0) ? lzp[wn - 1] : -1;
-        uint64_t cw = 0;
-        for (int i = 0; i < 64; i++) {
-          const int64_t n = c0 + 64 * ow + i;
-          const uint64_t m = ~word & ((2ull << i) - 1ull);
-          const long long lzv = m ? (long long)(wb0 + 64 * wn + 63 - __clzll(m)) : prevlz;
-          if (n < L && lzv <= n - cp - 2) cw |= 1ull << i;
-        }
-        const uint64_t v = allcond[ow] & cw;
-        allcond[ow] = v;
-        nz |= (v != 0ull);
-      }
-      any = __syncthreads_or(nz);   // no qualifying sample left: skip remaining antennas
+      int surv = 0;
+#pragma unroll
+      for (int it = 0; it < kScIters; it++) surv |= (acond[it][tid] != 0);
+      any = __syncthreads_or(surv);
+    }
+    if (a.prof && tid == 0) {
+      const long long t_end = clock64();
+      atomicAdd(&a.prof[0], 1ull);
+      atomicAdd(&a.prof[1], (unsigned long long)n_done);
+      atomicAdd(&a.prof[2], (unsigned long long)t_rows);
+      atomicAdd(&a.prof[3], (unsigned long long)t_words);
+      for (int k = 0; k < 5; k++) atomicAdd(&a.prof[12 + k], (unsigned long long)t_ph[k]);
+      atomicAdd(&a.prof[4], (unsigned long long)(t_end - t_res0));
+      atomicAdd(&a.prof[5], (unsigned long long)(t_end - t_item));
+      const long long w_end = wall_clock64();
+      atomicAdd(&a.prof[7], (unsigned long long)(w_end - w_item));
+      atomicMax(&a.prof[10], (unsigned long long)(w_end - w_item));
+      atomicMax(&a.prof[11], (unsigned long long)w_item);
     }
     if (any) {
-      for (int ow = tid; ow < kScChunk / 64; ow += kScT) {
-        const uint64_t v = allcond[ow];
-        if (v) atomicMin(&s_min, (unsigned long long)(c0 + 64 * ow + __ffsll((long long)v) - 1));
+#pragma unroll
+      for (int it = 0; it < kScIters; it++) {
+        const uint32_t v = acond[it][tid];
+        if (v)
+          atomicMin(&s_min, (unsigned long long)(w0 + (int64_t)it * kScIt + kScS * tid +
+                                                 __ffs((int)v) - 1));
       }
       __syncthreads();
       const unsigned long long cand = s_min;
@@ -332,20 +586,24 @@ __global__ __launch_bounds__(kScT) void sc_kernel(ScArgs a) {
           bool found = false;
           if (lane < (int)a.N) {
             const int s = lane;
-            const int64_t n = (int64_t)cand;
-            int64_t wn = (n - wb0) / 64;
-            const int64_t i = (n - wb0) % 64;
-            uint64_t m = ~words[s][wn] & ((1ull << i) - 1ull);
-            while (!m && wn > 0) m = ~words[s][--wn];   // rare: only for a candidate chunk
-            const long long lzv = m ? (long long)(wb0 + 64 * wn + 63 - __clzll(m)) : -1;
-            found = lzv >= pos0;    // a computed zero, not the halo padding
+            const int64_t o = (int64_t)cand - w0;
+            int it = (int)(o / kScIt), t = (int)((o % kScIt) / kScS);
+            const int i = (int)(o % kScS);
+            uint32_t m = ~(uint32_t)wbits[(s * kScIters + it) * kScT + t] & ((1u << i) - 1u);
+            while (!m) {   // rare: only for a candidate item
+              if (--t < 0) { t = kScT - 1; if (--it < 0) break; }
+              m = ~(uint32_t)wbits[(s * kScIters + it) * kScT + t] & 0xFFFFu;
+            }
+            const long long lzv =
+                m ? (long long)(w0 + (int64_t)it * kScIt + kScS * t + 31 - __clz(m)) : -1;
+            found = lzv >= w0;    // a computed zero, not the halo boundary
             rec->start[s] = found ? (unsigned long long)(lzv + 1) : 0ull;
           }
           const unsigned long long fm = __ballot(found);
           if (lane == 0) {
             rec->found = (uint32_t)fm;
             rec->n_cand = cand;
-            rec->pos0 = pos0;
+            rec->pos0 = w0;
             atomicMin(&a.trig[f], cand);
           }
         }
@@ -374,7 +632,7 @@ __global__ __launch_bounds__(64) void plateau_kernel(PlateauArgs a) {
     }
     return;
   }
-  const ScRecord &rec = a.rec[(uint64_t)f * a.rec_stride + n / kScChunk];
+  const ScRecord &rec = a.rec[(uint64_t)f * a.rec_stride + n / a.chunk_len];
   uint64_t sum = 0;
   for (uint32_t s = 0; s < a.N; s++) {
     int64_t start = 0;
@@ -425,13 +683,28 @@ __global__ __launch_bounds__(64) void plateau_kernel(PlateauArgs a) {
   }
 }
 
-void launch_sc(const ScArgs &a, uint32_t n_frames, uint32_t grid_x, hipStream_t s) {
-  dim3 grid(grid_x, n_frames);
-  const uint32_t RL = a.M / 2;
-  if (RL <= 256) hipLaunchKernelGGL(sc_kernel<1>, grid, dim3(kScT), 0, s, a);
-  else if (RL <= 512) hipLaunchKernelGGL(sc_kernel<2>, grid, dim3(kScT), 0, s, a);
-  else if (RL <= 1024) hipLaunchKernelGGL(sc_kernel<4>, grid, dim3(kScT), 0, s, a);
-  else hipLaunchKernelGGL(sc_kernel<8>, grid, dim3(kScT), 0, s, a);
+size_t sc_lds_bytes(uint32_t M, uint32_t N) {
+  const int ring = (int)M + kScIt;
+  return sizeof(float2) * (size_t)(ring + ((ring >> 5) << 1)) +
+         sizeof(uint16_t) * (size_t)N * kScIters * kScT;
+}
+
+void launch_sc(const ScArgs &a, uint32_t n_frames, uint32_t n_cu, hipStream_t s) {
+  const size_t shm = sc_lds_bytes(a.M, a.N);
+  static size_t set_shm = 0;
+  static int per_cu = 0;
+  if (shm != set_shm) {
+    (void)hipFuncSetAttribute((const void *)sc_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)shm);
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, sc_kernel, kScT, shm) !=
+            hipSuccess || per_cu < 1)
+      per_cu = 1;
+    set_shm = shm;
+  }
+  const uint64_t total = (a.chunk_hi - a.chunk_lo) * (uint64_t)n_frames;
+  const uint32_t grid = (uint32_t)std::min<uint64_t>(total, (uint64_t)n_cu * per_cu);
+  if (grid) hipLaunchKernelGGL(sc_kernel, dim3(grid), dim3(kScT), shm, s, a, n_frames);
+  if (a.prof) fprintf(stderr, "sc grid %u (per_cu %d, n_cu %u, lds %zu)\n", grid, per_cu, n_cu, shm);
 }
 
 void launch_plateau(const PlateauArgs &a, uint32_t n_frames, hipStream_t s) {
