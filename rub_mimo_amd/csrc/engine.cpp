@@ -220,7 +220,9 @@ struct mimo_rx {
   DevBuf<float> gain;
   DevBuf<double> nvp, evm_part, evm_out;
   DevBuf<unsigned long long> n_exact;   // S&C exact fp32 recomputes (diagnostic)
-  DevBuf<uint32_t> queue;               // S&C work-queue head
+  DevBuf<uint32_t> queue;               // S&C work-queue head, hot-item count
+  DevBuf<ScHot> hot;                    // S&C items awaiting exact resolution
+  uint32_t cap_hot = 0;
   DevBuf<unsigned long long> sc_prof;   // RMIMO_SC_PROF=1 cycle counters
   uint32_t last_frames = 0, last_max_out = 0;
   // streaming state (facade)
@@ -286,6 +288,16 @@ int ensure_workspace(mimo_rx *h, uint32_t F, uint64_t chunks, uint64_t evm_entri
   return MIMO_OK;
 }
 
+// Decision band of the fp64 S&C metric: a first-order bound on |y_fp32 - y| for the oracle's
+// sequential fp32 sums (framing.cc:626-637), for y <= 1 (|P| <= R always):
+//   |dy| <= 2 sqrt(2) (M/2 + 2) u sqrt(y) + 2 (M + 1) u y + 4 u y,   u = 2^-24,
+// with a 25% margin for the neglected O((M u)^2) terms. Outside the band the fp64 decision
+// equals the oracle's; inside it the sample is recomputed exactly.
+static double sc_band(uint32_t M) {
+  const double u = 0x1p-24;
+  return 1.25 * u * (std::sqrt(2.0) * (M + 4.0) + 2.0 * M + 6.0);
+}
+
 // S&C + plateau over chunks [chunk_lo, end) of every frame
 int run_sync(mimo_rx *h, const float2 *iq, uint64_t stride, uint32_t F, uint64_t frame_len,
              uint64_t chunk_lo, bool reset_trig, hipStream_t s) {
@@ -300,8 +312,9 @@ int run_sync(mimo_rx *h, const float2 *iq, uint64_t stride, uint32_t F, uint64_t
     a.N = h->N; a.M = h->M; a.cp = h->cp;
     // diagnostics only: RMIMO_SC_BAND overrides the exact-recompute band (a band below the
     // fp32 error bound breaks parity)
-    static const double band_env = [] { const char *e = getenv("RMIMO_SC_BAND"); return e ? atof(e) : 2e-3; }();
-    a.thr = h->thr; a.band = band_env;
+    static const double band_env = [] { const char *e = getenv("RMIMO_SC_BAND"); return e ? atof(e) : -1.0; }();
+    a.thr = h->thr;
+    a.band = band_env >= 0.0 ? band_env : sc_band(h->M);
     a.chunk_len = K; a.chunk_lo = chunk_lo; a.chunk_hi = nchunks;
     a.trig = h->trig.p; a.rec = h->rec.p; a.rec_stride = h->cap_chunks;
     if (!h->n_exact.p) {
@@ -309,21 +322,30 @@ int run_sync(mimo_rx *h, const float2 *iq, uint64_t stride, uint32_t F, uint64_t
       HIPCHK(hipMemsetAsync(h->n_exact.p, 0, sizeof(unsigned long long), s));
     }
     a.n_exact = h->n_exact.p;
-    if (!h->queue.p) HIPCHK(h->queue.ensure(1));
-    HIPCHK(hipMemsetAsync(h->queue.p, 0, sizeof(uint32_t), s));
+    if (!h->queue.p) HIPCHK(h->queue.ensure(2));
+    HIPCHK(hipMemsetAsync(h->queue.p, 0, 2 * sizeof(uint32_t), s));
     a.queue = h->queue.p;
+    a.hot_count = h->queue.p + 1;
+    const uint32_t hot_cap = 8 * F + 32;
+    if (hot_cap > h->cap_hot) {
+      HIPCHK(h->hot.ensure(hot_cap));
+      h->cap_hot = hot_cap;
+    }
+    a.hot = h->hot.p;
+    a.hot_cap = hot_cap;
     static const bool prof_env = [] { const char *e = getenv("RMIMO_SC_PROF"); return e && e[0] == '1'; }();
     if (prof_env) {
-      if (!h->sc_prof.p) HIPCHK(h->sc_prof.ensure(17));
-      HIPCHK(hipMemsetAsync(h->sc_prof.p, 0, 17 * sizeof(unsigned long long), s));
+      if (!h->sc_prof.p) HIPCHK(h->sc_prof.ensure(20));
+      HIPCHK(hipMemsetAsync(h->sc_prof.p, 0, 20 * sizeof(unsigned long long), s));
       HIPCHK(hipMemsetAsync(h->sc_prof.p + 8, 0xFF, sizeof(unsigned long long), s));
       a.prof = h->sc_prof.p;
     }
     hipEvent_t e = h->timer.begin(s);
     launch_sc(a, F, h->n_cu, s);
+    launch_sc_hot(a, s);
     h->timer.end(0, e, s);
     if (prof_env) {   // diagnostics: per-item cycle split of the S&C kernel
-      unsigned long long v[17];
+      unsigned long long v[20];
       HIPCHK(hipMemcpyAsync(v, h->sc_prof.p, sizeof(v), hipMemcpyDeviceToHost, s));
       HIPCHK(hipStreamSynchronize(s));
       const double it = v[0] ? (double)v[0] : 1.0;
@@ -332,8 +354,10 @@ int run_sync(mimo_rx *h, const float2 *iq, uint64_t stride, uint32_t F, uint64_t
               "last_start_us %.2f\n", v[0], v[6], v[1],
               v[2] / it, v[3] / it, v[4] / it, v[5] / it, v[7] / it / 100.0,
               (double)(v[9] - v[8]) / 100.0, v[10] / 100.0, (double)(v[11] - v[8]) / 100.0);
-      fprintf(stderr, "sc_prof phases/item warm %.0f A %.0f scan %.0f B %.0f run %.0f\n",
-              v[12] / it, v[13] / it, v[14] / it, v[15] / it, v[16] / it);
+      fprintf(stderr, "sc_prof phases/item warm %.0f A %.0f scan %.0f B %.0f run %.0f | resolve "
+              "passes %llu chain cycles/pass %.0f samples/pass %.1f\n",
+              v[12] / it, v[13] / it, v[14] / it, v[15] / it, v[16] / it, v[17],
+              v[17] ? (double)v[18] / v[17] : 0.0, v[17] ? (double)v[19] / v[17] : 0.0);
     }
   }
   PlateauArgs pa{};

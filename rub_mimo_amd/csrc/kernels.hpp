@@ -16,6 +16,29 @@ struct ScRecord {             // a chunk's trigger candidate and the run starts 
   uint32_t found;             // bit s: start[s] is final (a zero bit inside the chunk)
   uint32_t pad;
 };
+// an S&C work item spans kScSpan positions: a halo of >= cp+2 (run history, multiple of 16)
+// and the chunk's candidate positions; 256 threads own 16 positions each per 4096-position
+// iteration
+constexpr int kScSpan = 16384;
+constexpr int kScThreads = 256;
+constexpr int kScIterLen = 4096;
+constexpr int kScAmbMax = 256;   // near-threshold samples deferred per item
+inline uint64_t sc_chunk_len(uint32_t cp) { return kScSpan - ((uint64_t)cp + 2 + 15) / 16 * 16; }
+size_t sc_lds_bytes(uint32_t M, uint32_t N);
+size_t sc_table_bytes(uint32_t M);
+
+// an item whose plateau candidates hinge on near-threshold samples, handed from the item
+// kernel to the resolve and finalize kernels
+struct ScHot {
+  uint32_t f, n_done, namb, pad;
+  uint64_t chunk;
+  int64_t c0, w0, cend;
+  int64_t lo[kMaxStreams];                          // first evaluated position per antenna
+  int64_t amb_n[kScAmbMax];
+  uint8_t amb_s[kScAmbMax];
+  uint16_t wbits[kMaxStreams * (kScSpan / kScIterLen) * kScThreads];
+};
+
 struct ScArgs {
   const float2 *iq;
   uint64_t stride;          // complex samples between antenna arrays
@@ -28,17 +51,16 @@ struct ScArgs {
   ScRecord *rec;            // [F][rec_stride] per-chunk candidates
   uint64_t rec_stride;
   unsigned long long *n_exact;  // count of exact fp32 recomputes (null: not counted)
-  uint32_t *queue;          // work-queue head, zeroed before each launch
+  uint32_t *queue;          // [0] work-queue head, [1] hot-item count; zeroed before launch
+  uint32_t *hot_count;
+  ScHot *hot;               // [hot_cap] (null: resolve inside the item kernel)
+  uint32_t hot_cap;
   unsigned long long *prof; // diagnostics: [items, antenna passes, row, words, resolve, total
                             // cycles, skipped items] (null: off)
 };
-// an S&C work item spans kScSpan positions: a halo of >= cp+2 (run history, multiple of 16)
-// and the chunk's candidate positions
-constexpr int kScSpan = 16384;
-inline uint64_t sc_chunk_len(uint32_t cp) { return kScSpan - ((uint64_t)cp + 2 + 15) / 16 * 16; }
-size_t sc_lds_bytes(uint32_t M, uint32_t N);
 // persistent grid of n_cu x (resident blocks per CU) over the F x chunks items
 void launch_sc(const ScArgs &a, uint32_t n_frames, uint32_t n_cu, hipStream_t s);
+void launch_sc_hot(const ScArgs &a, hipStream_t s);   // resolve + finalize the hot items
 
 struct PlateauArgs {
   const unsigned long long *trig;

@@ -44,13 +44,21 @@
 
 #pragma clang fp contract(off)
 
+// cycle counters of the item kernel (build with -DMIMO_SC_PROFILE and run with RMIMO_SC_PROF=1)
+#ifdef MIMO_SC_PROFILE
+#define SC_PROF(...) __VA_ARGS__
+#else
+#define SC_PROF(...)
+#endif
+
 namespace mimo {
 
-constexpr int kScT = 256;               // threads per workgroup
+constexpr int kScT = kScThreads;        // threads per workgroup
 constexpr int kScS = 16;                // consecutive positions per thread per iteration
 constexpr int kScIt = kScT * kScS;      // 4096 positions per iteration
 constexpr int kScIters = kScSpan / kScIt;
-constexpr int kAmbMax = 256;            // provisional samples per item
+constexpr int kAmbMax = kScAmbMax;      // provisional samples per item
+static_assert(kScIt == kScIterLen, "iteration length");
 constexpr int kResGroup = kScT / 2;     // samples per resolve pass (two lanes each)
 static_assert(kScSpan % kScIt == 0, "item span");
 
@@ -197,6 +205,56 @@ MIMO_DEV uint32_t run_cond(uint32_t bits, int64_t sb, long long &carry, int64_t 
   return cond;
 }
 
+// sequential fp32 sum q[0] + q[1] + ... + q[n-1], in that order. Scalar head up to 16-byte
+// alignment, then 16-byte reads with the next 16 terms in flight while 16 are added (the
+// dependent-add latency, ~7 cycles on gfx950, is the bound: ~9 cycles per term measured).
+MIMO_DEV float seq_sum(const float *q, int n) {
+  float acc = 0.0f;
+  const int h = min(n, (int)((4u - (((uint32_t)(uintptr_t)q >> 2) & 3u)) & 3u));
+  for (int k = 0; k < h; k++) acc = acc + q[k];
+  const float4 *qa = reinterpret_cast<const float4 *>(q + h);
+  const int m = n - h, nb = m >> 4;
+  if (nb > 0) {
+    float4 n0 = qa[0], n1 = qa[1], n2 = qa[2], n3 = qa[3];
+    for (int b = 0; b < nb; b++) {
+      const float4 c0 = n0, c1 = n1, c2 = n2, c3 = n3;
+      if (b + 1 < nb) {
+        n0 = qa[4 * b + 4]; n1 = qa[4 * b + 5]; n2 = qa[4 * b + 6]; n3 = qa[4 * b + 7];
+      }
+      acc = acc + c0.x; acc = acc + c0.y; acc = acc + c0.z; acc = acc + c0.w;
+      acc = acc + c1.x; acc = acc + c1.y; acc = acc + c1.z; acc = acc + c1.w;
+      acc = acc + c2.x; acc = acc + c2.y; acc = acc + c2.z; acc = acc + c2.w;
+      acc = acc + c3.x; acc = acc + c3.y; acc = acc + c3.z; acc = acc + c3.w;
+    }
+  }
+  for (int k = h + 16 * nb; k < n; k++) acc = acc + q[k];
+  return acc;
+}
+
+// two interleaved sequential sums over complex terms (the .x and .y chains), same scheme
+MIMO_DEV float2 seq_sum2(const float2 *q, int n) {
+  float ax = 0.0f, ay = 0.0f;
+  const int h = min(n, (int)((((uint32_t)(uintptr_t)q) >> 3) & 1u));
+  for (int k = 0; k < h; k++) { ax = ax + q[k].x; ay = ay + q[k].y; }
+  const float4 *qa = reinterpret_cast<const float4 *>(q + h);
+  const int m = n - h, nb = m >> 3;
+  if (nb > 0) {
+    float4 n0 = qa[0], n1 = qa[1], n2 = qa[2], n3 = qa[3];
+    for (int b = 0; b < nb; b++) {
+      const float4 c0 = n0, c1 = n1, c2 = n2, c3 = n3;
+      if (b + 1 < nb) {
+        n0 = qa[4 * b + 4]; n1 = qa[4 * b + 5]; n2 = qa[4 * b + 6]; n3 = qa[4 * b + 7];
+      }
+      ax = ax + c0.x; ay = ay + c0.y; ax = ax + c0.z; ay = ay + c0.w;
+      ax = ax + c1.x; ay = ay + c1.y; ax = ax + c1.z; ay = ay + c1.w;
+      ax = ax + c2.x; ay = ay + c2.y; ax = ax + c2.z; ay = ay + c2.w;
+      ax = ax + c3.x; ay = ay + c3.y; ax = ax + c3.z; ay = ay + c3.w;
+    }
+  }
+  for (int k = h + 8 * nb; k < n; k++) { ax = ax + q[k].x; ay = ay + q[k].y; }
+  return make_float2(ax, ay);
+}
+
 // two consecutive samples (q even), zero outside [0, L)
 MIMO_DEV float4 ld_pair(const float2 *__restrict__ x, int64_t q, int64_t L, bool vec) {
   if (vec && q >= 0 && q + 1 < L) return *reinterpret_cast<const float4 *>(x + q);
@@ -222,7 +280,168 @@ MIMO_DEV float2 cj_mul(float2 d, float2 v) {
   return make_float2(d.x * v.x - (-d.y) * v.y, d.x * v.y + (-d.y) * v.x);
 }
 
-__global__ __launch_bounds__(kScT) void sc_kernel(ScArgs a, uint32_t n_frames) {
+struct ResolveLds {            // LDS scratch of the exact recompute
+  unsigned long long key;
+  int ng;
+  int res_i[kResGroup];
+  float res_v[3][kResGroup];
+};
+
+// Exact fp32 recompute of the pending samples pos[i] (antenna ant[i]; pos0 keeps the
+// positions, pos[i] becomes -1 once taken), a batch per (antenna, table window). The oracle's
+// per-sample terms -pr, -pi (P taps -1) and 0.5|x|^2 (R taps 0.5) are tabled once per window
+// with the same fp32 operations; each sample's three sequential sums then run on two lanes
+// (R; Pr and Pi interleaved), oldest -> newest exactly as framing.cc:626-637 under the pinned
+// liquid semantics. A sample whose exact metric fails the threshold clears its bit in wbits
+// ([antenna][iteration][thread] x 16 bits, LDS or global).
+MIMO_DEV void resolve_pending(const ScArgs &a, uint32_t f, int64_t w0, long long *pos,
+                              const long long *pos0, const uint8_t *ant, int namb,
+                              uint16_t *wbits, unsigned char *tables, int table_bytes,
+                              ResolveLds &rl) {
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int M = (int)a.M, RL = M / 2;
+  const int64_t L = (int64_t)a.frame_len;
+  const int WCAP = (table_bytes / 12) & ~3;
+  float *tz = reinterpret_cast<float *>(tables);
+  float2 *tp = reinterpret_cast<float2 *>(tables + sizeof(float) * WCAP);
+  for (;;) {
+    if (tid == 0) { rl.key = ~0ull; rl.ng = 0; }
+    __syncthreads();
+    for (int i = tid; i < namb; i += kScT)
+      if (pos[i] >= 0)
+        atomicMin(&rl.key, ((unsigned long long)ant[i] << 48) | (unsigned long long)pos[i]);
+    __syncthreads();
+    const unsigned long long key = rl.key;
+    if (key == ~0ull) break;   // block-uniform
+    const int s = (int)(key >> 48);
+    const int64_t nmin = (int64_t)(key & ((1ull << 48) - 1));
+    const int64_t q0 = nmin - M + 1;       // table index i <-> sample q0 + i
+    const float2 *__restrict__ x = a.iq + ((uint64_t)f * a.N + s) * a.stride;
+    for (int i = tid; i < WCAP; i += kScT) {
+      const int64_t k = q0 + i;
+      const float2 v = (k >= 0 && k < L) ? x[k] : make_float2(0.0f, 0.0f);
+      const float2 dd = (k - RL >= 0 && k - RL < L) ? x[k - RL] : make_float2(0.0f, 0.0f);
+      float z = v.x * v.x + v.y * v.y;
+      tz[i] = 0.5f * z;
+      const float2 pp = cj_mul(dd, v);
+      tp[i] = make_float2((-1.0f) * pp.x, (-1.0f) * pp.y);
+    }
+    // this window's samples (at most kResGroup per pass; the rest wait for the next pass)
+    for (int i = tid; i < namb; i += kScT) {
+      const int64_t n = pos[i];
+      if (n >= 0 && ant[i] == s && n - nmin <= WCAP - M) {
+        const int g = atomicAdd(&rl.ng, 1);
+        if (g < kResGroup) { rl.res_i[g] = i; pos[i] = -1; }
+      }
+    }
+    __syncthreads();
+    const int ng = rl.ng < kResGroup ? rl.ng : kResGroup;
+    {
+      const int g = lane + 64 * (wv >> 1);
+      if (g < ng) {
+        const int r = (int)(pos0[rl.res_i[g]] - nmin);
+        if ((wv & 1) == 0) {          // R over i = r .. r + M - 1
+          rl.res_v[0][g] = seq_sum(tz + r, M);
+        } else {                      // P over i = r + M/2 .. r + M - 1
+          const float2 P = seq_sum2(tp + r + RL, RL);
+          rl.res_v[1][g] = P.x;
+          rl.res_v[2][g] = P.y;
+        }
+      }
+    }
+    __syncthreads();
+    if (tid < ng) {
+      const float Pr = rl.res_v[1][tid], Pi = rl.res_v[2][tid], R = rl.res_v[0][tid];
+      const float y32 = (Pr * Pr + Pi * Pi) / (R * R);
+      if (!((double)y32 > a.thr)) {
+        const int64_t o = pos0[rl.res_i[tid]] - w0;
+        const int it = (int)(o / kScIt), t = (int)((o % kScIt) / kScS);
+        const int bit = (int)(o % kScS) + 16 * (t & 1);
+        uint32_t *w32 = reinterpret_cast<uint32_t *>(wbits) + ((s * kScIters + it) * kScT + t) / 2;
+        atomicAnd(w32, ~(1u << bit));
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// plateau rule for antennas [0, n_done) from their words into acond (candidates only in
+// [c0, cend)); returns the block-wide OR of the surviving bits
+MIMO_DEV int item_conditions(const uint16_t *wbits, uint16_t (*acond)[kScT], uint32_t n_done,
+                             int64_t w0, int64_t c0, int64_t cend, int64_t cp,
+                             long long (*run_ws)[kScT / 64], int &par) {
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int it = 0; it < kScIters; it++) acond[it][tid] = 0xFFFFu;
+  for (uint32_t s = 0; s < n_done; s++) {
+    long long carry = w0 - 1;
+#pragma unroll 1
+    for (int it = 0; it < kScIters; it++) {
+      const int64_t sb = w0 + (int64_t)it * kScIt + kScS * tid;
+      const uint32_t bits = wbits[((int)s * kScIters + it) * kScT + tid];
+      par ^= 1;
+      const uint32_t cond = run_cond(bits, sb, carry, cp, run_ws[par]);
+      const int64_t lo = c0 - sb, hi = cend - sb;
+      uint32_t mask = 0;
+      if (hi > 0 && lo < kScS) {
+        const int l = lo < 0 ? 0 : (int)lo, u = hi > kScS ? kScS : (int)hi;
+        mask = ((1u << u) - 1u) & ~((1u << l) - 1u);
+      }
+      acond[it][tid] = (uint16_t)(acond[it][tid] & cond & mask);
+    }
+  }
+  int surv = 0;
+#pragma unroll
+  for (int it = 0; it < kScIters; it++) surv |= (acond[it][tid] != 0);
+  return __syncthreads_or(surv);
+}
+
+// first qualifying position -> the chunk's record (run starts from the words) and trig[f].
+// s_min must be ~0 on entry.
+MIMO_DEV void item_record(const ScArgs &a, uint32_t f, uint64_t chunk, int64_t w0,
+                          const uint16_t *wbits, const uint16_t (*acond)[kScT],
+                          const long long *lo_s, unsigned long long &s_min) {
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+#pragma unroll
+  for (int it = 0; it < kScIters; it++) {
+    const uint32_t v = acond[it][tid];
+    if (v)
+      atomicMin(&s_min, (unsigned long long)(w0 + (int64_t)it * kScIt + kScS * tid +
+                                             __ffs((int)v) - 1));
+  }
+  __syncthreads();
+  const unsigned long long cand = s_min;
+  if (cand == ~0ull) return;
+  ScRecord *rec = a.rec + (uint64_t)f * a.rec_stride + chunk;
+  if (wv == 0) {   // run start: one past the last zero below the candidate
+    bool found = false;
+    if (lane < (int)a.N) {
+      const int s = lane;
+      const int64_t o = (int64_t)cand - w0;
+      int it = (int)(o / kScIt), t = (int)((o % kScIt) / kScS);
+      const int i = (int)(o % kScS);
+      uint32_t m = ~(uint32_t)wbits[(s * kScIters + it) * kScT + t] & ((1u << i) - 1u);
+      while (!m) {   // rare: only for a candidate item
+        if (--t < 0) { t = kScT - 1; if (--it < 0) break; }
+        m = ~(uint32_t)wbits[(s * kScIters + it) * kScT + t] & 0xFFFFu;
+      }
+      const long long lzv =
+          m ? (long long)(w0 + (int64_t)it * kScIt + kScS * t + 31 - __clz(m)) : -1;
+      found = lzv >= lo_s[s];    // a computed zero, not the evaluation boundary
+      // found: the run start; otherwise where plateau_kernel's exact backward scan begins
+      rec->start[s] = found ? (unsigned long long)(lzv + 1) : (unsigned long long)lo_s[s];
+    }
+    const unsigned long long fm = __ballot(found);
+    if (lane == 0) {
+      rec->found = (uint32_t)fm;
+      rec->n_cand = cand;
+      rec->pos0 = w0;
+      atomicMin(&a.trig[f], cand);
+    }
+  }
+}
+
+__global__ __launch_bounds__(kScT) __attribute__((amdgpu_waves_per_eu(2))) void sc_kernel(ScArgs a, uint32_t n_frames) {
   extern __shared__ __attribute__((aligned(16))) unsigned char sc_dyn[];
   const int M = (int)a.M, RL = M / 2, RING = M + kScIt;
   float2 *ring = reinterpret_cast<float2 *>(sc_dyn);
@@ -231,29 +450,30 @@ __global__ __launch_bounds__(kScT) void sc_kernel(ScArgs a, uint32_t n_frames) {
   __shared__ uint16_t acond[kScIters][kScT];
   __shared__ double scan_ws[2][5][kScT / 64];
   __shared__ long long run_ws[2][kScT / 64];
-  __shared__ unsigned long long s_trig, s_min, s_key;
+  __shared__ unsigned long long s_trig, s_min;
   __shared__ uint32_t s_item;
   __shared__ long long amb_n[kAmbMax];     // -1 once taken by a resolve pass
   __shared__ long long amb_pos[kAmbMax];
   __shared__ uint8_t amb_s[kAmbMax];
-  __shared__ int s_namb, s_ng;
-  __shared__ int res_i[kResGroup];
-  __shared__ float res_v[3][kResGroup];
-  auto amb_n_val = [&](int i) { return amb_pos[i]; };
+  __shared__ int s_namb;
+  __shared__ uint32_t s_slot;
+  __shared__ ResolveLds rl;
+  __shared__ long long s_lo[kMaxStreams];
+  __shared__ unsigned long long s_smin, s_smax;
 
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int64_t L = (int64_t)a.frame_len, cp = a.cp;
   const int64_t K = (int64_t)a.chunk_len, H = (int64_t)kScSpan - K;
   const uint64_t total = (a.chunk_hi - a.chunk_lo) * n_frames;
   int par = 0;
-  if (a.prof && tid == 0) atomicMin(&a.prof[8], (unsigned long long)wall_clock64());
+    SC_PROF(if (a.prof && tid == 0) atomicMin(&a.prof[8], (unsigned long long)wall_clock64());)
 
   for (;;) {
     if (tid == 0) s_item = atomicAdd(a.queue, 1u);
     __syncthreads();
     const uint64_t item = s_item;
     if (item >= total) {
-      if (a.prof && tid == 0) atomicMax(&a.prof[9], (unsigned long long)wall_clock64());
+    SC_PROF(if (a.prof && tid == 0) atomicMax(&a.prof[9], (unsigned long long)wall_clock64());)
       break;
     }
     const uint32_t f = (uint32_t)(item % n_frames);
@@ -268,50 +488,68 @@ __global__ __launch_bounds__(kScT) void sc_kernel(ScArgs a, uint32_t n_frames) {
     for (int it = 0; it < kScIters; it++) acond[it][tid] = 0xFFFFu;
     __syncthreads();
     if (c0 >= L || s_trig < (unsigned long long)c0) {  // an earlier trigger exists
-      if (a.prof && tid == 0) atomicAdd(&a.prof[6], 1ull);
+    SC_PROF(if (a.prof && tid == 0) atomicAdd(&a.prof[6], 1ull);)
       continue;
     }
-    const long long t_item = clock64();
-    const long long w_item = wall_clock64();
-    long long t_rows = 0, t_words = 0, t_ph[5] = {0, 0, 0, 0, 0};
+    SC_PROF(const long long t_item = clock64();)
+    SC_PROF(const long long w_item = wall_clock64();)
+    SC_PROF(long long t_rows = 0, t_words = 0, t_ph[5] = {0, 0, 0, 0, 0};)
     const int64_t w0 = c0 - H;                 // first evaluated position
     const int64_t org = w0 - M;                // ring slot 0 at the start of the item
     const int64_t cend = std::min<int64_t>(c0 + K, L);
     int any = 1;
     uint32_t n_done = 0;
+    // antenna 0 evaluates the whole item; antenna s > 0 only the iterations covering the
+    // survivors of antennas < s (and their cp+2 run history): a plateau region is short
+    int it_lo = 0, it_hi = kScIters - 1;
 
     for (uint32_t s = 0; s < a.N && any; s++) {
-      const long long t_r0 = clock64();
+    SC_PROF(const long long t_r0 = clock64();)
       const float2 *__restrict__ x = a.iq + ((uint64_t)f * a.N + s) * a.stride;
       const bool vec = ((uintptr_t)x & 15u) == 0;
-      // history [org, w0) -> slots [0, M); iteration 0's block in flight behind it
-      for (int j = tid; 2 * j < M; j += kScT)
-        *reinterpret_cast<float4 *>(ring + ring_pad(2 * j)) = ld_pair(x, org + 2 * j, L, vec);
+      const int64_t ib_lo = w0 + (int64_t)it_lo * kScIt;   // first evaluated position
+      if (tid == 0) s_lo[s] = ib_lo;
+      for (int it = 0; it < kScIters; it++)
+        if (it < it_lo || it > it_hi) {
+          acond[it][tid] = 0;
+          wbits[((int)s * kScIters + it) * kScT + tid] = 0;
+        }
+      // history [ib_lo - M, ib_lo) -> its ring slots; the first block in flight behind it
+      const int wb = (kScIt * it_lo) % RING;
+      for (int j = tid; 2 * j < M; j += kScT) {
+        int sl = wb + 2 * j;
+        if (sl >= RING) sl -= RING;
+        *reinterpret_cast<float4 *>(ring + ring_pad(sl)) = ld_pair(x, ib_lo - M + 2 * j, L, vec);
+      }
       float4 pre[kScIt / (2 * kScT)];
-      bool pf = fetch_block(pre, x, w0, L, vec);
+      bool pf = fetch_block(pre, x, ib_lo, L, vec);
       __syncthreads();
-      // window sums ending at w0 - 1: P over [w0-RL, w0), 2R and the nonzero count over [org, w0)
+      // window sums ending at ib_lo - 1: P over the last M/2, 2R and the nonzero count over M
       double c[4] = {0.0, 0.0, 0.0, 0.0}, t4[4], tot[5];
       for (int k = tid; k < M; k += kScT) {
-        const float2 v = ring[ring_pad(k)];
+        int sl = wb + k;
+        if (sl >= RING) sl -= RING;
+        const float2 v = ring[ring_pad(sl)];
         const float z = v.x * v.x + v.y * v.y;
         c[2] += (double)z;
         c[3] += (z != 0.0f) ? 1.0 : 0.0;
         if (k >= RL) {
-          const float2 pp = cj_mul(ring[ring_pad(k - RL)], v);
+          int sd = sl - RL;
+          if (sd < 0) sd += RING;
+          const float2 pp = cj_mul(ring[ring_pad(sd)], v);
           c[0] += (double)pp.x;
           c[1] += (double)pp.y;
         }
       }
       block_scan<4>(c, t4, scan_ws[par]);
-      long long t_m = clock64();
-      t_ph[0] += t_m - t_r0;
+    SC_PROF(long long t_m = clock64();)
+    SC_PROF(t_ph[0] += t_m - t_r0;)
       par ^= 1;
       double Pc_re = t4[0], Pc_im = t4[1], Zc = t4[2], Cc = t4[3], Ac = t4[2];
-      long long carry = w0 - 1;                // the halo boundary reads as a zero
+      long long carry = ib_lo - 1;             // the evaluation boundary reads as a zero
 
 #pragma unroll 1
-      for (int it = 0; it < kScIters; it++) {
+      for (int it = it_lo; it <= it_hi; it++) {
         const int64_t ib = w0 + (int64_t)it * kScIt;
         {
           const int slot = (M + it * kScIt) % RING + 2 * tid;
@@ -333,7 +571,7 @@ __global__ __launch_bounds__(kScT) void sc_kernel(ScArgs a, uint32_t n_frames) {
           }
         }
         __syncthreads();
-        if (it + 1 < kScIters) pf = fetch_block(pre, x, ib + kScIt, L, vec);
+        if (it + 1 <= it_hi) pf = fetch_block(pre, x, ib + kScIt, L, vec);
         const float2 *xn = ring + ring_pad((M + it * kScIt + kScS * tid) % RING);
         const float2 *xr = ring + ring_pad((RL + it * kScIt + kScS * tid) % RING);
         const float2 *xm = ring + ring_pad((it * kScIt + kScS * tid) % RING);
@@ -365,9 +603,9 @@ __global__ __launch_bounds__(kScT) void sc_kernel(ScArgs a, uint32_t n_frames) {
           }
         }
         d[3] = (double)dc;
-        { const long long t2 = clock64(); t_ph[1] += t2 - t_m; t_m = t2; }
+        SC_PROF({ const long long t2 = clock64(); t_ph[1] += t2 - t_m; t_m = t2; })
         block_scan<5>(d, tot, scan_ws[par]);
-        { const long long t2 = clock64(); t_ph[2] += t2 - t_m; t_m = t2; }
+        SC_PROF({ const long long t2 = clock64(); t_ph[2] += t2 - t_m; t_m = t2; })
         par ^= 1;
         // phase B: walk the segment
         double Pre = Pc_re + d[0], Pim = Pc_im + d[1], Z = Zc + d[2], C = Cc + d[3];
@@ -385,8 +623,8 @@ __global__ __launch_bounds__(kScT) void sc_kernel(ScArgs a, uint32_t n_frames) {
           if (rmin > 0.0 && Z > 16.0 * zfloor && pmax * pmax < (a.thr - 2.0 * a.band) * (rmin * rmin))
             walk = false;
         }
-#pragma unroll 2
-        for (int i = 0; walk && i < kScS; i += 2) {
+#pragma unroll 1
+        for (int i = 0; walk && i < kScS; i += 2) {   // rare: near a plateau
           const float4 vn = *reinterpret_cast<const float4 *>(xn + i);
           const float4 vr = *reinterpret_cast<const float4 *>(xr + i);
           const float4 vm = *reinterpret_cast<const float4 *>(xm + i);
@@ -431,7 +669,7 @@ __global__ __launch_bounds__(kScT) void sc_kernel(ScArgs a, uint32_t n_frames) {
         }
         Pc_re += tot[0]; Pc_im += tot[1]; Zc += tot[2]; Cc += tot[3]; Ac = Aend;
         wbits[((int)s * kScIters + it) * kScT + tid] = (uint16_t)bits;
-        { const long long t2 = clock64(); t_ph[3] += t2 - t_m; t_m = t2; }
+        SC_PROF({ const long long t2 = clock64(); t_ph[3] += t2 - t_m; t_m = t2; })
         const uint32_t cond = run_cond(bits, sb, carry, cp, run_ws[par]);
         // candidates only inside [c0, cend)
         const int64_t lo = c0 - sb, hi = cend - sb;
@@ -441,121 +679,63 @@ __global__ __launch_bounds__(kScT) void sc_kernel(ScArgs a, uint32_t n_frames) {
           mask = ((1u << u) - 1u) & ~((1u << l) - 1u);
         }
         acond[it][tid] = (uint16_t)(acond[it][tid] & cond & mask);
-        { const long long t2 = clock64(); t_ph[4] += t2 - t_m; t_m = t2; }
+        SC_PROF({ const long long t2 = clock64(); t_ph[4] += t2 - t_m; t_m = t2; })
       }
-      const long long t_r1 = clock64();
-      t_rows += t_r1 - t_r0;
-      int surv = 0;
+    SC_PROF(const long long t_r1 = clock64();)
+    SC_PROF(t_rows += t_r1 - t_r0;)
+      if (tid == 0) { s_smin = ~0ull; s_smax = 0ull; }
+      __syncthreads();
+      {
+        uint64_t lo = ~0ull, hi = 0ull;
 #pragma unroll
-      for (int it = 0; it < kScIters; it++) surv |= (acond[it][tid] != 0);
-      any = __syncthreads_or(surv);
+        for (int it = 0; it < kScIters; it++) {
+          const uint32_t v = acond[it][tid];
+          if (v) {
+            const uint64_t base = (uint64_t)(w0 + (int64_t)it * kScIt + kScS * tid);
+            lo = std::min<uint64_t>(lo, base + __ffs((int)v) - 1);
+            hi = std::max<uint64_t>(hi, base + 31 - __clz(v));
+          }
+        }
+        if (lo != ~0ull) { atomicMin(&s_smin, (unsigned long long)lo); atomicMax(&s_smax, (unsigned long long)hi); }
+      }
+      __syncthreads();
+      any = (s_smin != ~0ull) ? 1 : 0;
+      if (any) {
+        const int64_t ra = (int64_t)s_smin - cp - 2, rb = (int64_t)s_smax;
+        it_lo = (int)std::max<int64_t>(0, (ra - w0) / kScIt);
+        it_hi = (int)std::min<int64_t>(kScIters - 1, (rb - w0) / kScIt);
+      }
       n_done = s + 1;
-      t_words += clock64() - t_r1;
+    SC_PROF(t_words += clock64() - t_r1;)
     }
 
     const int namb = s_namb < kAmbMax ? s_namb : kAmbMax;
-    const long long t_res0 = clock64();
+    SC_PROF(const long long t_res0 = clock64();)
     if (any && namb > 0) {
-      // exact fp32 recompute of the provisional bits, a batch per (antenna, LDS window). The
-      // oracle's per-sample terms -pr, -pi (P taps -1) and 0.5|x|^2 (R taps 0.5) are tabled
-      // once per window (the same fp32 operations); each sample's three sequential sums then
-      // run on two lanes (R; Pr+Pi interleaved), oldest -> newest exactly as framing.cc does.
       if (a.n_exact && tid == 0) atomicAdd(a.n_exact, (unsigned long long)namb);
-      const int WCAP = (int)((sizeof(float2) * ring_pad(RING)) / 12) & ~3;
-      float *tz = reinterpret_cast<float *>(sc_dyn);
-      float2 *tp = reinterpret_cast<float2 *>(sc_dyn + sizeof(float) * WCAP);
-      for (;;) {
-        if (tid == 0) { s_key = ~0ull; s_ng = 0; }
-        __syncthreads();
-        for (int i = tid; i < namb; i += kScT)
-          if (amb_n[i] >= 0)
-            atomicMin(&s_key, ((unsigned long long)amb_s[i] << 48) | (unsigned long long)amb_n[i]);
-        __syncthreads();
-        const unsigned long long key = s_key;
-        if (key == ~0ull) break;   // block-uniform
-        const int s = (int)(key >> 48);
-        const int64_t nmin = (int64_t)(key & ((1ull << 48) - 1));
-        const int64_t q0 = nmin - M + 1;       // table index i <-> sample q0 + i
-        const float2 *__restrict__ x = a.iq + ((uint64_t)f * a.N + s) * a.stride;
-        for (int i = tid; i < WCAP; i += kScT) {
-          const int64_t k = q0 + i;
-          const float2 v = (k >= 0 && k < L) ? x[k] : make_float2(0.0f, 0.0f);
-          const float2 dd = (k - RL >= 0 && k - RL < L) ? x[k - RL] : make_float2(0.0f, 0.0f);
-          float z = v.x * v.x + v.y * v.y;
-          tz[i] = 0.5f * z;
-          const float2 pp = cj_mul(dd, v);
-          tp[i] = make_float2((-1.0f) * pp.x, (-1.0f) * pp.y);
+      // hand the item to the hot-item kernels (every antenna's windows resolve in parallel);
+      // resolve here only when the hot buffer is full
+      if (tid == 0) s_slot = a.hot ? atomicAdd(a.hot_count, 1u) : ~0u;
+      __syncthreads();
+      if (s_slot < a.hot_cap) {
+        ScHot *hp = a.hot + s_slot;
+        if (tid == 0) {
+          hp->f = f; hp->n_done = n_done; hp->namb = (uint32_t)namb;
+          hp->chunk = chunk; hp->c0 = c0; hp->w0 = w0; hp->cend = cend;
         }
-        // this window's samples (at most kResGroup per pass; the rest wait for the next pass)
-        for (int i = tid; i < namb; i += kScT) {
-          const int64_t n = amb_n[i];
-          if (n >= 0 && amb_s[i] == s && n - nmin <= WCAP - M) {
-            const int g = atomicAdd(&s_ng, 1);
-            if (g < kResGroup) { res_i[g] = i; amb_n[i] = -1; }
-          }
-        }
-        __syncthreads();
-        const int ng = s_ng < kResGroup ? s_ng : kResGroup;
-        {
-          const int g = lane + 64 * (wv >> 1);
-          if (g < ng) {
-            const int r = (int)(amb_n_val(res_i[g]) - nmin);
-            if ((wv & 1) == 0) {          // R over i = r .. r + M - 1
-              const float *q = tz + r;
-              float R = 0.0f;
-#pragma unroll 8
-              for (int k = 0; k < M; k++) R = R + q[k];
-              res_v[0][g] = R;
-            } else {                      // P over i = r + M/2 .. r + M - 1
-              const float2 *q = tp + r + RL;
-              float Pr = 0.0f, Pi = 0.0f;
-#pragma unroll 8
-              for (int k = 0; k < RL; k++) { const float2 t = q[k]; Pr = Pr + t.x; Pi = Pi + t.y; }
-              res_v[1][g] = Pr;
-              res_v[2][g] = Pi;
-            }
-          }
-        }
-        __syncthreads();
-        if (tid < ng) {
-          const float Pr = res_v[1][tid], Pi = res_v[2][tid], R = res_v[0][tid];
-          const float y32 = (Pr * Pr + Pi * Pi) / (R * R);
-          if (!((double)y32 > a.thr)) {
-            const int64_t o = amb_n_val(res_i[tid]) - w0;
-            const int it = (int)(o / kScIt), t = (int)((o % kScIt) / kScS);
-            const int bit = (int)(o % kScS) + 16 * (t & 1);
-            uint32_t *w32 = reinterpret_cast<uint32_t *>(wbits) +
-                            ((s * kScIters + it) * kScT + t) / 2;
-            atomicAnd(w32, ~(1u << bit));
-          }
-        }
-        __syncthreads();
+        if (tid < (int)n_done) hp->lo[tid] = s_lo[tid];
+        for (int i = tid; i < namb; i += kScT) { hp->amb_n[i] = amb_pos[i]; hp->amb_s[i] = amb_s[i]; }
+        uint32_t *dst = reinterpret_cast<uint32_t *>(hp->wbits);
+        const uint32_t *src = reinterpret_cast<const uint32_t *>(wbits);
+        for (int i = tid; i < (int)n_done * kScIters * kScT / 2; i += kScT) dst[i] = src[i];
+        any = 0;
+      } else {
+        resolve_pending(a, f, w0, amb_n, amb_pos, amb_s, namb, wbits, sc_dyn,
+                        (int)(sizeof(float2) * ring_pad(RING)), rl);
+        any = item_conditions(wbits, acond, n_done, w0, c0, cend, cp, run_ws, par);
       }
-      // plateau rule again from the corrected bits
-#pragma unroll
-      for (int it = 0; it < kScIters; it++) acond[it][tid] = 0xFFFFu;
-      for (uint32_t s = 0; s < n_done; s++) {
-        long long carry = w0 - 1;
-#pragma unroll 1
-        for (int it = 0; it < kScIters; it++) {
-          const int64_t sb = w0 + (int64_t)it * kScIt + kScS * tid;
-          const uint32_t bits = wbits[((int)s * kScIters + it) * kScT + tid];
-          par ^= 1;
-          const uint32_t cond = run_cond(bits, sb, carry, cp, run_ws[par]);
-          const int64_t lo = c0 - sb, hi = cend - sb;
-          uint32_t mask = 0;
-          if (hi > 0 && lo < kScS) {
-            const int l = lo < 0 ? 0 : (int)lo, u = hi > kScS ? kScS : (int)hi;
-            mask = ((1u << u) - 1u) & ~((1u << l) - 1u);
-          }
-          acond[it][tid] = (uint16_t)(acond[it][tid] & cond & mask);
-        }
-      }
-      int surv = 0;
-#pragma unroll
-      for (int it = 0; it < kScIters; it++) surv |= (acond[it][tid] != 0);
-      any = __syncthreads_or(surv);
     }
+#ifdef MIMO_SC_PROFILE
     if (a.prof && tid == 0) {
       const long long t_end = clock64();
       atomicAdd(&a.prof[0], 1ull);
@@ -570,47 +750,61 @@ __global__ __launch_bounds__(kScT) void sc_kernel(ScArgs a, uint32_t n_frames) {
       atomicMax(&a.prof[10], (unsigned long long)(w_end - w_item));
       atomicMax(&a.prof[11], (unsigned long long)w_item);
     }
-    if (any) {
-#pragma unroll
-      for (int it = 0; it < kScIters; it++) {
-        const uint32_t v = acond[it][tid];
-        if (v)
-          atomicMin(&s_min, (unsigned long long)(w0 + (int64_t)it * kScIt + kScS * tid +
-                                                 __ffs((int)v) - 1));
-      }
-      __syncthreads();
-      const unsigned long long cand = s_min;
-      if (cand != ~0ull) {
-        ScRecord *rec = a.rec + (uint64_t)f * a.rec_stride + chunk;
-        if (wv == 0) {   // run start: one past the last zero below the candidate
-          bool found = false;
-          if (lane < (int)a.N) {
-            const int s = lane;
-            const int64_t o = (int64_t)cand - w0;
-            int it = (int)(o / kScIt), t = (int)((o % kScIt) / kScS);
-            const int i = (int)(o % kScS);
-            uint32_t m = ~(uint32_t)wbits[(s * kScIters + it) * kScT + t] & ((1u << i) - 1u);
-            while (!m) {   // rare: only for a candidate item
-              if (--t < 0) { t = kScT - 1; if (--it < 0) break; }
-              m = ~(uint32_t)wbits[(s * kScIters + it) * kScT + t] & 0xFFFFu;
-            }
-            const long long lzv =
-                m ? (long long)(w0 + (int64_t)it * kScIt + kScS * t + 31 - __clz(m)) : -1;
-            found = lzv >= w0;    // a computed zero, not the halo boundary
-            rec->start[s] = found ? (unsigned long long)(lzv + 1) : 0ull;
-          }
-          const unsigned long long fm = __ballot(found);
-          if (lane == 0) {
-            rec->found = (uint32_t)fm;
-            rec->n_cand = cand;
-            rec->pos0 = w0;
-            atomicMin(&a.trig[f], cand);
-          }
-        }
-      }
-    }
+#endif
+    if (any) item_record(a, f, chunk, w0, wbits, acond, s_lo, s_min);
     __syncthreads();
   }
+}
+
+// hot items, stage 1: one workgroup per (item, antenna) resolves that antenna's pending samples
+// against the capture and clears the failing bits of the item's saved plateau words
+__global__ __launch_bounds__(kScT) void sc_resolve_kernel(ScArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char tables[];
+  __shared__ long long pos[kAmbMax], pos0[kAmbMax];
+  __shared__ uint8_t ant[kAmbMax];
+  __shared__ ResolveLds rl;
+  __shared__ int s_n;
+  const uint32_t h = blockIdx.x, s = blockIdx.y;
+  const uint32_t count = min(*a.hot_count, a.hot_cap);
+  if (h >= count) return;
+  ScHot *hp = a.hot + h;
+  if (s >= hp->n_done) return;
+  if (threadIdx.x == 0) s_n = 0;
+  __syncthreads();
+  for (int i = threadIdx.x; i < (int)hp->namb; i += kScT)
+    if (hp->amb_s[i] == s) {
+      const int j = atomicAdd(&s_n, 1);
+      pos[j] = pos0[j] = hp->amb_n[i];
+      ant[j] = (uint8_t)s;
+    }
+  __syncthreads();
+  if (s_n == 0) return;
+  resolve_pending(a, hp->f, hp->w0, pos, pos0, ant, s_n, hp->wbits, tables,
+                  (int)(sizeof(float2) * ring_pad((int)a.M + kScIt)), rl);
+}
+
+// hot items, stage 2: plateau rule on the corrected words, candidate, record, trigger
+__global__ __launch_bounds__(kScT) void sc_finalize_kernel(ScArgs a) {
+  __shared__ __attribute__((aligned(16))) uint16_t wb[kMaxStreams * kScIters * kScT];
+  __shared__ uint16_t acond[kScIters][kScT];
+  __shared__ long long run_ws[2][kScT / 64];
+  __shared__ long long lo[kMaxStreams];
+  __shared__ unsigned long long s_min;
+  const uint32_t h = blockIdx.x;
+  const uint32_t count = min(*a.hot_count, a.hot_cap);
+  if (h >= count) return;
+  const ScHot *hp = a.hot + h;
+  const uint32_t n_done = hp->n_done;
+  const uint32_t *src = reinterpret_cast<const uint32_t *>(hp->wbits);
+  uint32_t *dst = reinterpret_cast<uint32_t *>(wb);
+  for (int i = threadIdx.x; i < (int)n_done * kScIters * kScT / 2; i += kScT) dst[i] = src[i];
+  if (threadIdx.x < n_done) lo[threadIdx.x] = hp->lo[threadIdx.x];
+  if (threadIdx.x == 0) s_min = ~0ull;
+  __syncthreads();
+  int par = 0;
+  const int any = item_conditions(wb, acond, n_done, hp->w0, hp->c0, hp->cend, (int64_t)a.cp,
+                                  run_ws, par);
+  if (any) item_record(a, hp->f, hp->chunk, hp->w0, wb, acond, lo, s_min);
 }
 
 // run starts (from the trigger chunk's record, exact backward scan where the run began
@@ -642,7 +836,7 @@ __global__ __launch_bounds__(64) void plateau_kernel(PlateauArgs a) {
       // every computed sample of the chunk's range is in the run: walk back exactly
       const float2 *__restrict__ x = a.iq + ((uint64_t)f * a.N + s) * a.stride;
       start = 0;
-      for (int64_t q0 = rec.pos0 - 1; q0 >= 0; q0 -= 64) {
+      for (int64_t q0 = (int64_t)rec.start[s] - 1; q0 >= 0; q0 -= 64) {
         const int64_t q = q0 - lane;
         bool zero = true;
         if (q >= 0) {
@@ -705,6 +899,24 @@ void launch_sc(const ScArgs &a, uint32_t n_frames, uint32_t n_cu, hipStream_t s)
   const uint32_t grid = (uint32_t)std::min<uint64_t>(total, (uint64_t)n_cu * per_cu);
   if (grid) hipLaunchKernelGGL(sc_kernel, dim3(grid), dim3(kScT), shm, s, a, n_frames);
   if (a.prof) fprintf(stderr, "sc grid %u (per_cu %d, n_cu %u, lds %zu)\n", grid, per_cu, n_cu, shm);
+}
+
+size_t sc_table_bytes(uint32_t M) {
+  const int ring = (int)M + kScIt;
+  return sizeof(float2) * (size_t)(ring + ((ring >> 5) << 1));
+}
+
+void launch_sc_hot(const ScArgs &a, hipStream_t s) {
+  if (!a.hot || !a.hot_cap) return;
+  const size_t shm = sc_table_bytes(a.M);
+  static size_t set_shm = 0;
+  if (shm != set_shm) {
+    (void)hipFuncSetAttribute((const void *)sc_resolve_kernel,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
+    set_shm = shm;
+  }
+  hipLaunchKernelGGL(sc_resolve_kernel, dim3(a.hot_cap, a.N), dim3(kScT), shm, s, a);
+  hipLaunchKernelGGL(sc_finalize_kernel, dim3(a.hot_cap), dim3(kScT), 0, s, a);
 }
 
 void launch_plateau(const PlateauArgs &a, uint32_t n_frames, hipStream_t s) {
