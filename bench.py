@@ -69,7 +69,8 @@ def main():
     sh = stream.cuda_stream
 
     # ---- synthetic captures, generated on this GPU (outside the timed region)
-    frame_id0 = rank * F
+    from rub_mimo_amd.shard import frame_ids, reduce_stats
+    frame_id0, _ = frame_ids(rank, F)
     sp = SynthParams(M=M, cp_len=cp, num_streams=N, num_access_codes=nac, pid=pid,
                      qam_order=args.qam, seed=args.seed, snr_db=args.snr)
     syn = Synthesizer(sp)
@@ -114,16 +115,12 @@ def main():
     errors = sum(int(np.sum(r["errors"])) for r in res)
 
     samples_local = float(N) * true_len * args.steps
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-        c = torch.tensor([samples_local, ok, evm_num, evm_den, errors], dtype=torch.float64,
-                         device=dev)
-        dist.all_reduce(c, op=dist.ReduceOp.SUM)
-        samples_total, ok, evm_num, evm_den, errors = [float(v) for v in c.tolist()]
-    else:
-        samples_total = samples_local
+    tot, elapsed = reduce_stats(dict(samples=samples_local, frames_ok=ok, evm_num=evm_num,
+                                     evm_den=evm_den, errors=errors), elapsed,
+                                dist if world > 1 else None, device=dev)
+    samples_total, ok, evm_num, evm_den, errors = (tot[k] for k in
+                                                   ("samples", "frames_ok", "evm_num",
+                                                    "evm_den", "errors"))
 
     # ---- roofline of the dominant kernel: decode (HBM bound)
     dec_ms, dec_n = stages["decode"]
