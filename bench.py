@@ -41,6 +41,9 @@ def parse():
     ap.add_argument("--detector", default="mmse", choices=["zf2", "zf", "mmse"])
     ap.add_argument("--seed", type=int, default=1234)
     ap.add_argument("--cpu-baseline", type=int, default=1, help="0 to skip the oracle timing")
+    ap.add_argument("--ref-mode", type=int, default=2,
+                    help="EVM reference: 0 decided symbols, 1 transmitted indices from HBM, "
+                         "2 transmitted indices regenerated from the seed")
     ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "decode_pmc.json"))
     return ap.parse_args()
 
@@ -76,7 +79,9 @@ def main():
     syn = Synthesizer(sp)
     L = sp.max_frame_len()
     iq = torch.empty((F, N, L), dtype=torch.complex64, device=dev)
-    syn.generate(iq, L, L, F, frame_id0=frame_id0, stream=sh)
+    m_occ_s = M   # all-carrier allocation (framing.cc:949-954)
+    tx_idx = torch.empty((F, N, pid, m_occ_s), dtype=torch.uint8, device=dev)
+    syn.generate(iq, L, L, F, frame_id0=frame_id0, tx_idx=tx_idx, stream=sh)
     true_len = sum(syn.frame_len(frame_id0 + f) for f in range(F))   # samples per antenna
 
     rx = Receiver(RxParams(M=M, cp_len=cp, num_streams=N, num_access_codes=nac, pid_max=pid,
@@ -86,7 +91,8 @@ def main():
     out_idx = torch.empty((F, N, pid, m_occ), dtype=torch.uint8, device=dev)
 
     def step():
-        rx.process(iq, L, L, F, max_out=pid, out_sym=out_sym, out_idx=out_idx, ref_mode=2,
+        rx.process(iq, L, L, F, max_out=pid, out_sym=out_sym, out_idx=out_idx,
+                   ref_mode=args.ref_mode, ref_idx=tx_idx if args.ref_mode == 1 else None,
                    ref_seed=args.seed, frame_id0=frame_id0, stream=sh)
 
     for _ in range(args.warmup):
@@ -115,17 +121,21 @@ def main():
     errors = sum(int(np.sum(r["errors"])) for r in res)
 
     samples_local = float(N) * true_len * args.steps
-    tot, elapsed = reduce_stats(dict(samples=samples_local, frames_ok=ok, evm_num=evm_num,
-                                     evm_den=evm_den, errors=errors), elapsed,
+    # symbols decoded per step (frames that sync; the others are scanned, not decoded)
+    n_dec = sum(min(int(r["n_sym"]), pid) for r in res if r["status"] == _lib.FRAME_OK)
+    tot, elapsed = reduce_stats(dict(samples=samples_local, frames_ok=ok, symbols=n_dec,
+                                     evm_num=evm_num, evm_den=evm_den, errors=errors), elapsed,
                                 dist if world > 1 else None, device=dev)
-    samples_total, ok, evm_num, evm_den, errors = (tot[k] for k in
-                                                   ("samples", "frames_ok", "evm_num",
-                                                    "evm_den", "errors"))
+    samples_total, ok, n_dec_all, evm_num, evm_den, errors = (
+        tot[k] for k in ("samples", "frames_ok", "symbols", "evm_num", "evm_den", "errors"))
 
     # ---- roofline of the dominant kernel: decode (HBM bound)
     dec_ms, dec_n = stages["decode"]
     dec_avg_s = dec_ms / max(dec_n, 1) / 1e3
-    dec_bytes = F * (N * pid * M * 8 + N * pid * m_occ * 9)   # body reads + sym/idx writes
+    # per decoded symbol: N bodies read, N x M_occ complex64 + uint8 written (+ the uint8
+    # transmitted index read when the EVM reference comes from HBM)
+    per_sym = N * M * 8 + N * m_occ * 9 + (N * m_occ if args.ref_mode == 1 else 0)
+    dec_bytes = n_dec * per_sym
     achieved = dec_bytes / dec_avg_s / 1e9 if dec_avg_s > 0 else 0.0
     traffic = None
     if os.path.exists(args.pmc_json):
@@ -138,25 +148,39 @@ def main():
         except Exception:
             traffic = None
 
-    # ---- CPU baseline: the C oracle (faithful brute-force search, 1 core) on one frame
+    # ---- CPU baseline: the C oracle (faithful brute-force search, 1 core) on the first frame
+    # of this rank's batch that syncs, plus the EVM-dB delta of the GPU vs the oracle on it
     cpu = None
+    evm_delta = None
     if rank == 0 and world == 1 and args.cpu_baseline:
         from oracle import ref
-        L0 = syn.frame_len(frame_id0)
-        host = iq[0, :, :L0].cpu().numpy()
-        o = ref.FrameSyncRef(M, cp, N, nac, pid_max=pid, detector=det)
-        c0 = time.perf_counter()
-        o.execute(host)
-        c1 = time.perf_counter()
-        cpu = {"value": N * L0 / (c1 - c0), "unit": "complex samples/s", "cores": 1,
-               "kind": "port",
-               "sample": "1 full C3 frame (%d samples x %d antennas) through oracle/mimo_ref.c "
-                         "framesync (brute-force search as framing.cc:702-744), gcc -O3, "
-                         "1 thread, %.1f s" % (L0, N, c1 - c0)}
+        fsel = next((f for f, r in enumerate(res) if r["status"] == _lib.FRAME_OK), None)
+        if fsel is not None:
+            L0 = syn.frame_len(frame_id0 + fsel)
+            host = iq[fsel, :, :L0].cpu().numpy()
+            o = ref.FrameSyncRef(M, cp, N, nac, pid_max=pid, detector=det)
+            c0 = time.perf_counter()
+            o.execute(host)
+            c1 = time.perf_counter()
+            cpu = {"value": N * L0 / (c1 - c0), "unit": "complex samples/s", "cores": 1,
+                   "kind": "port",
+                   "sample": "frame %d of the batch (first that syncs): %d samples x %d "
+                             "antennas through oracle/mimo_ref.c framesync (Schmidl-Cox direct "
+                             "sums, brute-force search as framing.cc:702-744, MMSE, decode), "
+                             "gcc -O3, 1 thread, %.1f s" % (fsel, L0, N, c1 - c0)}
+            sym = o.symbols()[:pid]
+            if len(sym):
+                _, en, ed, _ = ref.demap_evm(sym, args.qam, tx_idx[fsel, :, :len(sym)].cpu().numpy())
+                r = res[fsel]
+                evm_cpu = 10 * np.log10(float(np.sum(en)) / float(np.sum(ed)))
+                evm_gpu = 10 * np.log10(float(np.sum(r["evm_num"])) / float(np.sum(r["evm_den"])))
+                evm_delta = {"frame": fsel, "gpu_db": evm_gpu, "cpu_db": evm_cpu,
+                             "delta_db": evm_gpu - evm_cpu,
+                             "sync_index_equal": int(o.get_sync_index()) == int(r["sync_index"])}
 
     value = samples_total / elapsed
     ms_step = elapsed / args.steps * 1e3
-    bytes_alg = (samples_total * 8 + world * args.steps * F * N * m_occ * pid * 9)
+    bytes_alg = samples_total * 8 + args.steps * n_dec_all * N * m_occ * 9
     line = {
         "metric": "complex IQ samples/s through 4x4 MMSE detect; EVM-dB delta vs CPU ref",
         "value": value,
@@ -178,9 +202,12 @@ def main():
                    "parallelism": "frames sharded across %d GPU(s), no collective" % world},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "kernel": "decode_kernel", "bytes_per_launch": dec_bytes,
+                     "kernel": "decode_persistent_kernel<11,4,512>" if M == 2048 and N == 4
+                     else "decode", "bytes_per_launch": dec_bytes,
+                     "symbols_per_launch": n_dec, "bytes_per_symbol": per_sym,
                      "avg_launch_ms": dec_avg_s * 1e3},
         "cpu_baseline": cpu,
+        "evm_db_delta_vs_cpu": evm_delta,
         "pipeline_hbm_gbs": bytes_alg / elapsed / 1e9,
         "stages_ms_per_step": {k: v[0] / max(args.steps, 1) for k, v in stages.items()},
         "frames_ok": int(ok), "frames": int(F * world),

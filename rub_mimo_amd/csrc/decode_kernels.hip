@@ -14,11 +14,22 @@
 // demap, EVM partials and the equalised symbol + uint8 index stores are fused into the same
 // pass. Algorithmic HBM traffic per symbol: N*M*8 read + N*M_occ*9 written.
 #include <algorithm>
+#include <type_traits>
+#include <cstdlib>
 
 #include "fft.hpp"
 #include "kernels.hpp"
 
+// per-phase cycle counters (build with -DMIMO_DEC_PROFILE, run with RMIMO_DEC_PROF=1)
+#ifdef MIMO_DEC_PROFILE
+#define DEC_PROF(...) __VA_ARGS__
+#else
+#define DEC_PROF(...)
+#endif
+
 namespace mimo {
+
+constexpr uint32_t kDecMaxFrames = 256;   // frames per launch for the persistent decode
 
 template <int LOG2M, int NA, int GA, int T>
 __global__ __launch_bounds__(T) void decode_kernel(DecodeArgs a) {
@@ -158,18 +169,41 @@ __global__ __launch_bounds__(T) void decode_kernel(DecodeArgs a) {
 // loaded into registers (16-byte loads) while the current item is transformed, so HBM
 // reads overlap the FFT and the NxN apply. Each thread owns 4 consecutive subcarriers per
 // group, so weights, gains, equalised symbols and indices move as 16-byte / 4-byte vectors.
-template <int LOG2M, int NA, int T>
-__global__ __launch_bounds__(T) void decode_persistent_kernel(DecodeArgs a) {
+template <int LOG2M, int NA, int T, bool SB, bool PF, int REF>
+__global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(PF ? 1 : 2 * T / 256)))
+void decode_persistent_kernel(DecodeArgs a) {
   constexpr int M = 1 << LOG2M, PB = lds_padded_len(M);
   constexpr int NPAIR = M / 2;                 // complex pairs per antenna body
   constexpr int NIN = NPAIR / T;               // 16-byte loads per thread per antenna
   constexpr int G4 = M / (4 * T);              // 4-subcarrier groups per thread
   static_assert(NIN >= 1 && G4 >= 1, "decode_persistent_kernel needs M >= 4T");
   extern __shared__ __attribute__((aligned(16))) float2 lds[];
-  __shared__ double red[3][NA][T / 64];
+  float2 *tw_lds = lds + NA * PB;              // N/2 twiddles after the antenna bodies
   const int tid = threadIdx.x;
-  const uint32_t total = a.n_frames * a.max_out;
   const bool siso = (a.detector == 3);
+  fill_twiddles_lds<LOG2M, T>(tw_lds, a.tw);   // visible after the first item's barrier
+  // the grid walks decodable symbols only: pfx[f] = symbols of frames < f
+  __shared__ uint32_t pfx[kDecMaxFrames + 1];
+  if (tid == 0) {
+    uint32_t acc = 0;
+    for (uint32_t f = 0; f < a.n_frames; f++) {
+      pfx[f] = acc;
+      const FrameInfo &I = a.info[f];
+      acc += (I.status == 0) ? min(I.n_sym, a.max_out) : 0u;
+    }
+    pfx[a.n_frames] = acc;
+  }
+  __syncthreads();
+  const uint32_t total = pfx[a.n_frames];
+  auto locate = [&](uint32_t q, uint32_t &fo, uint32_t &so) {   // q < total
+    uint32_t lo = 0, hi = a.n_frames;       // largest f with pfx[f] <= q
+    while (hi - lo > 1) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (pfx[mid] <= q) lo = mid; else hi = mid;
+    }
+    fo = lo;
+    so = q - pfx[lo];
+  };
 
   float4 pre[NA][NIN];
   // issue the loads of one item into pre[] (zeros for items without a decodable symbol)
@@ -178,14 +212,11 @@ __global__ __launch_bounds__(T) void decode_persistent_kernel(DecodeArgs a) {
     int64_t abs0 = 0;
     uint32_t f = 0;
     if (item < total) {
-      f = item / a.max_out;
-      const uint32_t s = item % a.max_out;
+      uint32_t s;
+      locate(item, f, s);
       const FrameInfo &I = a.info[f];
-      const uint32_t n_out = (I.status == 0) ? min(I.n_sym, a.max_out) : 0u;
-      if (s < n_out) {
-        abs0 = I.base + (int64_t)I.i0 + (int64_t)s * a.SL + a.cp;
-        ok = abs0 >= 0 && abs0 + M <= (int64_t)a.frame_len;
-      }
+      abs0 = I.base + (int64_t)I.i0 + (int64_t)s * a.SL + a.cp;
+      ok = abs0 >= 0 && abs0 + M <= (int64_t)a.frame_len;
     }
 #pragma unroll
     for (int r = 0; r < NA; r++) {
@@ -206,93 +237,121 @@ __global__ __launch_bounds__(T) void decode_persistent_kernel(DecodeArgs a) {
   };
 
   uint32_t item = blockIdx.x;
-  fetch(item);
+  if constexpr (PF) fetch(item);
   for (; item < total; item += gridDim.x) {
-    const uint32_t f = item / a.max_out, s = item % a.max_out;
-    const FrameInfo &I = a.info[f];
-    const uint32_t n_out = (I.status == 0) ? min(I.n_sym, a.max_out) : 0u;
-    double *ep = a.evm_part + (((uint64_t)f * a.max_out + s) * NA) * 3;
+    // an opaque copy of the thread index: LDS/global address arithmetic is recomputed per
+    // item instead of being hoisted out of the loop into (spilled) registers
+    int tid = threadIdx.x;
+    asm volatile("" : "+v"(tid));
+    uint32_t f, s;
+    locate(item, f, s);
+    DEC_PROF(const long long t0 = clock64();)
+    if constexpr (!PF) fetch(item);   // two resident workgroups hide each other's loads
     __syncthreads();   // the previous item's LDS reads are done
 #pragma unroll
     for (int r = 0; r < NA; r++)
 #pragma unroll
-      for (int u = 0; u < NIN; u++) {
-        const int i = 2 * (tid + u * T);
-        lds[r * PB + lds_pad(i)] = make_float2(pre[r][u].x, pre[r][u].y);
-        lds[r * PB + lds_pad(i + 1)] = make_float2(pre[r][u].z, pre[r][u].w);
-      }
-    fetch(item + gridDim.x);   // next item's input in flight during this item's compute
-    if (s >= n_out) {          // block-uniform
-      if (tid < NA * 3) ep[tid] = 0.0;
-      continue;
-    }
+      for (int u = 0; u < NIN; u++)   // samples 2i, 2i+1 are adjacent in the padded image
+        *reinterpret_cast<float4 *>(lds + r * PB + lds_pad(2 * (tid + u * T))) = pre[r][u];
+    if constexpr (PF) fetch(item + gridDim.x);   // next item's input in flight meanwhile
     __syncthreads();
-    fft_lds<LOG2M, T, NA, false>(lds, a.tw);
+    DEC_PROF(const long long t1 = clock64();)
+    fft_lds_twl<LOG2M, T, NA, false>(lds, tw_lds, tid);
+    DEC_PROF(const long long t2 = clock64();)
 
-    // per-thread partials over <= 4*G4 subcarriers stay fp32; waves and items sum in fp64
+    // per-thread partials over <= 4*G4 subcarriers stay fp32; each wave writes its own
+    // partial set (no block barrier), the EVM kernel sums them in fp64
     float e_num[NA], e_den[NA], e_err[NA];
 #pragma unroll
     for (int t = 0; t < NA; t++) e_num[t] = e_den[t] = e_err[t] = 0.0f;
     const uint64_t frame_id = a.frame_id0 + f;
     const float2 *__restrict__ Wf = a.W + (uint64_t)f * NA * NA * M;
     const float *__restrict__ gf = a.gain + (uint64_t)f * M;
+    const v2f *vl = reinterpret_cast<const v2f *>(lds);
 #pragma unroll
     for (int g = 0; g < G4; g++) {
       const int k0 = 4 * (tid + g * T);
-      float2 X[NA][4];
+      v2f X[NA][4];                      // 2 packed FMAs per complex MAC below
 #pragma unroll
       for (int r = 0; r < NA; r++)
 #pragma unroll
-        for (int e = 0; e < 4; e++) {
-          const float2 v = lds[r * PB + lds_pad(k0 + e)];
-          X[r][e] = make_float2(v.x * a.dn, v.y * a.dn);   // (:561) x dft_normalizer
-        }
+        for (int e = 0; e < 4; e++)
+          X[r][e] = vl[r * PB + lds_pad(k0 + e)] * a.dn;   // (:561) x dft_normalizer
       float gn[4] = {1.0f, 1.0f, 1.0f, 1.0f};
+      float4 wnext[NA][2];
       if (!siso) {
         const float4 g4 = *reinterpret_cast<const float4 *>(gf + k0);
         gn[0] = g4.x; gn[1] = g4.y; gn[2] = g4.z; gn[3] = g4.w;
+#pragma unroll
+        for (int r = 0; r < NA; r++) {   // stream 0's weight row
+          const float4 *wp = reinterpret_cast<const float4 *>(Wf + (uint64_t)r * M + k0);
+          wnext[r][0] = wp[0];
+          wnext[r][1] = wp[1];
+        }
       }
 #pragma unroll
       for (int t = 0; t < NA; t++) {
-        float2 y[4];
+        v2f y[4];
         if (siso) {
 #pragma unroll
           for (int e = 0; e < 4; e++) {
-            y[e] = make_float2(0.0f, 0.0f);
+            y[e] = v2f{0.0f, 0.0f};
             if (t == (int)a.siso_rx) {
               const float2 gg =
                   a.G[(((uint64_t)f * M + k0 + e) * NA + a.siso_rx) * NA + a.siso_tx];
-              y[e] = cdiv(X[t][e], gg);
+              const float2 q = cdiv(make_float2(X[t][e].x, X[t][e].y), gg);
+              y[e] = v2f{q.x, q.y};
             }
           }
         } else {
+          // this stream's weight row is in registers; issue the next row's loads now
+          float4 wcur[NA][2];
 #pragma unroll
-          for (int r = 0; r < NA; r++) {
-            const float4 *wp = reinterpret_cast<const float4 *>(Wf + ((uint64_t)t * NA + r) * M + k0);
-            const float4 w01 = wp[0], w23 = wp[1];
-            const float2 w[4] = {make_float2(w01.x, w01.y), make_float2(w01.z, w01.w),
-                                 make_float2(w23.x, w23.y), make_float2(w23.z, w23.w)};
+          for (int r = 0; r < NA; r++) { wcur[r][0] = wnext[r][0]; wcur[r][1] = wnext[r][1]; }
+          if (t + 1 < NA) {
 #pragma unroll
-            for (int e = 0; e < 4; e++)
-              y[e] = (r == 0) ? cmul(w[e], X[r][e]) : cadd(y[e], cmul(w[e], X[r][e]));
+            for (int r = 0; r < NA; r++) {
+              const float4 *wp =
+                  reinterpret_cast<const float4 *>(Wf + ((uint64_t)(t + 1) * NA + r) * M + k0);
+              wnext[r][0] = wp[0];
+              wnext[r][1] = wp[1];
+            }
           }
 #pragma unroll
-          for (int e = 0; e < 4; e++) y[e] = make_float2(y[e].x * gn[e], y[e].y * gn[e]);
+          for (int e = 0; e < 4; e++) y[e] = v2f{0.0f, 0.0f};
+#pragma unroll
+          for (int r = 0; r < NA; r++) {
+            const float4 w01 = wcur[r][0], w23 = wcur[r][1];
+            const v2f w[4] = {v2f{w01.x, w01.y}, v2f{w01.z, w01.w}, v2f{w23.x, w23.y},
+                              v2f{w23.z, w23.w}};
+#pragma unroll
+            for (int e = 0; e < 4; e++) {
+              y[e] = __builtin_elementwise_fma(w[e].xx, X[r][e], y[e]);
+              y[e] = __builtin_elementwise_fma(w[e].yy, v2f{-X[r][e].y, X[r][e].x}, y[e]);
+            }
+          }
+#pragma unroll
+          for (int e = 0; e < 4; e++) y[e] = y[e] * gn[e];
         }
         uint32_t packed = 0;
+        uint32_t refs = 0;
+        if constexpr (REF == 1)
+          refs = *reinterpret_cast<const uint32_t *>(
+              a.ref_idx + (((uint64_t)f * NA + t) * a.max_out + s) * a.M_occ + k0);
 #pragma unroll
         for (int e = 0; e < 4; e++) {
           const int k = k0 + e;
-          const uint32_t d = qam_demap(y[e], a.qam);
+          const float2 ye = make_float2(y[e].x, y[e].y);
+          const uint32_t d = qam_demap(ye, a.qam);
           uint32_t refi = d;
-          if (a.ref_mode == 1)
-            refi = a.ref_idx[(((uint64_t)f * NA + t) * a.max_out + s) * a.M_occ + k];
-          else if (a.ref_mode == 2)
+          if constexpr (REF == 1)
+            refi = (refs >> (8 * e)) & 0xFFu;
+          else if constexpr (REF == 2)
             refi = (uint32_t)(hash5(a.ref_seed, DOM_DATA, frame_id, t,
                                     (uint64_t)s * a.M_occ + k) &
                               (uint64_t)(a.qam.L * a.qam.L - 1));
           const float2 sp = qam_point(refi, a.qam);
-          const float er = y[e].x - sp.x, ei = y[e].y - sp.y;
+          const float er = ye.x - sp.x, ei = ye.y - sp.y;
           e_num[t] += er * er + ei * ei;
           e_den[t] += sp.x * sp.x + sp.y * sp.y;
           e_err[t] += (d != refi) ? 1.0f : 0.0f;
@@ -305,31 +364,39 @@ __global__ __launch_bounds__(T) void decode_persistent_kernel(DecodeArgs a) {
           op[1] = make_float4(y[2].x, y[2].y, y[3].x, y[3].y);
         }
         if (a.out_idx) *reinterpret_cast<uint32_t *>(a.out_idx + o) = packed;
-        __builtin_amdgcn_sched_barrier(0);   // keep stream t+1's W loads after stream t
+        if constexpr (SB) __builtin_amdgcn_sched_barrier(0);   // stream t+1's W loads after t
       }
     }
+    DEC_PROF(const long long t3 = clock64();)
+    {
+      const int lane = tid & 63, wv = tid >> 6;
+      double *epw = a.evm_part + ((((uint64_t)f * a.max_out + s) * (T / 64) + wv) * NA) * 3;
 #pragma unroll
-    for (int t = 0; t < NA; t++) {
-      double vn = e_num[t], vd = e_den[t], ve = e_err[t];
+      for (int t = 0; t < NA; t++) {
 #pragma unroll
-      for (int off = 32; off > 0; off >>= 1) {
-        vn += __shfl_xor(vn, off);
-        vd += __shfl_xor(vd, off);
-        ve += __shfl_xor(ve, off);
+        for (int off = 32; off > 0; off >>= 1) {
+          e_num[t] += __shfl_xor(e_num[t], off);
+          e_den[t] += __shfl_xor(e_den[t], off);
+          e_err[t] += __shfl_xor(e_err[t], off);
+        }
       }
-      if ((tid & 63) == 0) {
-        red[0][t][tid >> 6] = vn;
-        red[1][t][tid >> 6] = vd;
-        red[2][t][tid >> 6] = ve;
+      if (lane < NA * 3) {
+        const int t = lane / 3, c = lane % 3;
+        float v = 0.0f;
+#pragma unroll
+        for (int u = 0; u < NA; u++)
+          if (u == t) v = c == 0 ? e_num[u] : (c == 1 ? e_den[u] : e_err[u]);
+        epw[lane] = (double)v;
       }
     }
-    __syncthreads();
-    if (tid < NA * 3) {
-      const int t = tid / 3, c = tid % 3;
-      double v = 0.0;
-      for (int w = 0; w < T / 64; w++) v += red[c][t][w];
-      ep[t * 3 + c] = v;
-    }
+    DEC_PROF(if (a.prof && tid == 0) {
+      const long long t4 = clock64();
+      atomicAdd(&a.prof[0], 1ull);
+      atomicAdd(&a.prof[1], (unsigned long long)(t1 - t0));
+      atomicAdd(&a.prof[2], (unsigned long long)(t2 - t1));
+      atomicAdd(&a.prof[3], (unsigned long long)(t3 - t2));
+      atomicAdd(&a.prof[4], (unsigned long long)(t4 - t3));
+    })
   }
 }
 
@@ -337,28 +404,26 @@ __global__ __launch_bounds__(T) void decode_persistent_kernel(DecodeArgs a) {
 // result is bitwise reproducible run to run
 __global__ __launch_bounds__(256) void evm_kernel(EvmArgs a) {
   __shared__ double red[256];
-  const uint32_t f = blockIdx.x, tid = threadIdx.x;
+  const uint32_t f = blockIdx.x, c = blockIdx.y, tid = threadIdx.x;
   const FrameInfo &I = a.info[f];
   const uint32_t n_out = (I.status == 0) ? min(I.n_sym, a.max_out) : 0u;
   const uint32_t per = a.N * 3;
-  for (uint32_t c = 0; c < per; c++) {
-    double v = 0.0;
-    for (uint32_t s = tid; s < n_out; s += 256)
-      v += a.evm_part[((uint64_t)f * a.max_out + s) * per + c];
-    red[tid] = v;
-    __syncthreads();
-    for (uint32_t w = 128; w > 0; w >>= 1) {
-      if (tid < w) red[tid] += red[tid + w];
-      __syncthreads();
-    }
-    if (tid == 0) a.evm_out[(uint64_t)f * per + c] = red[0];
+  const uint64_t n = (uint64_t)n_out * a.parts;    // (symbol, part) pairs, fixed order
+  double v = 0.0;
+  for (uint64_t q = tid; q < n; q += 256)
+    v += a.evm_part[((uint64_t)f * a.max_out * a.parts + q) * per + c];
+  red[tid] = v;
+  __syncthreads();
+  for (uint32_t w = 128; w > 0; w >>= 1) {
+    if (tid < w) red[tid] += red[tid + w];
     __syncthreads();
   }
+  if (tid == 0) a.evm_out[(uint64_t)f * per + c] = red[0];
 }
 
 // ------------------------------------------------------------------------------------
 template <int LOG2M, int NA>
-static void decode_launch_na(const DecodeArgs &a, uint32_t nf, hipStream_t s) {
+static uint32_t decode_launch_na(const DecodeArgs &a, uint32_t nf, hipStream_t s) {
   constexpr int M = 1 << LOG2M;
   constexpr int GA0 = (8192 / M) < 1 ? 1 : (8192 / M);
   constexpr int GA = GA0 < NA ? GA0 : NA;
@@ -369,47 +434,61 @@ static void decode_launch_na(const DecodeArgs &a, uint32_t nf, hipStream_t s) {
   constexpr int TP0 = (NA * M / 16) < 64 ? 64 : ((NA * M / 16) > 1024 ? 1024 : (NA * M / 16));
   constexpr int TP = TP0 > M / 4 ? M / 4 : TP0;
   if constexpr (GA == NA && TP >= 64) {
-    if (a.all_occ) {
-      const size_t shm = sizeof(float2) * lds_padded_len(M) * NA;
-      (void)hipFuncSetAttribute((const void *)decode_persistent_kernel<LOG2M, NA, TP>,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
-      const uint32_t per_cu = (uint32_t)std::max<size_t>(1, (160u * 1024u) / (shm + 2048));
-      const uint32_t total = nf * a.max_out;
-      const uint32_t grid = std::min<uint32_t>(total, a.n_cu * std::min<uint32_t>(per_cu, 4));
-      hipLaunchKernelGGL((decode_persistent_kernel<LOG2M, NA, TP>), dim3(grid), dim3(TP), shm,
-                         s, a);
-      return;
+    if (a.all_occ && nf <= kDecMaxFrames) {
+      const size_t shm = sizeof(float2) * (lds_padded_len(M) * NA + M / 2);
+      static const int var = [] { const char *e = getenv("RMIMO_DECODE_VAR"); return e ? atoi(e) : 0; }();
+      // 0: register prefetch of the next item (1 workgroup/CU); 1: the same with stream-
+      // ordered weight loads; 2: no prefetch, 2 workgroups/CU
+      auto pick = [&](auto ref) {
+        constexpr int R = decltype(ref)::value;
+        return var == 1 ? decode_persistent_kernel<LOG2M, NA, TP, true, true, R>
+             : var == 2 ? decode_persistent_kernel<LOG2M, NA, TP, true, false, R>
+                        : decode_persistent_kernel<LOG2M, NA, TP, false, true, R>;
+      };
+      auto kern = a.ref_mode == 1 ? pick(std::integral_constant<int, 1>{})
+                : a.ref_mode == 2 ? pick(std::integral_constant<int, 2>{})
+                                  : pick(std::integral_constant<int, 0>{});
+      (void)hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)shm);
+      int per_cu = 1;
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, TP, shm) != hipSuccess ||
+          per_cu < 1)
+        per_cu = 1;
+      const uint32_t grid = std::min<uint32_t>(nf * a.max_out, a.n_cu * (uint32_t)per_cu);
+      hipLaunchKernelGGL(kern, dim3(grid), dim3(TP), shm, s, a);
+      return TP / 64;
     }
   }
   const size_t shm = sizeof(float2) * lds_padded_len(M) * GA;
   (void)hipFuncSetAttribute((const void *)decode_kernel<LOG2M, NA, GA, T>,
                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
   hipLaunchKernelGGL((decode_kernel<LOG2M, NA, GA, T>), dim3(a.max_out, nf), dim3(T), shm, s, a);
+  return 1;
 }
 
 template <int LOG2M>
-static void decode_dispatch(const DecodeArgs &a, int log2M, uint32_t nf, hipStream_t s) {
+static uint32_t decode_dispatch(const DecodeArgs &a, int log2M, uint32_t nf, hipStream_t s) {
   if constexpr (LOG2M <= 12) {
     if (log2M == LOG2M) {
       switch (a.N) {
-        case 1: decode_launch_na<LOG2M, 1>(a, nf, s); break;
-        case 2: decode_launch_na<LOG2M, 2>(a, nf, s); break;
-        case 4: decode_launch_na<LOG2M, 4>(a, nf, s); break;
-        case 8: decode_launch_na<LOG2M, 8>(a, nf, s); break;
-        default: break;
+        case 1: return decode_launch_na<LOG2M, 1>(a, nf, s);
+        case 2: return decode_launch_na<LOG2M, 2>(a, nf, s);
+        case 4: return decode_launch_na<LOG2M, 4>(a, nf, s);
+        case 8: return decode_launch_na<LOG2M, 8>(a, nf, s);
+        default: return 0;
       }
-      return;
     }
-    decode_dispatch<LOG2M + 1>(a, log2M, nf, s);
+    return decode_dispatch<LOG2M + 1>(a, log2M, nf, s);
   }
+  return 0;
 }
 
-void launch_decode(const DecodeArgs &a, int log2M, uint32_t n_frames, hipStream_t s) {
-  decode_dispatch<6>(a, log2M, n_frames, s);
+uint32_t launch_decode(const DecodeArgs &a, int log2M, uint32_t n_frames, hipStream_t s) {
+  return decode_dispatch<6>(a, log2M, n_frames, s);
 }
 
 void launch_evm(const EvmArgs &a, uint32_t n_frames, hipStream_t s) {
-  hipLaunchKernelGGL(evm_kernel, dim3(n_frames), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(evm_kernel, dim3(n_frames, a.N * 3), dim3(256), 0, s, a);
 }
 
 }  // namespace mimo

@@ -409,7 +409,7 @@ int run_estimate(mimo_rx *h, const float2 *iq, uint64_t stride, uint32_t F, uint
 int run_decode(mimo_rx *h, const float2 *iq, uint64_t stride, uint32_t F, uint64_t frame_len,
                uint32_t max_out, float2 *out_sym, uint8_t *out_idx, int ref_mode,
                const uint8_t *ref_idx, uint64_t ref_seed, uint64_t frame_id0, hipStream_t s) {
-  int rc = ensure_workspace(h, F, 0, (uint64_t)F * max_out * h->N * 3);
+  int rc = ensure_workspace(h, F, 0, (uint64_t)F * max_out * h->N * 3 * kMaxEvmParts);
   if (rc) return rc;
   if (max_out == 0) return MIMO_OK;
   DecodeArgs d{};
@@ -424,11 +424,26 @@ int run_decode(mimo_rx *h, const float2 *iq, uint64_t stride, uint32_t F, uint64
   // RMIMO_DECODE_GRID=1 forces the one-workgroup-per-symbol grid (A/B against the persistent form)
   static const bool grid_only = [] { const char *e = getenv("RMIMO_DECODE_GRID"); return e && e[0] == '1'; }();
   d.all_occ = (h->M_occ == h->M && !grid_only) ? 1 : 0;
+  static const bool dprof = [] { const char *e = getenv("RMIMO_DEC_PROF"); return e && e[0] == '1'; }();
+  if (dprof) {
+    if (!h->sc_prof.p) HIPCHK(h->sc_prof.ensure(20));
+    HIPCHK(hipMemsetAsync(h->sc_prof.p, 0, 5 * sizeof(unsigned long long), s));
+    d.prof = h->sc_prof.p;
+  }
   hipEvent_t e = h->timer.begin(s);
-  launch_decode(d, h->log2M, F, s);
+  const uint32_t parts = launch_decode(d, h->log2M, F, s);
   h->timer.end(5, e, s);
+  if (dprof) {   // diagnostics: per-item cycle split of the decode kernel
+    unsigned long long v[5];
+    HIPCHK(hipMemcpyAsync(v, h->sc_prof.p, sizeof(v), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    const double it = v[0] ? (double)v[0] : 1.0;
+    fprintf(stderr, "dec_prof items %llu cycles/item load %.0f fft %.0f apply %.0f reduce %.0f\n",
+            v[0], v[1] / it, v[2] / it, v[3] / it, v[4] / it);
+  }
   EvmArgs ea{};
-  ea.N = h->N; ea.max_out = max_out; ea.info = h->info.p; ea.evm_part = h->evm_part.p;
+  ea.N = h->N; ea.max_out = max_out; ea.parts = parts; ea.info = h->info.p;
+  ea.evm_part = h->evm_part.p;
   ea.evm_out = h->evm_out.p;
   e = h->timer.begin(s);
   launch_evm(ea, F, s);

@@ -18,90 +18,107 @@ namespace mimo {
 MIMO_DEV int lds_pad(int i) { return i + (i >> 5); }
 constexpr int lds_padded_len(int n) { return n + (n >> 5); }
 
+// complex values as 2-wide fp32 vectors: adds, multiplies and FMAs on them lower to the
+// packed v_pk_add/mul/fma_f32 instructions (two lanes of work per VALU op), with swizzles and
+// negations folded into op_sel / neg modifiers
+typedef float v2f __attribute__((ext_vector_type(2)));
+
+MIMO_DEV v2f vmul(v2f a, v2f b) {          // a * b
+  const v2f bs = {-b.y, b.x};
+  return __builtin_elementwise_fma(a.yy, bs, a.xx * b);
+}
+MIMO_DEV v2f vmulc(v2f a, v2f b) {         // a * conj(b)
+  const v2f as = {a.y, -a.x};
+  return __builtin_elementwise_fma(b.yy, as, b.xx * a);
+}
+
 template <bool INV>
-MIMO_DEV float2 twiddle(const float2 *__restrict__ tw, int idx) {
-  float2 w = tw[idx];
-  return INV ? make_float2(w.x, -w.y) : w;
+MIMO_DEV v2f twiddle(const float2 *__restrict__ tw, int idx) {
+  const float2 w = tw[idx];
+  return INV ? v2f{w.x, -w.y} : v2f{w.x, w.y};
 }
 
 // (x + iy) * (-i) forward, * (+i) inverse
 template <bool INV>
-MIMO_DEV float2 rot_mi(float2 a) {
-  return INV ? make_float2(-a.y, a.x) : make_float2(a.y, -a.x);
+MIMO_DEV v2f rot_mi(v2f a) {
+  return INV ? v2f{-a.y, a.x} : v2f{a.y, -a.x};
 }
 
 template <int R, bool INV>
-MIMO_DEV void dft_small(float2 *a) {
+MIMO_DEV void dft_small(v2f *a) {
   if constexpr (R == 2) {
-    float2 t0 = cadd(a[0], a[1]), t1 = csub(a[0], a[1]);
+    const v2f t0 = a[0] + a[1], t1 = a[0] - a[1];
     a[0] = t0; a[1] = t1;
   } else if constexpr (R == 4) {
-    float2 b0 = cadd(a[0], a[2]), b1 = csub(a[0], a[2]);
-    float2 b2 = cadd(a[1], a[3]), b3 = rot_mi<INV>(csub(a[1], a[3]));
-    a[0] = cadd(b0, b2); a[2] = csub(b0, b2);
-    a[1] = cadd(b1, b3); a[3] = csub(b1, b3);
+    const v2f b0 = a[0] + a[2], b1 = a[0] - a[2];
+    const v2f b2 = a[1] + a[3], b3 = rot_mi<INV>(a[1] - a[3]);
+    a[0] = b0 + b2; a[2] = b0 - b2;
+    a[1] = b1 + b3; a[3] = b1 - b3;
   } else {
     static_assert(R == 8, "radix");
     const float c = 0.70710678118654752f;
-    float2 b0 = cadd(a[0], a[4]), b4 = csub(a[0], a[4]);
-    float2 b1 = cadd(a[1], a[5]), b5 = csub(a[1], a[5]);
-    float2 b2 = cadd(a[2], a[6]), b6 = csub(a[2], a[6]);
-    float2 b3 = cadd(a[3], a[7]), b7 = csub(a[3], a[7]);
+    const v2f b0 = a[0] + a[4], b4 = a[0] - a[4];
+    const v2f b1 = a[1] + a[5];
+    v2f b5 = a[1] - a[5];
+    const v2f b2 = a[2] + a[6];
+    v2f b6 = a[2] - a[6];
+    const v2f b3 = a[3] + a[7];
+    v2f b7 = a[3] - a[7];
+    b6 = rot_mi<INV>(b6);                                    // * W8^2 = -i (fwd)
     if (!INV) {
-      b5 = make_float2(c * (b5.x + b5.y), c * (b5.y - b5.x));   // * W8^1
-      b6 = make_float2(b6.y, -b6.x);                            // * W8^2 = -i
-      b7 = make_float2(c * (b7.y - b7.x), -c * (b7.x + b7.y));  // * W8^3
+      b5 = c * (b5 + v2f{b5.y, -b5.x});                      // * W8^1
+      b7 = c * (v2f{b7.y, -b7.x} - b7);                      // * W8^3
     } else {
-      b5 = make_float2(c * (b5.x - b5.y), c * (b5.x + b5.y));
-      b6 = make_float2(-b6.y, b6.x);
-      b7 = make_float2(-c * (b7.x + b7.y), c * (b7.x - b7.y));
+      b5 = c * (b5 + v2f{-b5.y, b5.x});
+      b7 = c * (v2f{-b7.y, b7.x} - b7);
     }
-    float2 c0 = cadd(b0, b2), c2 = csub(b0, b2);
-    float2 c1 = cadd(b1, b3), c3 = rot_mi<INV>(csub(b1, b3));
-    float2 c4 = cadd(b4, b6), c6 = csub(b4, b6);
-    float2 c5 = cadd(b5, b7), c7 = rot_mi<INV>(csub(b5, b7));
-    a[0] = cadd(c0, c1); a[4] = csub(c0, c1);
-    a[2] = cadd(c2, c3); a[6] = csub(c2, c3);
-    a[1] = cadd(c4, c5); a[5] = csub(c4, c5);
-    a[3] = cadd(c6, c7); a[7] = csub(c6, c7);
+    const v2f c0 = b0 + b2, c2 = b0 - b2;
+    const v2f c1 = b1 + b3, c3 = rot_mi<INV>(b1 - b3);
+    const v2f c4 = b4 + b6, c6 = b4 - b6;
+    const v2f c5 = b5 + b7, c7 = rot_mi<INV>(b5 - b7);
+    a[0] = c0 + c1; a[4] = c0 - c1;
+    a[2] = c2 + c3; a[6] = c2 - c3;
+    a[1] = c4 + c5; a[5] = c4 - c5;
+    a[3] = c6 + c7; a[7] = c6 - c7;
   }
 }
 
 // one Stockham pass: sub-transform size NS -> NS*R
-template <int N, int R, int NS, int T, int B, bool INV>
-MIMO_DEV void fft_pass(float2 *buf, const float2 *__restrict__ tw) {
+template <int N, int R, int NS, int T, int B, bool INV, int TWN>
+MIMO_DEV void fft_pass(float2 *buf, const float2 *__restrict__ tw, int tid) {
   constexpr int NB = N / R;
   constexpr int TOT = NB * B;
   constexpr int PER = (TOT + T - 1) / T;
   constexpr int PB = lds_padded_len(N);
-  float2 a[PER][R];
+  v2f *vb = reinterpret_cast<v2f *>(buf);
+  v2f a[PER][R];
 #pragma unroll
   for (int q = 0; q < PER; q++) {
-    const int g = threadIdx.x + q * T;
+    const int g = tid + q * T;
     if ((TOT % T == 0) || g < TOT) {
       const int b = g / NB, j = g % NB;
-      const float2 *base = buf + b * PB;
+      const v2f *base = vb + b * PB;
 #pragma unroll
       for (int r = 0; r < R; r++) a[q][r] = base[lds_pad(j + r * NB)];
       if constexpr (NS > 1) {
         // one table read per butterfly; the other R-2 twiddles are products of it
         // (<= 3 roundings deep, well inside the fp32 FFT error budget)
         const int k = j % NS;
-        constexpr int STEP = kTwN / (NS * R);
-        float2 w[R];
+        constexpr int STEP = TWN / (NS * R);
+        v2f w[R];
         w[1] = twiddle<INV>(tw, k * STEP);
         if constexpr (R >= 4) {
-          w[2] = cmul(w[1], w[1]);
-          w[3] = cmul(w[2], w[1]);
+          w[2] = vmul(w[1], w[1]);
+          w[3] = vmul(w[2], w[1]);
         }
         if constexpr (R == 8) {
-          w[4] = cmul(w[2], w[2]);
-          w[5] = cmul(w[4], w[1]);
-          w[6] = cmul(w[3], w[3]);
-          w[7] = cmul(w[4], w[3]);
+          w[4] = vmul(w[2], w[2]);
+          w[5] = vmul(w[4], w[1]);
+          w[6] = vmul(w[3], w[3]);
+          w[7] = vmul(w[4], w[3]);
         }
 #pragma unroll
-        for (int r = 1; r < R; r++) a[q][r] = cmul(a[q][r], w[r]);
+        for (int r = 1; r < R; r++) a[q][r] = vmul(a[q][r], w[r]);
       }
       dft_small<R, INV>(a[q]);
     }
@@ -109,12 +126,12 @@ MIMO_DEV void fft_pass(float2 *buf, const float2 *__restrict__ tw) {
   __syncthreads();
 #pragma unroll
   for (int q = 0; q < PER; q++) {
-    const int g = threadIdx.x + q * T;
+    const int g = tid + q * T;
     if ((TOT % T == 0) || g < TOT) {
       const int b = g / NB, j = g % NB;
       const int k = j % NS;
       const int o = (j / NS) * NS * R + k;
-      float2 *base = buf + b * PB;
+      v2f *base = vb + b * PB;
 #pragma unroll
       for (int r = 0; r < R; r++) base[lds_pad(o + r * NS)] = a[q][r];
     }
@@ -122,21 +139,37 @@ MIMO_DEV void fft_pass(float2 *buf, const float2 *__restrict__ tw) {
   __syncthreads();
 }
 
-template <int N, int NS, int REM, int T, int B, bool INV>
-MIMO_DEV void fft_passes(float2 *buf, const float2 *__restrict__ tw) {
+template <int N, int NS, int REM, int T, int B, bool INV, int TWN>
+MIMO_DEV void fft_passes(float2 *buf, const float2 *__restrict__ tw, int tid) {
   if constexpr (REM > 0) {
     constexpr int LR = (REM == 4) ? 2 : ((REM >= 3) ? 3 : REM);
     constexpr int R = 1 << LR;
-    fft_pass<N, R, NS, T, B, INV>(buf, tw);
-    fft_passes<N, NS * R, REM - LR, T, B, INV>(buf, tw);
+    fft_pass<N, R, NS, T, B, INV, TWN>(buf, tw, tid);
+    fft_passes<N, NS * R, REM - LR, T, B, INV, TWN>(buf, tw, tid);
   }
 }
 
 // B transforms of 2^LOG2N points at buf[b * lds_padded_len(N) + lds_pad(i)]. Caller must
 // __syncthreads() after filling buf; on return buf holds the result (barrier included).
+// tw is the process-wide kTwN-entry table (global memory) ...
 template <int LOG2N, int T, int B, bool INV>
 MIMO_DEV void fft_lds(float2 *buf, const float2 *__restrict__ tw) {
-  fft_passes<(1 << LOG2N), 1, LOG2N, T, B, INV>(buf, tw);
+  fft_passes<(1 << LOG2N), 1, LOG2N, T, B, INV, kTwN>(buf, tw, (int)threadIdx.x);
+}
+
+// ... or an N/2-entry table in LDS (tw[m] = e^{-2 pi i m / N}, see fill_twiddles_lds): no
+// vector-memory wait inside the passes, so loads in flight (a prefetched next item) are not
+// drained by the first twiddle read. tid is threadIdx.x, passed in so a persistent caller
+// can keep the per-pass address arithmetic inside its loop (no hoisted, spilled invariants).
+template <int LOG2N, int T, int B, bool INV>
+MIMO_DEV void fft_lds_twl(float2 *buf, const float2 *tw_lds, int tid) {
+  fft_passes<(1 << LOG2N), 1, LOG2N, T, B, INV, (1 << LOG2N)>(buf, tw_lds, tid);
+}
+
+template <int LOG2N, int T>
+MIMO_DEV void fill_twiddles_lds(float2 *tw_lds, const float2 *__restrict__ tw) {
+  constexpr int N = 1 << LOG2N;
+  for (int m = threadIdx.x; m < N / 2; m += T) tw_lds[m] = tw[m * (kTwN / N)];
 }
 
 }  // namespace mimo

@@ -143,16 +143,20 @@ struct DecodeArgs {
   const uint8_t *ref_idx;
   uint64_t ref_seed, frame_id0;
   Qam qam;
-  double *evm_part;                // [F][max_out][N][3]
+  double *evm_part;                // [F][max_out][parts][N][3]
   const float2 *tw;
   uint32_t n_frames;
   int all_occ;                     // every subcarrier occupied (j == k): vector stores
   uint32_t n_cu;                   // compute units (persistent grid size)
+  unsigned long long *prof;        // diagnostics: [items, load, fft, apply, reduce] cycles
 };
-void launch_decode(const DecodeArgs &a, int log2M, uint32_t n_frames, hipStream_t s);
+// returns the number of EVM partial sets written per symbol (see EvmArgs::parts)
+uint32_t launch_decode(const DecodeArgs &a, int log2M, uint32_t n_frames, hipStream_t s);
+constexpr uint32_t kMaxEvmParts = 16;
 
 struct EvmArgs {
   uint32_t N, max_out;
+  uint32_t parts;                  // partial sets per symbol (launch_decode's return value)
   const FrameInfo *info;
   const double *evm_part;
   double *evm_out;                 // [F][N][3]

@@ -3,11 +3,12 @@
 Captured frames are independent: G, W and the sync state are per frame, so the receive path
 shards with no exchange on the data path. Rank r of W owns frames [r*F, (r+1)*F) of the job
 (its synthetic frame ids, or its own capture stream). The one collective is the reduction
-of a few counters after the timed region: the sums of samples, frames received, EVM
-numerator/denominator and symbol errors, and the max of the per-rank elapsed time.
+of a few counters after the timed region: the sums of samples, frames received, decoded
+symbols, EVM numerator/denominator and symbol errors, and the max of the per-rank elapsed
+time.
 """
 
-STAT_KEYS = ("samples", "frames_ok", "evm_num", "evm_den", "errors")
+STAT_KEYS = ("samples", "frames_ok", "symbols", "evm_num", "evm_den", "errors")
 
 
 def frame_ids(rank, frames_per_rank):

@@ -42,8 +42,8 @@ def _frame_stats(name):
     if ok:
         _, en, ed, er = ref.demap_evm(sym, int(g["qam"]), g["tx_idx"][:, :len(sym)])
         num, den, err = float(np.sum(en)), float(np.sum(ed)), float(np.sum(er))
-    return dict(samples=float(g["rx"].size), frames_ok=ok, evm_num=num, evm_den=den,
-                errors=err)
+    return dict(samples=float(g["rx"].size), frames_ok=ok, symbols=float(len(sym)), evm_num=num,
+                evm_den=den, errors=err)
 
 
 def _worker(rank, world, port, frames_per_rank, q):
@@ -74,7 +74,7 @@ def test_frame_ids_partition():
 
 
 def test_reduce_stats_single_process_is_identity():
-    s = dict(samples=10, frames_ok=1, evm_num=2.0, evm_den=4.0, errors=3)
+    s = dict(samples=10, frames_ok=1, symbols=5, evm_num=2.0, evm_den=4.0, errors=3)
     tot, e = reduce_stats(s, 1.5, None)
     assert tot == {k: float(v) for k, v in s.items()} and e == 1.5
 
