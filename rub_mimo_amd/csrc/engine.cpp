@@ -218,7 +218,8 @@ struct mimo_rx {
   DevBuf<FrameInfo> info;
   DevBuf<float2> G, W;
   DevBuf<float> gain;
-  DevBuf<double> nvp, evm_part, evm_out;
+  DevBuf<double> nvp, evm_part, evm_out, lspart;
+  size_t cap_lspart = 0;
   DevBuf<unsigned long long> n_exact;   // S&C exact fp32 recomputes (diagnostic)
   DevBuf<uint32_t> queue;               // S&C work-queue head, hot-item count
   DevBuf<ScHot> hot;                    // S&C items awaiting exact resolution
@@ -265,7 +266,7 @@ int ensure_workspace(mimo_rx *h, uint32_t F, uint64_t chunks, uint64_t evm_entri
     HIPCHK(h->G.ensure((size_t)nf * h->M * h->N * h->N));
     HIPCHK(h->W.ensure((size_t)nf * h->M * h->N * h->N));
     HIPCHK(h->gain.ensure((size_t)nf * h->M));
-    HIPCHK(h->nvp.ensure((size_t)nf * h->N * h->N));
+    HIPCHK(h->nvp.ensure((size_t)nf * 64));   // >= ceil(M/256) partials per frame
     HIPCHK(h->evm_out.ensure((size_t)nf * h->N * 3));
     h->cap_frames = nf;
     HIPCHK(h->rec.ensure((size_t)nf * h->cap_chunks));
@@ -389,7 +390,16 @@ int run_estimate(mimo_rx *h, const float2 *iq, uint64_t stride, uint32_t F, uint
   la.N = h->N; la.M = h->M; la.nac = h->nac; la.n_slots = h->n_slots;
   la.keys = h->keys.p; la.s1sign = h->s1sign.p; la.occ_index = h->occ.p;
   la.keep_bias = h->keep_bias; la.scale = h->ls_scale; la.info = h->info.p;
-  la.G = h->G.p; la.nv_part = h->nvp.p; la.tw = h->tw;
+  la.n_groups = (h->nac + kLsCodesPerGroup - 1) / kLsCodesPerGroup;
+  la.n_nvp = (h->M + 255) / 256;
+  {
+    const size_t need = (size_t)F * h->N * h->N * la.n_groups * 3 * h->M;
+    if (need > h->cap_lspart) {
+      HIPCHK(h->lspart.ensure(need));
+      h->cap_lspart = need;
+    }
+  }
+  la.G = h->G.p; la.part = h->lspart.p; la.nv_part = h->nvp.p; la.tw = h->tw;
   e = h->timer.begin(s);
   launch_ls(la, h->log2M, F, s);
   h->timer.end(3, e, s);
@@ -397,7 +407,8 @@ int run_estimate(mimo_rx *h, const float2 *iq, uint64_t stride, uint32_t F, uint
   wa.N = h->N; wa.M = h->M; wa.M_occ = h->M_occ; wa.nac = h->nac; wa.SL = h->SL;
   wa.n_slots = h->n_slots; wa.detector = h->det; wa.noise_var = h->noise_var;
   wa.nv_norm = h->nv_norm; wa.occ_index = h->occ.p; wa.G = h->G.p; wa.W = h->W.p;
-  wa.gain = h->gain.p; wa.nv_part = h->nvp.p; wa.keys = h->keys.p; wa.win_len = h->win_len;
+  wa.gain = h->gain.p; wa.nv_part = h->nvp.p; wa.n_nvp = la.n_nvp; wa.keys = h->keys.p;
+  wa.win_len = h->win_len;
   wa.info = h->info.p;
   e = h->timer.begin(s);
   launch_weights(wa, F, s);

@@ -114,79 +114,100 @@ MIMO_DEV uint32_t key_index(unsigned long long k) {
 }
 
 // ------------------------------------------------------------------------------------
+// LS estimate, two stages. ls_kernel: one workgroup per (frame, rx, tx, code group) FFTs the
+// group's CB access codes as received on rx (the window at the search's corr index) and
+// writes the group's per-subcarrier sums of X/S1 (S1 = +-1, framing.cc:811) and |X/S1|^2 in
+// fp64. ls_combine_kernel: per (frame, subcarrier) the groups are summed in fixed order into
+// G = (I + sum) * dft_normalizer / nac (framing.cc:809-824, identity bias from :309-311) and
+// the training-residual variance sum |v - mean|^2 for the MMSE noise estimate.
 template <int LOG2M, int T, int CB>
 __global__ __launch_bounds__(T) void ls_kernel(LsArgs a) {
   constexpr int M = 1 << LOG2M, PB = lds_padded_len(M), PER = M / T;
   extern __shared__ __attribute__((aligned(16))) float2 lds[];
-  __shared__ double red[T / 64];
   const uint32_t f = blockIdx.y;
   const FrameInfo &I = a.info[f];
   if (I.status != 0) return;
-  const uint32_t r = blockIdx.x / a.N, t = blockIdx.x % a.N;
+  const uint32_t P = a.n_groups;
+  const uint32_t rt = blockIdx.x / P, grp = blockIdx.x % P;
+  const uint32_t r = rt / a.N, t = rt % a.N;
   const int tid = threadIdx.x;
   const float2 *__restrict__ x = a.iq + ((uint64_t)f * a.N + r) * a.stride;
   const int64_t L = (int64_t)a.frame_len;
-  float2 acc[PER];
-  double sr[PER], si[PER], s2[PER];
-#pragma unroll
-  for (int q = 0; q < PER; q++) {
-    const int k = tid + q * T;
-    const bool diag = a.keep_bias && (r == t) && (a.occ_index[k] >= 0);
-    acc[q] = make_float2(diag ? 1.0f : 0.0f, 0.0f);   // framing.cc:309-311
-    sr[q] = si[q] = s2[q] = 0.0;
-  }
-  for (uint32_t c0 = 0; c0 < a.nac; c0 += CB) {
-    const uint32_t nb = min((uint32_t)CB, a.nac - c0);
-    for (int b = 0; b < CB; b++) {
-      int64_t abs0 = 0;
-      if (b < (int)nb) {
-        const uint32_t ac = (c0 + b) * a.N + t;
-        abs0 = I.base + key_index(a.keys[((uint64_t)f * a.N + r) * a.n_slots + 1 + ac]);
-      }
+  const uint32_t c0 = grp * CB;
+  const uint32_t nb = min((uint32_t)CB, a.nac - c0);
+  for (int b = 0; b < CB; b++) {
+    int64_t abs0 = 0;
+    if (b < (int)nb) {
+      const uint32_t ac = (c0 + b) * a.N + t;
+      abs0 = I.base + key_index(a.keys[((uint64_t)f * a.N + r) * a.n_slots + 1 + ac]);
+    }
+    const bool inb = b < (int)nb && abs0 >= 0 && abs0 + M <= L;
+    if (inb && (abs0 & 1) == 0) {   // 16-byte loads of two samples
+      const float4 *x4 = reinterpret_cast<const float4 *>(x + abs0);
+      for (int i = tid; i < M / 2; i += T)
+        *reinterpret_cast<float4 *>(lds + b * PB + lds_pad(2 * i)) = x4[i];
+    } else {
       for (int i = tid; i < M; i += T) {
         const int64_t n = abs0 + i;
         lds[b * PB + lds_pad(i)] =
             (b < (int)nb && n >= 0 && n < L) ? x[n] : make_float2(0.0f, 0.0f);
       }
     }
-    __syncthreads();
-    fft_lds<LOG2M, T, CB, false>(lds, a.tw);
-    for (int b = 0; b < (int)nb; b++) {
-      const int8_t *sg = a.s1sign + ((size_t)t * a.nac + c0 + b) * M;
-#pragma unroll
-      for (int q = 0; q < PER; q++) {
-        const int k = tid + q * T;
-        const int s = sg[k];
-        if (s == 0) continue;                      // null subcarrier
-        const float2 X = lds[b * PB + lds_pad(k)];
-        const float2 v = (s > 0) ? X : cneg(X);    // X / S1 with S1 = +-1 (framing.cc:811)
-        acc[q] = cadd(acc[q], v);
-        sr[q] += (double)v.x;
-        si[q] += (double)v.y;
-        s2[q] += (double)v.x * v.x + (double)v.y * v.y;
-      }
-    }
-    __syncthreads();
   }
-  double nv = 0.0;
+  __syncthreads();
+  fft_lds<LOG2M, T, CB, false>(lds, a.tw);
+  double *pp = a.part + (((uint64_t)f * a.N * a.N + rt) * P + grp) * 3 * M;
 #pragma unroll
   for (int q = 0; q < PER; q++) {
     const int k = tid + q * T;
+    double sr = 0.0, si = 0.0, s2 = 0.0;
+    for (int b = 0; b < (int)nb; b++) {
+      const int sg = a.s1sign[((size_t)t * a.nac + c0 + b) * M + k];
+      if (sg == 0) continue;                     // null subcarrier
+      const float2 X = lds[b * PB + lds_pad(k)];
+      const float2 v = (sg > 0) ? X : cneg(X);   // X / S1
+      sr += (double)v.x;
+      si += (double)v.y;
+      s2 += (double)v.x * v.x + (double)v.y * v.y;
+    }
+    pp[k] = sr;
+    pp[M + k] = si;
+    pp[2 * M + k] = s2;
+  }
+}
+
+__global__ __launch_bounds__(256) void ls_combine_kernel(LsArgs a) {
+  __shared__ double red[4];
+  const uint32_t f = blockIdx.y;
+  const FrameInfo &I = a.info[f];
+  if (I.status != 0) return;
+  const uint32_t M = a.M, N = a.N, P = a.n_groups;
+  const uint32_t k = blockIdx.x * 256 + threadIdx.x;
+  double nv = 0.0;
+  if (k < M) {
     const bool occ = a.occ_index[k] >= 0;
-    const float2 g = occ ? make_float2(acc[q].x * a.scale, acc[q].y * a.scale)   // :821
-                         : make_float2(0.0f, 0.0f);
-    a.G[(((uint64_t)f * M + k) * a.N + r) * a.N + t] = g;
-    if (occ) nv += s2[q] - (sr[q] * sr[q] + si[q] * si[q]) / (double)a.nac;
+    for (uint32_t rt = 0; rt < N * N; rt++) {
+      const double *pp = a.part + ((uint64_t)f * N * N + rt) * P * 3 * M;
+      double sr = 0.0, si = 0.0, s2 = 0.0;
+      for (uint32_t g = 0; g < P; g++) {
+        sr += pp[(uint64_t)g * 3 * M + k];
+        si += pp[(uint64_t)g * 3 * M + M + k];
+        s2 += pp[(uint64_t)g * 3 * M + 2 * M + k];
+      }
+      const uint32_t r = rt / N, t = rt % N;
+      const double bias = (a.keep_bias && r == t) ? 1.0 : 0.0;
+      a.G[(((uint64_t)f * M + k) * N + r) * N + t] =
+          occ ? make_float2((float)((bias + sr) * a.scale), (float)(si * a.scale))
+              : make_float2(0.0f, 0.0f);
+      if (occ) nv += s2 - (sr * sr + si * si) / (double)a.nac;
+    }
   }
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) nv += __shfl_xor(nv, off);
-  if ((tid & 63) == 0) red[tid >> 6] = nv;
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = nv;
   __syncthreads();
-  if (tid == 0) {
-    double s = 0.0;
-    for (int w = 0; w < T / 64; w++) s += red[w];
-    a.nv_part[(uint64_t)f * a.N * a.N + r * a.N + t] = s;
-  }
+  if (threadIdx.x == 0)
+    a.nv_part[(uint64_t)f * a.n_nvp + blockIdx.x] = red[0] + red[1] + red[2] + red[3];
 }
 
 // ------------------------------------------------------------------------------------
@@ -253,7 +274,7 @@ __global__ __launch_bounds__(256) void weights_kernel(WeightArgs a) {
   double s2 = (double)a.noise_var;
   if (a.noise_var < 0.0f) {
     double acc = 0.0;
-    for (uint32_t e = 0; e < N * N; e++) acc += a.nv_part[(uint64_t)f * N * N + e];
+    for (uint32_t e = 0; e < a.n_nvp; e++) acc += a.nv_part[(uint64_t)f * a.n_nvp + e];
     s2 = (double)(float)(acc * a.nv_norm);
   }
   if (blockIdx.x == 0 && threadIdx.x == 0) {
@@ -385,11 +406,13 @@ static void ls_dispatch(const LsArgs &a, int log2M, uint32_t nf, hipStream_t s) 
     if (log2M == LOG2M) {
       constexpr int M = 1 << LOG2M;
       constexpr int T = M < 256 ? M : 256;
-      constexpr int CB = (8192 / M) < 8 ? (8192 / M) : 8;
+      constexpr int CB = kLsCodesPerGroup;
       const size_t shm = sizeof(float2) * lds_padded_len(M) * CB;
       (void)hipFuncSetAttribute((const void *)ls_kernel<LOG2M, T, CB>,
                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
-      hipLaunchKernelGGL((ls_kernel<LOG2M, T, CB>), dim3(a.N * a.N, nf), dim3(T), shm, s, a);
+      hipLaunchKernelGGL((ls_kernel<LOG2M, T, CB>), dim3(a.N * a.N * a.n_groups, nf), dim3(T),
+                         shm, s, a);
+      hipLaunchKernelGGL(ls_combine_kernel, dim3((a.M + 255) / 256, nf), dim3(256), 0, s, a);
       return;
     }
     ls_dispatch<LOG2M + 1>(a, log2M, nf, s);

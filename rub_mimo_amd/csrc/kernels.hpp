@@ -101,9 +101,13 @@ struct LsArgs {
   float scale;                     // dft_normalizer / float(nac) (framing.cc:821)
   const FrameInfo *info;
   float2 *G;                       // [F][M][N][N]
-  double *nv_part;                 // [F][N*N]
+  double *part;                    // [F][N*N][n_groups][3][M] per-group sums (ls_kernel)
+  uint32_t n_groups;               // ceil(nac / kLsCodesPerGroup)
+  double *nv_part;                 // [F][n_nvp] residual-variance partials
+  uint32_t n_nvp;                  // ceil(M / 256)
   const float2 *tw;
 };
+constexpr uint32_t kLsCodesPerGroup = 4;   // access codes FFT'd per LS workgroup
 void launch_ls(const LsArgs &a, int log2M, uint32_t n_frames, hipStream_t s);
 
 // per-subcarrier weights, framing.cc:826-831 -> 1344-1367 (+ NxN ZF/MMSE)
@@ -117,6 +121,7 @@ struct WeightArgs {
   float2 *W;                       // [F][N(out)][N(rx)][M]
   float *gain;                     // [F][M]
   const double *nv_part;
+  uint32_t n_nvp;
   const unsigned long long *keys;
   uint64_t win_len;
   FrameInfo *info;
