@@ -210,6 +210,43 @@ def test_batch_frames_are_independent():
     assert res[4]["status"] == _lib.FRAME_NO_SYNC
 
 
+def test_repeated_batch_graph_replay_is_identical():
+    """A repeated process() call is captured into a HIP graph and replayed (engine.cpp); its
+    results, symbols and indices must equal the direct launches bit for bit, and a changed
+    argument must fall back to direct launches."""
+    import torch
+    from rub_mimo_amd.receiver import Synthesizer, SynthParams
+    M, cp, N, nac, pid, F = 256, 19, 4, 4, 24, 3
+    sp = SynthParams(M=M, cp_len=cp, num_streams=N, num_access_codes=nac, pid=pid,
+                     qam_order=16, seed=5, snr_db=30.0)
+    syn = Synthesizer(sp)
+    L = sp.max_frame_len()
+    dev = torch.device("cuda", 0)
+    iq = torch.empty((F, N, L), dtype=torch.complex64, device=dev)
+    syn.generate(iq, L, L, F, frame_id0=0)
+    rx = Receiver(RxParams(M=M, cp_len=cp, num_streams=N, num_access_codes=nac, pid_max=pid,
+                           detector=_lib.DET_MMSE, qam_order=16))
+    sym = torch.zeros((F, N, pid, M), dtype=torch.complex64, device=dev)
+    idx = torch.zeros((F, N, pid, M), dtype=torch.uint8, device=dev)
+    outs = []
+    for it in range(4):   # direct, capture, replay, replay
+        sym.zero_()
+        idx.zero_()
+        rx.process(iq, L, L, F, max_out=pid, out_sym=sym, out_idx=idx, ref_mode=2, ref_seed=5)
+        torch.cuda.synchronize()
+        res = rx.results()
+        outs.append((sym.clone(), idx.clone(), [(r["status"], r["sync_index"],
+                                                 float(np.sum(r["evm_num"]))) for r in res]))
+    for o in outs[1:]:
+        assert torch.equal(o[0], outs[0][0]) and torch.equal(o[1], outs[0][1])
+        assert o[2] == outs[0][2]
+    # a different frame count must not replay the captured batch
+    rx.process(iq, L, L, F - 1, max_out=pid, out_sym=sym, out_idx=idx, ref_mode=2, ref_seed=5)
+    torch.cuda.synchronize()
+    res2 = rx.results(F - 1)
+    assert [(r["status"], r["sync_index"]) for r in res2] == [t[:2] for t in outs[0][2][:F - 1]]
+
+
 def test_gpu_synth_matches_oracle_synth():
     M, cp, N, nac, pid, qam = 128, 16, 4, 3, 5, 64
     S = Synthesizer(SynthParams(M=M, cp_len=cp, num_streams=N, num_access_codes=nac, pid=pid,
