@@ -152,8 +152,8 @@ def main():
         try:
             pm = json.load(open(args.pmc_json))
             cfgm = pm.get("config", {})
-            if (cfgm.get("M"), cfgm.get("streams"), cfgm.get("frames"), cfgm.get("pid")) == (
-                    M, N, F, pid):
+            if (cfgm.get("M"), cfgm.get("streams"), cfgm.get("frames"), cfgm.get("pid"),
+                    cfgm.get("ref_mode")) == (M, N, F, pid, args.ref_mode):
                 traffic = pm.get("decode_hbm_bytes_per_launch")
         except Exception:
             traffic = None
