@@ -212,8 +212,9 @@ def main():
                    "parallelism": "frames sharded across %d GPU(s), no collective" % world},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "kernel": "decode_persistent_kernel<11,4,512>" if M == 2048 and N == 4
-                     else "decode", "bytes_per_launch": dec_bytes,
+                     "kernel": ("decode_reg_kernel<%d,%d>" % (M.bit_length() - 1, N))
+                     if 512 <= M <= 4096 else "decode_persistent_kernel",
+                     "bytes_per_launch": dec_bytes,
                      "symbols_per_launch": n_dec, "bytes_per_symbol": per_sym,
                      "avg_launch_ms": dec_avg_s * 1e3},
         "cpu_baseline": cpu,

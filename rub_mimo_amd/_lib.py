@@ -10,7 +10,8 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "librub_mimo_amd.so")
+# RMIMO_LIB selects a diagnostics build of the same library (e.g. make PROFILE=1 into another path)
+LIB_PATH = os.environ.get("RMIMO_LIB") or os.path.join(_HERE, "librub_mimo_amd.so")
 
 MIMO_OK = 0
 MAX_STREAMS = 8

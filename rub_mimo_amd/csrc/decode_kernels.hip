@@ -400,6 +400,278 @@ void decode_persistent_kernel(DecodeArgs a) {
   }
 }
 
+// ------------------------------------------------------------------------------------
+// Register-resident form (512 <= M <= 4096): one workgroup of T = M/4 threads per (frame,
+// symbol). Antennas go through the FFT in pairs; in every pass each thread holds 8 points of
+// the pair. Pass 0 is a radix-8 butterfly read straight from HBM (samples j + r*M/8 of one
+// antenna: 512 B contiguous per wave instruction); the middle passes exchange through one
+// LDS image per antenna of the pair; the last pass is radix-4 with the thread taking
+// butterfly tid of BOTH antennas, so it ends holding subcarriers tid + T*q (q < 4) of the
+// pair. After all pairs a thread owns 4 subcarriers of every antenna and runs the NxN apply,
+// gain, demap and EVM in registers; every load of the item is issued before its first store
+// (stores count on the same vmcnt as loads on gfx950, so a load behind stores waits for them).
+// 34 KB of LDS and ~100 VGPRs per 512-thread workgroup let several share a CU: one's HBM
+// wait overlaps another's FFT and apply.
+template <int LOG2M>
+struct RegFftPlan {
+  static constexpr int M = 1 << LOG2M;
+  static constexpr int T = M / 4;
+  static constexpr int P8 = (LOG2M - 2) / 3;            // radix-8 passes (pass 0 included)
+  static constexpr int TAIL = (LOG2M - 2) % 3;          // then one radix-2/-4 pass if nonzero
+  static constexpr int NP = P8 + (TAIL ? 1 : 0) + 1;    // ... and a final radix-4 pass
+  static constexpr int radix(int p) { return p < P8 ? 8 : (p == NP - 1 ? 4 : (1 << TAIL)); }
+  static constexpr int ns(int p) {                      // sub-transform size before pass p
+    int n = 1;
+    for (int q = 0; q < p; q++) n *= radix(q);
+    return n;
+  }
+  // butterflies per thread (over the antenna pair) and distinct base twiddles per thread
+  static constexpr int bt(int p) { return 8 / radix(p); }
+  static constexpr int ntw(int p) { return radix(p) == 2 ? 2 : 1; }
+};
+
+// butterfly i of the thread in pass P: antenna (of the pair) and index within the antenna
+template <int LOG2M, int P>
+MIMO_DEV void reg_bfly(int tid, int i, int &g, int &j) {
+  using PL = RegFftPlan<LOG2M>;
+  constexpr int NB = PL::M / PL::radix(P);
+  const int u = tid + i * PL::T;
+  g = u / NB;
+  j = u % NB;
+}
+
+// outputs of pass P (butterfly i at v[i*R .. i*R+R)) -> the pair's LDS images
+template <int LOG2M, int P>
+MIMO_DEV void reg_pass_store(v2f *buf, const v2f *v, int tid) {
+  using PL = RegFftPlan<LOG2M>;
+  constexpr int R = PL::radix(P), NS = PL::ns(P), PB = lds_padded_len(PL::M);
+#pragma unroll
+  for (int i = 0; i < PL::bt(P); i++) {
+    int g, j;
+    reg_bfly<LOG2M, P>(tid, i, g, j);
+    const int o = (j / NS) * NS * R + (j % NS);
+#pragma unroll
+    for (int r = 0; r < R; r++) buf[g * PB + lds_pad(o + r * NS)] = v[i * R + r];
+  }
+}
+
+// inputs of pass P from the LDS images, twiddle, radix-R DFT
+template <int LOG2M, int P>
+MIMO_DEV void reg_pass_load(const v2f *buf, v2f *v, const v2f *w1, int tid) {
+  using PL = RegFftPlan<LOG2M>;
+  constexpr int R = PL::radix(P), NB = PL::M / R, PB = lds_padded_len(PL::M);
+#pragma unroll
+  for (int i = 0; i < PL::bt(P); i++) {
+    int g, j;
+    reg_bfly<LOG2M, P>(tid, i, g, j);
+#pragma unroll
+    for (int r = 0; r < R; r++) v[i * R + r] = buf[g * PB + lds_pad(j + r * NB)];
+    v2f w[R];
+    w[1] = w1[PL::ntw(P) == 2 ? (i & 1) : 0];
+    if constexpr (R >= 4) {
+      w[2] = vmul(w[1], w[1]);
+      w[3] = vmul(w[2], w[1]);
+    }
+    if constexpr (R == 8) {
+      w[4] = vmul(w[2], w[2]);
+      w[5] = vmul(w[4], w[1]);
+      w[6] = vmul(w[3], w[3]);
+      w[7] = vmul(w[4], w[3]);
+    }
+#pragma unroll
+    for (int r = 1; r < R; r++) v[i * R + r] = vmul(v[i * R + r], w[r]);
+    dft_small<R, false>(v + i * R);
+  }
+}
+
+template <int LOG2M, int P>
+MIMO_DEV void reg_passes(v2f *lds, v2f *v, const v2f (*w1)[2], int tid) {
+  using PL = RegFftPlan<LOG2M>;
+  if constexpr (P < PL::NP) {
+    __syncthreads();                        // readers of the previous images are done
+    reg_pass_store<LOG2M, P - 1>(lds, v, tid);
+    __syncthreads();
+    reg_pass_load<LOG2M, P>(lds, v, w1[P], tid);
+    reg_passes<LOG2M, P + 1>(lds, v, w1, tid);
+  }
+}
+
+// hard decision on the square-Gray-QAM level grid: the index (as qam_demap) and the decided
+// point (as qam_point of that index) from one set of level computations, with the oracle's
+// two roundings in (y * inv_scale + L) * 0.5 (no contraction into an FMA)
+MIMO_DEV uint32_t qam_slice(float2 y, const Qam &q, float2 &pt) {
+#pragma clang fp contract(off)
+  const float L = (float)q.L, Lm1 = (float)(q.L - 1);
+  const float tI = (y.x * q.inv_scale + L) * 0.5f;
+  const float tQ = (y.y * q.inv_scale + L) * 0.5f;
+  const float fI = fminf(fmaxf(floorf(tI), 0.0f), Lm1);   // NaN -> 0 (fmaxf), as qam_level
+  const float fQ = fminf(fmaxf(floorf(tQ), 0.0f), Lm1);
+  pt = make_float2((2.0f * fI - Lm1) * q.scale, (2.0f * fQ - Lm1) * q.scale);
+  return (gray_enc((uint32_t)fI) << q.b) | gray_enc((uint32_t)fQ);
+}
+
+template <int LOG2M, int NA>
+__global__ __launch_bounds__(1 << (LOG2M - 2)) void decode_reg_kernel(DecodeArgs a) {
+  using PL = RegFftPlan<LOG2M>;
+  constexpr int M = PL::M, T = PL::T;
+  static_assert(NA % 2 == 0, "antenna pairs");
+  extern __shared__ __attribute__((aligned(16))) float2 lds_raw[];
+  v2f *lds = reinterpret_cast<v2f *>(lds_raw);
+  const int tid = threadIdx.x;
+  const uint32_t f = blockIdx.y, s = blockIdx.x;
+  const FrameInfo &I = a.info[f];
+  const uint32_t n_out = (I.status == 0) ? min(I.n_sym, a.max_out) : 0u;
+  if (s >= n_out) return;                  // uniform per workgroup
+  const int64_t abs0 = I.base + (int64_t)I.i0 + (int64_t)s * a.SL + a.cp;
+  const bool inb = abs0 >= 0 && abs0 + M <= (int64_t)a.frame_len;
+
+  // per-thread base twiddles of passes 1..NP-1: e^{-2 pi i k/(NS R)}, k = j mod NS
+  v2f w1[PL::NP][2];
+#pragma unroll
+  for (int p = 1; p < PL::NP; p++) {
+    const int R = PL::radix(p), NS = PL::ns(p), NB = M / R;
+#pragma unroll
+    for (int i = 0; i < PL::ntw(p); i++) {
+      const int j = (tid + i * T) % NB;
+      w1[p][i] = twiddle<false>(a.tw, (j % NS) * (kTwN / (NS * R)));
+    }
+  }
+
+  v2f X[NA][4];                            // X[r][q]: subcarrier tid + T*q of antenna r
+#pragma unroll
+  for (int g0 = 0; g0 < NA; g0 += 2) {
+    v2f v[8];
+    {                                      // pass 0 straight from HBM
+      const int g = tid / (M / 8), j = tid % (M / 8);
+      const v2f *x = reinterpret_cast<const v2f *>(a.iq + ((uint64_t)f * NA + g0 + g) * a.stride);
+#pragma unroll
+      for (int r = 0; r < 8; r++) {
+        const int64_t n = abs0 + j + r * (M / 8);
+        v[r] = (inb || (n >= 0 && n < (int64_t)a.frame_len)) ? x[n] : v2f{0.0f, 0.0f};
+      }
+      dft_small<8, false>(v);
+    }
+    reg_passes<LOG2M, 1>(lds, v, w1, tid);
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      X[g0][q] = v[q] * a.dn;              // (:561) x dft_normalizer
+      X[g0 + 1][q] = v[4 + q] * a.dn;
+    }
+  }
+
+  // ---- phase A: every load of the apply and demap, then the arithmetic; no stores yet
+  const bool siso = (a.detector == 3);
+  const int ref_mode = a.ref_mode;
+  const float2 *__restrict__ Wf = a.W + (uint64_t)f * NA * NA * M;
+  const float *__restrict__ gf = a.gain + (uint64_t)f * M;
+  int jq[4];
+  float gn[4];
+#pragma unroll
+  for (int q = 0; q < 4; q++) {
+    const int k = tid + T * q;
+    jq[q] = a.all_occ ? k : a.occ_index[k];
+    gn[q] = siso ? 1.0f : gf[k];
+  }
+  uint32_t refb[NA][4];
+  const uint64_t frame_id = a.frame_id0 + f;
+#pragma unroll
+  for (int t = 0; t < NA; t++) {
+    const uint64_t ob = (((uint64_t)f * NA + t) * a.max_out + s) * a.M_occ;
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      refb[t][q] = 0;
+      if (ref_mode == 1 && jq[q] >= 0) refb[t][q] = a.ref_idx[ob + jq[q]];
+    }
+  }
+  float e_num[NA], e_den[NA], e_err[NA];
+#pragma unroll
+  for (int t = 0; t < NA; t++) e_num[t] = e_den[t] = e_err[t] = 0.0f;
+  uint32_t dpk[NA];                        // decided indices, byte q = subcarrier q
+#pragma unroll
+  for (int t = 0; t < NA; t++) dpk[t] = 0;
+#pragma unroll
+  for (int q = 0; q < 4; q++) {
+    const int k = tid + T * q;
+    v2f y[NA];
+    if (siso) {
+#pragma unroll
+      for (int t = 0; t < NA; t++) {
+        y[t] = v2f{0.0f, 0.0f};
+        if (t == (int)a.siso_rx) {
+          const float2 gg = a.G[(((uint64_t)f * M + k) * NA + a.siso_rx) * NA + a.siso_tx];
+          const float2 z = cdiv(make_float2(X[t][q].x, X[t][q].y), gg);
+          y[t] = v2f{z.x, z.y};
+        }
+      }
+    } else {
+#pragma unroll
+      for (int t = 0; t < NA; t++) {
+        y[t] = v2f{0.0f, 0.0f};
+#pragma unroll
+        for (int r = 0; r < NA; r++) {
+          const v2f w = reinterpret_cast<const v2f *>(Wf + ((uint64_t)t * NA + r) * M)[k];
+          y[t] = __builtin_elementwise_fma(w.xx, X[r][q], y[t]);
+          y[t] = __builtin_elementwise_fma(w.yy, v2f{-X[r][q].y, X[r][q].x}, y[t]);
+        }
+        y[t] = y[t] * gn[q];
+      }
+    }
+#pragma unroll
+    for (int t = 0; t < NA; t++) {
+      X[t][q] = y[t];                      // subcarrier q of every antenna is consumed
+      if (jq[q] < 0) continue;
+      const float2 ye = make_float2(y[t].x, y[t].y);
+      float2 sp;
+      const uint32_t d = qam_slice(ye, a.qam, sp);
+      dpk[t] |= d << (8 * q);
+      uint32_t refi = d;
+      if (ref_mode == 1)
+        refi = refb[t][q];
+      else if (ref_mode == 2)
+        refi = (uint32_t)(hash5(a.ref_seed, DOM_DATA, frame_id, t,
+                                (uint64_t)s * a.M_occ + jq[q]) &
+                          (uint64_t)(a.qam.L * a.qam.L - 1));
+      if (refi != d) {                       // symbol error (rare): the transmitted point
+        sp = qam_point(refi, a.qam);
+        e_err[t] += 1.0f;
+      }
+      const float er = ye.x - sp.x, ei = ye.y - sp.y;
+      e_num[t] += er * er + ei * ei;
+      e_den[t] += sp.x * sp.x + sp.y * sp.y;
+    }
+  }
+  // ---- phase B: stores (equalised symbols, indices, per-wave EVM partials)
+#pragma unroll
+  for (int t = 0; t < NA; t++) {
+    const uint64_t ob = (((uint64_t)f * NA + t) * a.max_out + s) * a.M_occ;
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      if (jq[q] < 0) continue;
+      if (a.out_sym) a.out_sym[ob + jq[q]] = make_float2(X[t][q].x, X[t][q].y);
+      if (a.out_idx) a.out_idx[ob + jq[q]] = (uint8_t)(dpk[t] >> (8 * q));
+    }
+  }
+  const int lane = tid & 63, wv = tid >> 6;
+  double *epw = a.evm_part + ((((uint64_t)f * a.max_out + s) * (T / 64) + wv) * NA) * 3;
+#pragma unroll
+  for (int t = 0; t < NA; t++) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+      e_num[t] += __shfl_xor(e_num[t], off);
+      e_den[t] += __shfl_xor(e_den[t], off);
+      e_err[t] += __shfl_xor(e_err[t], off);
+    }
+  }
+  if (lane < NA * 3) {
+    const int t = lane / 3, c = lane % 3;
+    float v = 0.0f;
+#pragma unroll
+    for (int u = 0; u < NA; u++)
+      if (u == t) v = c == 0 ? e_num[u] : (c == 1 ? e_den[u] : e_err[u]);
+    epw[lane] = (double)v;
+  }
+}
+
 // per-frame EVM / symbol-error totals: fixed-order strided partial sums + LDS tree, so the
 // result is bitwise reproducible run to run
 __global__ __launch_bounds__(256) void evm_kernel(EvmArgs a) {
@@ -433,17 +705,21 @@ static uint32_t decode_launch_na(const DecodeArgs &a, uint32_t nf, hipStream_t s
   // persistent kernel: 16 complex per thread per item (4 antennas x 4 subcarriers at C3)
   constexpr int TP0 = (NA * M / 16) < 64 ? 64 : ((NA * M / 16) > 1024 ? 1024 : (NA * M / 16));
   constexpr int TP = TP0 > M / 4 ? M / 4 : TP0;
-  if constexpr (GA == NA && TP >= 64) {
+  if constexpr (LOG2M >= 9 && LOG2M <= 12 && NA % 2 == 0) {
+    // register-resident form, grid (symbol, frame), T = M/4 threads, two LDS images
+    const size_t shm = sizeof(float2) * lds_padded_len(M) * 2;
+    (void)hipFuncSetAttribute((const void *)decode_reg_kernel<LOG2M, NA>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
+    hipLaunchKernelGGL((decode_reg_kernel<LOG2M, NA>), dim3(a.max_out, nf), dim3(M / 4), shm, s,
+                       a);
+    return (M / 4) / 64;
+  }
+  if constexpr (GA == NA && TP >= 64 && LOG2M < 9) {
     if (a.all_occ && nf <= kDecMaxFrames) {
       const size_t shm = sizeof(float2) * (lds_padded_len(M) * NA + M / 2);
-      static const int var = [] { const char *e = getenv("RMIMO_DECODE_VAR"); return e ? atoi(e) : 0; }();
-      // 0: register prefetch of the next item (1 workgroup/CU); 1: the same with stream-
-      // ordered weight loads; 2: no prefetch, 2 workgroups/CU
       auto pick = [&](auto ref) {
         constexpr int R = decltype(ref)::value;
-        return var == 1 ? decode_persistent_kernel<LOG2M, NA, TP, true, true, R>
-             : var == 2 ? decode_persistent_kernel<LOG2M, NA, TP, true, false, R>
-                        : decode_persistent_kernel<LOG2M, NA, TP, false, true, R>;
+        return decode_persistent_kernel<LOG2M, NA, TP, false, true, R>;
       };
       auto kern = a.ref_mode == 1 ? pick(std::integral_constant<int, 1>{})
                 : a.ref_mode == 2 ? pick(std::integral_constant<int, 2>{})
@@ -459,11 +735,15 @@ static uint32_t decode_launch_na(const DecodeArgs &a, uint32_t nf, hipStream_t s
       return TP / 64;
     }
   }
-  const size_t shm = sizeof(float2) * lds_padded_len(M) * GA;
-  (void)hipFuncSetAttribute((const void *)decode_kernel<LOG2M, NA, GA, T>,
-                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
-  hipLaunchKernelGGL((decode_kernel<LOG2M, NA, GA, T>), dim3(a.max_out, nf), dim3(T), shm, s, a);
-  return 1;
+  if constexpr (LOG2M < 9 || LOG2M > 12 || NA % 2 != 0) {
+    const size_t shm = sizeof(float2) * lds_padded_len(M) * GA;
+    (void)hipFuncSetAttribute((const void *)decode_kernel<LOG2M, NA, GA, T>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
+    hipLaunchKernelGGL((decode_kernel<LOG2M, NA, GA, T>), dim3(a.max_out, nf), dim3(T), shm, s,
+                       a);
+    return 1;
+  }
+  return 0;
 }
 
 template <int LOG2M>
