@@ -488,10 +488,12 @@ template <int LOG2M, int P>
 MIMO_DEV void reg_passes(v2f *lds, v2f *v, const v2f (*w1)[2], int tid) {
   using PL = RegFftPlan<LOG2M>;
   if constexpr (P < PL::NP) {
+    int t = tid;                            // opaque per pass: addresses are not hoisted
+    asm volatile("" : "+v"(t));
     __syncthreads();                        // readers of the previous images are done
-    reg_pass_store<LOG2M, P - 1>(lds, v, tid);
+    reg_pass_store<LOG2M, P - 1>(lds, v, t);
     __syncthreads();
-    reg_pass_load<LOG2M, P>(lds, v, w1[P], tid);
+    reg_pass_load<LOG2M, P>(lds, v, w1[P], t);
     reg_passes<LOG2M, P + 1>(lds, v, w1, tid);
   }
 }
@@ -510,8 +512,10 @@ MIMO_DEV uint32_t qam_slice(float2 y, const Qam &q, float2 &pt) {
   return (gray_enc((uint32_t)fI) << q.b) | gray_enc((uint32_t)fQ);
 }
 
-template <int LOG2M, int NA>
-__global__ __launch_bounds__(1 << (LOG2M - 2)) void decode_reg_kernel(DecodeArgs a) {
+template <int LOG2M, int NA, bool SISO>
+__global__ __launch_bounds__(1 << (LOG2M - 2))
+__attribute__((amdgpu_waves_per_eu(4)))
+void decode_reg_kernel(DecodeArgs a) {
   using PL = RegFftPlan<LOG2M>;
   constexpr int M = PL::M, T = PL::T;
   static_assert(NA % 2 == 0, "antenna pairs");
@@ -560,29 +564,23 @@ __global__ __launch_bounds__(1 << (LOG2M - 2)) void decode_reg_kernel(DecodeArgs
   }
 
   // ---- phase A: every load of the apply and demap, then the arithmetic; no stores yet
-  const bool siso = (a.detector == 3);
-  const int ref_mode = a.ref_mode;
   const float2 *__restrict__ Wf = a.W + (uint64_t)f * NA * NA * M;
   const float *__restrict__ gf = a.gain + (uint64_t)f * M;
   int jq[4];
   float gn[4];
+  v2f gs[4];                               // SISO: G[k][rx][tx]
 #pragma unroll
   for (int q = 0; q < 4; q++) {
     const int k = tid + T * q;
     jq[q] = a.all_occ ? k : a.occ_index[k];
-    gn[q] = siso ? 1.0f : gf[k];
-  }
-  uint32_t refb[NA][4];
-  const uint64_t frame_id = a.frame_id0 + f;
-#pragma unroll
-  for (int t = 0; t < NA; t++) {
-    const uint64_t ob = (((uint64_t)f * NA + t) * a.max_out + s) * a.M_occ;
-#pragma unroll
-    for (int q = 0; q < 4; q++) {
-      refb[t][q] = 0;
-      if (ref_mode == 1 && jq[q] >= 0) refb[t][q] = a.ref_idx[ob + jq[q]];
+    if constexpr (SISO) {
+      const float2 gg = a.G[(((uint64_t)f * M + k) * NA + a.siso_rx) * NA + a.siso_tx];
+      gs[q] = v2f{gg.x, gg.y};
+    } else {
+      gn[q] = gf[k];
     }
   }
+  const uint64_t frame_id = a.frame_id0 + f;
   float e_num[NA], e_den[NA], e_err[NA];
 #pragma unroll
   for (int t = 0; t < NA; t++) e_num[t] = e_den[t] = e_err[t] = 0.0f;
@@ -592,28 +590,47 @@ __global__ __launch_bounds__(1 << (LOG2M - 2)) void decode_reg_kernel(DecodeArgs
 #pragma unroll
   for (int q = 0; q < 4; q++) {
     const int k = tid + T * q;
+    // reference indices for the EVM: transmitted (HBM, ref_mode 1), regenerated from the seed
+    // (ref_mode 2) or the decisions themselves (ref_mode 0)
+    uint32_t refq[NA];
+#pragma unroll
+    for (int t = 0; t < NA; t++) {
+      const uint64_t ob = (((uint64_t)f * NA + t) * a.max_out + s) * a.M_occ;
+      refq[t] = 0xFFFFFFFFu;
+      if (a.ref_mode == 1 && jq[q] >= 0) refq[t] = a.ref_idx[ob + jq[q]];
+    }
     v2f y[NA];
-    if (siso) {
+    if constexpr (SISO) {
 #pragma unroll
       for (int t = 0; t < NA; t++) {
         y[t] = v2f{0.0f, 0.0f};
         if (t == (int)a.siso_rx) {
-          const float2 gg = a.G[(((uint64_t)f * M + k) * NA + a.siso_rx) * NA + a.siso_tx];
-          const float2 z = cdiv(make_float2(X[t][q].x, X[t][q].y), gg);
+          const float2 z = cdiv(make_float2(X[t][q].x, X[t][q].y), make_float2(gs[q].x, gs[q].y));
           y[t] = v2f{z.x, z.y};
         }
       }
     } else {
+      // this subcarrier's weights, TB streams' rows in flight together
+      constexpr int TB = NA <= 4 ? NA : 2;
 #pragma unroll
-      for (int t = 0; t < NA; t++) {
-        y[t] = v2f{0.0f, 0.0f};
+      for (int t0 = 0; t0 < NA; t0 += TB) {
+        v2f w[TB][NA];
 #pragma unroll
-        for (int r = 0; r < NA; r++) {
-          const v2f w = reinterpret_cast<const v2f *>(Wf + ((uint64_t)t * NA + r) * M)[k];
-          y[t] = __builtin_elementwise_fma(w.xx, X[r][q], y[t]);
-          y[t] = __builtin_elementwise_fma(w.yy, v2f{-X[r][q].y, X[r][q].x}, y[t]);
+        for (int tb = 0; tb < TB; tb++)
+#pragma unroll
+          for (int r = 0; r < NA; r++)
+            w[tb][r] = reinterpret_cast<const v2f *>(Wf + ((uint64_t)(t0 + tb) * NA + r) * M)[k];
+#pragma unroll
+        for (int tb = 0; tb < TB; tb++) {
+          const int t = t0 + tb;
+          y[t] = v2f{0.0f, 0.0f};
+#pragma unroll
+          for (int r = 0; r < NA; r++) {
+            y[t] = __builtin_elementwise_fma(w[tb][r].xx, X[r][q], y[t]);
+            y[t] = __builtin_elementwise_fma(w[tb][r].yy, v2f{-X[r][q].y, X[r][q].x}, y[t]);
+          }
+          y[t] = y[t] * gn[q];
         }
-        y[t] = y[t] * gn[q];
       }
     }
 #pragma unroll
@@ -624,12 +641,10 @@ __global__ __launch_bounds__(1 << (LOG2M - 2)) void decode_reg_kernel(DecodeArgs
       float2 sp;
       const uint32_t d = qam_slice(ye, a.qam, sp);
       dpk[t] |= d << (8 * q);
-      uint32_t refi = d;
-      if (ref_mode == 1)
-        refi = refb[t][q];
-      else if (ref_mode == 2)
-        refi = (uint32_t)(hash5(a.ref_seed, DOM_DATA, frame_id, t,
-                                (uint64_t)s * a.M_occ + jq[q]) &
+      uint32_t refi = refq[t];
+      if (a.ref_mode == 0) refi = d;
+      else if (a.ref_mode == 2)
+        refi = (uint32_t)(hash5(a.ref_seed, DOM_DATA, frame_id, t, (uint64_t)s * a.M_occ + jq[q]) &
                           (uint64_t)(a.qam.L * a.qam.L - 1));
       if (refi != d) {                       // symbol error (rare): the transmitted point
         sp = qam_point(refi, a.qam);
@@ -672,25 +687,49 @@ __global__ __launch_bounds__(1 << (LOG2M - 2)) void decode_reg_kernel(DecodeArgs
   }
 }
 
-// per-frame EVM / symbol-error totals: fixed-order strided partial sums + LDS tree, so the
-// result is bitwise reproducible run to run
+// per-frame EVM / symbol-error totals, bitwise reproducible run to run: workgroup (frame,
+// chunk) sums a contiguous range of the frame's (symbol, part) entries in a fixed strided order
+// (256/C lanes per component, C = 3N components, coalesced) and an LDS pass in fixed order;
+// the workgroup that completes a frame's last chunk sums the kEvmChunks chunk partials in
+// chunk order (release/acquire on the per-frame counter, which it resets for the next launch)
 __global__ __launch_bounds__(256) void evm_kernel(EvmArgs a) {
   __shared__ double red[256];
-  const uint32_t f = blockIdx.x, c = blockIdx.y, tid = threadIdx.x;
+  __shared__ int s_last;
+  const uint32_t f = blockIdx.x, ch = blockIdx.y, tid = threadIdx.x;
   const FrameInfo &I = a.info[f];
   const uint32_t n_out = (I.status == 0) ? min(I.n_sym, a.max_out) : 0u;
-  const uint32_t per = a.N * 3;
-  const uint64_t n = (uint64_t)n_out * a.parts;    // (symbol, part) pairs, fixed order
+  const uint32_t per = a.N * 3, G = 256 / per;
+  const uint64_t n = (uint64_t)n_out * a.parts;    // (symbol, part) entries, fixed order
+  const uint64_t lo = n * ch / kEvmChunks, hi = n * (ch + 1) / kEvmChunks;
+  const uint32_t g = tid / per, c = tid % per;
+  const double *src = a.evm_part + (uint64_t)f * a.max_out * a.parts * per;
   double v = 0.0;
-  for (uint64_t q = tid; q < n; q += 256)
-    v += a.evm_part[((uint64_t)f * a.max_out * a.parts + q) * per + c];
+  if (g < G)
+    for (uint64_t e = lo + g; e < hi; e += G) v += src[e * per + c];
   red[tid] = v;
   __syncthreads();
-  for (uint32_t w = 128; w > 0; w >>= 1) {
-    if (tid < w) red[tid] += red[tid + w];
-    __syncthreads();
+  double *cp = a.chunk_part + ((uint64_t)f * kEvmChunks + ch) * per;
+  if (tid < per) {
+    double t = 0.0;
+    for (uint32_t q = 0; q < G; q++) t += red[q * per + tid];
+    __hip_atomic_store(cp + tid, t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
-  if (tid == 0) a.evm_out[(uint64_t)f * per + c] = red[0];
+  __syncthreads();
+  if (tid == 0) {
+    const uint32_t done = __hip_atomic_fetch_add(a.counter + f, 1u, __ATOMIC_ACQ_REL,
+                                                 __HIP_MEMORY_SCOPE_AGENT);
+    s_last = (done == kEvmChunks - 1);
+  }
+  __syncthreads();
+  if (!s_last) return;
+  if (tid < per) {
+    double t = 0.0;
+    for (uint32_t q = 0; q < kEvmChunks; q++)
+      t += __hip_atomic_load(a.chunk_part + ((uint64_t)f * kEvmChunks + q) * per + tid,
+                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    a.evm_out[(uint64_t)f * per + tid] = t;
+  }
+  if (tid == 0) __hip_atomic_store(a.counter + f, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // ------------------------------------------------------------------------------------
@@ -705,13 +744,14 @@ static uint32_t decode_launch_na(const DecodeArgs &a, uint32_t nf, hipStream_t s
   // persistent kernel: 16 complex per thread per item (4 antennas x 4 subcarriers at C3)
   constexpr int TP0 = (NA * M / 16) < 64 ? 64 : ((NA * M / 16) > 1024 ? 1024 : (NA * M / 16));
   constexpr int TP = TP0 > M / 4 ? M / 4 : TP0;
-  if constexpr (LOG2M >= 9 && LOG2M <= 12 && NA % 2 == 0) {
+  if constexpr (LOG2M >= 9 && LOG2M <= 12 && (NA == 2 || NA == 4)) {
     // register-resident form, grid (symbol, frame), T = M/4 threads, two LDS images
     const size_t shm = sizeof(float2) * lds_padded_len(M) * 2;
-    (void)hipFuncSetAttribute((const void *)decode_reg_kernel<LOG2M, NA>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
-    hipLaunchKernelGGL((decode_reg_kernel<LOG2M, NA>), dim3(a.max_out, nf), dim3(M / 4), shm, s,
-                       a);
+    auto kern = (a.detector == 3) ? decode_reg_kernel<LOG2M, NA, true>
+                                  : decode_reg_kernel<LOG2M, NA, false>;
+    (void)hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)shm);
+    hipLaunchKernelGGL(kern, dim3(a.max_out, nf), dim3(M / 4), shm, s, a);
     return (M / 4) / 64;
   }
   if constexpr (GA == NA && TP >= 64 && LOG2M < 9) {
@@ -735,7 +775,7 @@ static uint32_t decode_launch_na(const DecodeArgs &a, uint32_t nf, hipStream_t s
       return TP / 64;
     }
   }
-  if constexpr (LOG2M < 9 || LOG2M > 12 || NA % 2 != 0) {
+  if constexpr (LOG2M < 9 || LOG2M > 12 || !(NA == 2 || NA == 4)) {
     const size_t shm = sizeof(float2) * lds_padded_len(M) * GA;
     (void)hipFuncSetAttribute((const void *)decode_kernel<LOG2M, NA, GA, T>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
@@ -768,7 +808,7 @@ uint32_t launch_decode(const DecodeArgs &a, int log2M, uint32_t n_frames, hipStr
 }
 
 void launch_evm(const EvmArgs &a, uint32_t n_frames, hipStream_t s) {
-  hipLaunchKernelGGL(evm_kernel, dim3(n_frames, a.N * 3), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(evm_kernel, dim3(n_frames, kEvmChunks), dim3(256), 0, s, a);
 }
 
 }  // namespace mimo

@@ -219,7 +219,8 @@ struct mimo_rx {
   DevBuf<FrameInfo> info;
   DevBuf<float2> G, W;
   DevBuf<float> gain;
-  DevBuf<double> nvp, evm_part, evm_out, lspart;
+  DevBuf<double> nvp, evm_part, evm_out, lspart, evm_chunk;
+  DevBuf<uint32_t> evm_cnt;             // per-frame chunk counters of evm_kernel (self-resetting)
   size_t cap_lspart = 0;
   DevBuf<unsigned long long> n_exact;   // S&C exact fp32 recomputes (diagnostic)
   DevBuf<uint32_t> queue;               // S&C work-queue head, hot-item count
@@ -273,8 +274,11 @@ int ensure_workspace(mimo_rx *h, uint32_t F, uint64_t chunks, uint64_t evm_entri
     HIPCHK(h->G.ensure((size_t)nf * h->M * h->N * h->N));
     HIPCHK(h->W.ensure((size_t)nf * h->M * h->N * h->N));
     HIPCHK(h->gain.ensure((size_t)nf * h->M));
-    HIPCHK(h->nvp.ensure((size_t)nf * 64));   // >= ceil(M/256) partials per frame
+    HIPCHK(h->nvp.ensure((size_t)nf * h->N * h->N * ((h->M + 255) / 256)));   // ls_combine blocks
     HIPCHK(h->evm_out.ensure((size_t)nf * h->N * 3));
+    HIPCHK(h->evm_chunk.ensure((size_t)nf * kEvmChunks * h->N * 3));
+    HIPCHK(h->evm_cnt.ensure(nf));
+    HIPCHK(hipMemset(h->evm_cnt.p, 0, sizeof(uint32_t) * nf));
     h->cap_frames = nf;
     HIPCHK(h->rec.ensure((size_t)nf * h->cap_chunks));
   }
@@ -398,7 +402,7 @@ int run_estimate(mimo_rx *h, const float2 *iq, uint64_t stride, uint32_t F, uint
   la.keys = h->keys.p; la.s1sign = h->s1sign.p; la.occ_index = h->occ.p;
   la.keep_bias = h->keep_bias; la.scale = h->ls_scale; la.info = h->info.p;
   la.n_groups = (h->nac + kLsCodesPerGroup - 1) / kLsCodesPerGroup;
-  la.n_nvp = (h->M + 255) / 256;
+  la.n_nvp = h->N * h->N * ((h->M + 255) / 256);
   {
     const size_t need = (size_t)F * h->N * h->N * la.n_groups * 3 * h->M;
     if (need > h->cap_lspart) {
@@ -463,6 +467,8 @@ int run_decode(mimo_rx *h, const float2 *iq, uint64_t stride, uint32_t F, uint64
   ea.N = h->N; ea.max_out = max_out; ea.parts = parts; ea.info = h->info.p;
   ea.evm_part = h->evm_part.p;
   ea.evm_out = h->evm_out.p;
+  ea.chunk_part = h->evm_chunk.p;
+  ea.counter = h->evm_cnt.p;
   e = h->timer.begin(s);
   launch_evm(ea, F, s);
   h->timer.end(6, e, s);

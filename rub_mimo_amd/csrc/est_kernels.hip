@@ -13,6 +13,7 @@
 // [0, F-M] are exact linear correlations. First-maximum semantics (strict '>', initial 0,
 // framing.cc:718, 735) are kept by packing (value bits, ~index) into one 64-bit atomicMax.
 #include "fft.hpp"
+#include "fft_reg.hpp"
 #include "kernels.hpp"
 
 namespace mimo {
@@ -109,6 +110,76 @@ __global__ __launch_bounds__(kEstT) void search_kernel(SearchArgs a) {
     atomicMax(&a.keys[((uint64_t)f * a.N + r) * a.n_slots + slot], s_key);
 }
 
+// Register-resident form (F >= 1024): T = F/16 threads, 16 points each. The forward FFT_F
+// reads the window segment straight from HBM in its first pass, its last pass leaves
+// elements j + r*F/8 in the thread, which are multiplied by conj(code spectrum) in place and
+// are exactly the inputs of the inverse's first pass; the inverse's last pass leaves lags
+// j + r*F/8, scored in registers. 2*(NP-1) LDS exchanges per (frame, rx, slot, lag chunk),
+// twiddles loaded once per thread.
+template <int LOG2F>
+__global__ __launch_bounds__((1 << LOG2F) / 16) __attribute__((amdgpu_waves_per_eu(4)))
+void search_reg_kernel(SearchArgs a) {
+  constexpr int PTS = 16;
+  using PL = RegPlan<LOG2F, PTS>;
+  constexpr int F = PL::N;
+  extern __shared__ __attribute__((aligned(16))) float2 lds_raw[];
+  v2f *buf = reinterpret_cast<v2f *>(lds_raw);
+  __shared__ unsigned long long s_key;
+  const uint32_t f = blockIdx.y;
+  const FrameInfo &I = a.info[f];
+  if (I.status != 0) return;
+  const int tid = threadIdx.x;
+  const uint32_t lc = blockIdx.x % a.n_lagc;
+  const uint32_t r = (blockIdx.x / a.n_lagc) % a.N;
+  const uint32_t slot = blockIdx.x / (a.n_lagc * a.N);
+  const int64_t lag0 = (int64_t)lc * a.lagc;
+  const int64_t nl = min((int64_t)a.lagc, (int64_t)a.SL - lag0);
+  const int64_t ws = (int64_t)a.SL * slot + lag0;   // window index of lag 0 of this segment
+  const int64_t abs0 = I.base + ws;
+  const int64_t L = (int64_t)a.frame_len;
+  const v2f *__restrict__ x = reinterpret_cast<const v2f *>(a.iq + ((uint64_t)f * a.N + r) * a.stride);
+  const bool inb = abs0 >= 0 && abs0 + F <= L;
+  v2f v[PTS], cs[PTS];
+#pragma unroll
+  for (int e = 0; e < PTS; e++) {
+    const int64_t n = abs0 + reg_index<LOG2F, PTS>(tid, e);
+    v[e] = (inb || (n >= 0 && n < L)) ? x[n] : v2f{0.0f, 0.0f};
+  }
+  v2f w1[PL::NTW > 0 ? PL::NTW : 1];
+  reg_twiddles<LOG2F, PTS>(w1, a.tw, tid);
+  if (tid == 0) s_key = 0ull;
+  reg_compute<LOG2F, PTS, 0, false>(v, w1);
+  reg_rest<LOG2F, PTS, 1, false>(buf, v, w1, tid);
+  const v2f *__restrict__ csp = reinterpret_cast<const v2f *>(a.codespec + (size_t)slot * F);
+#pragma unroll
+  for (int e = 0; e < PTS; e++) cs[e] = csp[reg_index<LOG2F, PTS>(tid, e)];   // L2-resident
+#pragma unroll
+  for (int e = 0; e < PTS; e++) v[e] = vmulc(v[e], cs[e]);   // X * conj(S_F)
+  reg_compute<LOG2F, PTS, 0, true>(v, w1);
+  reg_rest<LOG2F, PTS, 1, true>(buf, v, w1, tid);
+  const float vs = a.vscale[slot];
+  unsigned long long best = 0ull;
+#pragma unroll
+  for (int e = 0; e < PTS; e++) {
+    const int i = reg_index<LOG2F, PTS>(tid, e);
+    const float val = (v[e].x * v[e].x + v[e].y * v[e].y) * vs;
+    if (i < nl && val > 0.0f) {
+      const unsigned long long key = ((unsigned long long)__float_as_uint(val) << 32) |
+                                     (unsigned long long)(0xFFFFFFFFu - (uint32_t)(ws + i));
+      best = key > best ? key : best;
+    }
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    const unsigned long long o = __shfl_xor(best, off);
+    best = o > best ? o : best;
+  }
+  if ((tid & 63) == 0 && best) atomicMax(&s_key, best);
+  __syncthreads();
+  if (tid == 0 && s_key)
+    atomicMax(&a.keys[((uint64_t)f * a.N + r) * a.n_slots + slot], s_key);
+}
+
 MIMO_DEV uint32_t key_index(unsigned long long k) {
   return k ? (0xFFFFFFFFu - (uint32_t)(k & 0xFFFFFFFFull)) : 0u;
 }
@@ -176,9 +247,11 @@ __global__ __launch_bounds__(T) void ls_kernel(LsArgs a) {
   }
 }
 
+// one thread per (frame, subcarrier, rx-tx pair): the code groups in fixed order, G, and this
+// block's share of the residual variance (nv_part[f][rt][block], summed in order by weights)
 __global__ __launch_bounds__(256) void ls_combine_kernel(LsArgs a) {
   __shared__ double red[4];
-  const uint32_t f = blockIdx.y;
+  const uint32_t rt = blockIdx.y, f = blockIdx.z;
   const FrameInfo &I = a.info[f];
   if (I.status != 0) return;
   const uint32_t M = a.M, N = a.N, P = a.n_groups;
@@ -186,28 +259,27 @@ __global__ __launch_bounds__(256) void ls_combine_kernel(LsArgs a) {
   double nv = 0.0;
   if (k < M) {
     const bool occ = a.occ_index[k] >= 0;
-    for (uint32_t rt = 0; rt < N * N; rt++) {
-      const double *pp = a.part + ((uint64_t)f * N * N + rt) * P * 3 * M;
-      double sr = 0.0, si = 0.0, s2 = 0.0;
-      for (uint32_t g = 0; g < P; g++) {
-        sr += pp[(uint64_t)g * 3 * M + k];
-        si += pp[(uint64_t)g * 3 * M + M + k];
-        s2 += pp[(uint64_t)g * 3 * M + 2 * M + k];
-      }
-      const uint32_t r = rt / N, t = rt % N;
-      const double bias = (a.keep_bias && r == t) ? 1.0 : 0.0;
-      a.G[(((uint64_t)f * M + k) * N + r) * N + t] =
-          occ ? make_float2((float)((bias + sr) * a.scale), (float)(si * a.scale))
-              : make_float2(0.0f, 0.0f);
-      if (occ) nv += s2 - (sr * sr + si * si) / (double)a.nac;
+    const double *pp = a.part + ((uint64_t)f * N * N + rt) * P * 3 * M;
+    double sr = 0.0, si = 0.0, s2 = 0.0;
+    for (uint32_t g = 0; g < P; g++) {
+      sr += pp[(uint64_t)g * 3 * M + k];
+      si += pp[(uint64_t)g * 3 * M + M + k];
+      s2 += pp[(uint64_t)g * 3 * M + 2 * M + k];
     }
+    const uint32_t r = rt / N, t = rt % N;
+    const double bias = (a.keep_bias && r == t) ? 1.0 : 0.0;
+    a.G[(((uint64_t)f * M + k) * N + r) * N + t] =
+        occ ? make_float2((float)((bias + sr) * a.scale), (float)(si * a.scale))
+            : make_float2(0.0f, 0.0f);
+    if (occ) nv = s2 - (sr * sr + si * si) / (double)a.nac;
   }
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) nv += __shfl_xor(nv, off);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = nv;
   __syncthreads();
   if (threadIdx.x == 0)
-    a.nv_part[(uint64_t)f * a.n_nvp + blockIdx.x] = red[0] + red[1] + red[2] + red[3];
+    a.nv_part[(uint64_t)f * a.n_nvp + (uint64_t)rt * gridDim.x + blockIdx.x] =
+        red[0] + red[1] + red[2] + red[3];
 }
 
 // ------------------------------------------------------------------------------------
@@ -273,9 +345,19 @@ __global__ __launch_bounds__(256) void weights_kernel(WeightArgs a) {
   // noise variance (same double expression as the oracle) and replay bookkeeping
   double s2 = (double)a.noise_var;
   if (a.noise_var < 0.0f) {
-    double acc = 0.0;
-    for (uint32_t e = 0; e < a.n_nvp; e++) acc += a.nv_part[(uint64_t)f * a.n_nvp + e];
-    s2 = (double)(float)(acc * a.nv_norm);
+    // the residual-variance partials, summed by wave 0 in a fixed order (lane-strided, then a
+    // fixed shuffle tree) and broadcast through LDS
+    __shared__ double s_acc;
+    if (threadIdx.x < 64) {
+      double acc = 0.0;
+      for (uint32_t e = threadIdx.x; e < a.n_nvp; e += 64)
+        acc += a.nv_part[(uint64_t)f * a.n_nvp + e];
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off);
+      if (threadIdx.x == 0) s_acc = acc;
+    }
+    __syncthreads();
+    s2 = (double)(float)(s_acc * a.nv_norm);
   }
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     I.noise_var = (float)s2;
@@ -386,10 +468,16 @@ static void search_dispatch(const SearchArgs &a, int log2F, uint32_t nf, hipStre
   if constexpr (LOG2F <= 13) {
     if (log2F == LOG2F) {
       const size_t shm = sizeof(float2) * lds_padded_len(1 << LOG2F);
-      (void)hipFuncSetAttribute((const void *)search_kernel<LOG2F>,
-                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
       dim3 grid(a.n_slots * a.N * a.n_lagc, nf);
-      hipLaunchKernelGGL(search_kernel<LOG2F>, grid, dim3(kEstT), shm, s, a);
+      if constexpr (LOG2F >= 10) {
+        (void)hipFuncSetAttribute((const void *)search_reg_kernel<LOG2F>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
+        hipLaunchKernelGGL(search_reg_kernel<LOG2F>, grid, dim3((1 << LOG2F) / 16), shm, s, a);
+      } else {
+        (void)hipFuncSetAttribute((const void *)search_kernel<LOG2F>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
+        hipLaunchKernelGGL(search_kernel<LOG2F>, grid, dim3(kEstT), shm, s, a);
+      }
       return;
     }
     search_dispatch<LOG2F + 1>(a, log2F, nf, s);
@@ -412,7 +500,8 @@ static void ls_dispatch(const LsArgs &a, int log2M, uint32_t nf, hipStream_t s) 
                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
       hipLaunchKernelGGL((ls_kernel<LOG2M, T, CB>), dim3(a.N * a.N * a.n_groups, nf), dim3(T),
                          shm, s, a);
-      hipLaunchKernelGGL(ls_combine_kernel, dim3((a.M + 255) / 256, nf), dim3(256), 0, s, a);
+      hipLaunchKernelGGL(ls_combine_kernel, dim3((a.M + 255) / 256, a.N * a.N, nf), dim3(256),
+                         0, s, a);
       return;
     }
     ls_dispatch<LOG2M + 1>(a, log2M, nf, s);

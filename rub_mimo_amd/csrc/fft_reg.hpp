@@ -1,0 +1,141 @@
+// rub_mimo_amd/csrc/fft_reg.hpp -- register-resident Stockham FFT for one workgroup (gfx950).
+//
+// One N-point transform, T threads, PTS = N/T points per thread held in registers. Every pass
+// is radix 8 except one radix-2/-4 pass (log2 N not a multiple of 3), placed third so that the
+// first and the last pass are radix 8 and the twiddles of the forward and the inverse plan are
+// the same per-thread values (conjugated). In a pass of radix R the thread runs PTS/R
+// butterflies j = tid + i*T; butterfly j reads elements j + r*N/R and writes Stockham order.
+// Between passes the thread's values go through one padded LDS image (two barriers). The
+// first pass may read straight from global memory and the last pass leaves elements
+// j + r*N/8 in the thread, which is exactly what the first pass of the next transform (of the
+// same plan) reads: a forward transform, a pointwise product and an inverse transform chain
+// in registers with no exchange between them (search_kernel).
+#pragma once
+
+#include "fft.hpp"
+
+namespace mimo {
+
+template <int LOG2N, int PTS>
+struct RegPlan {
+  static constexpr int N = 1 << LOG2N;
+  static constexpr int T = N / PTS;
+  static constexpr int P8 = LOG2N / 3;
+  static constexpr int TAIL = LOG2N % 3;
+  static constexpr int NP = P8 + (TAIL ? 1 : 0);
+  static constexpr int TPOS = P8 < 2 ? P8 : 2;          // index of the radix-2/-4 pass
+  static constexpr int radix(int p) { return (TAIL && p == TPOS) ? (1 << TAIL) : 8; }
+  static constexpr int ns(int p) {
+    int n = 1;
+    for (int q = 0; q < p; q++) n *= radix(q);
+    return n;
+  }
+  static constexpr int bt(int p) { return PTS / radix(p); }   // butterflies per thread
+  // distinct base twiddles per thread in pass p: k = (tid + i*T) mod ns(p)
+  static constexpr int ntw(int p) {
+    if (p == 0) return 0;
+    const int n = ns(p);
+    return (T % n == 0) ? 1 : bt(p);
+  }
+  static constexpr int tw_off(int p) {
+    int o = 0;
+    for (int q = 0; q < p; q++) o += ntw(q);
+    return o;
+  }
+  static constexpr int NTW = tw_off(NP);
+};
+
+// this thread's base twiddles e^{-2 pi i k / (NS R)} of every pass, from the kTwN table
+template <int LOG2N, int PTS>
+MIMO_DEV void reg_twiddles(v2f *w1, const float2 *__restrict__ tw, int tid) {
+  using PL = RegPlan<LOG2N, PTS>;
+#pragma unroll
+  for (int p = 1; p < PL::NP; p++) {
+    const int R = PL::radix(p), NS = PL::ns(p);
+#pragma unroll
+    for (int i = 0; i < PL::ntw(p); i++) {
+      const int j = tid + i * PL::T;
+      w1[PL::tw_off(p) + i] = twiddle<false>(tw, (j % NS) * (kTwN / (NS * R)));
+    }
+  }
+}
+
+template <int LOG2N, int PTS, int P>
+MIMO_DEV void reg_store(v2f *buf, const v2f *v, int tid) {
+  using PL = RegPlan<LOG2N, PTS>;
+  constexpr int R = PL::radix(P), NS = PL::ns(P);
+#pragma unroll
+  for (int i = 0; i < PL::bt(P); i++) {
+    const int j = tid + i * PL::T;
+    const int o = (j / NS) * NS * R + (j % NS);
+#pragma unroll
+    for (int r = 0; r < R; r++) buf[lds_pad(o + r * NS)] = v[i * R + r];
+  }
+}
+
+// twiddle and radix-R DFT of the values already in v (pass P)
+template <int LOG2N, int PTS, int P, bool INV>
+MIMO_DEV void reg_compute(v2f *v, const v2f *w1) {
+  using PL = RegPlan<LOG2N, PTS>;
+  constexpr int R = PL::radix(P);
+#pragma unroll
+  for (int i = 0; i < PL::bt(P); i++) {
+    if constexpr (P > 0) {
+      v2f w[R];
+      const v2f b = w1[PL::tw_off(P) + (PL::ntw(P) == 1 ? 0 : i)];
+      w[1] = INV ? v2f{b.x, -b.y} : b;
+      if constexpr (R >= 4) {
+        w[2] = vmul(w[1], w[1]);
+        w[3] = vmul(w[2], w[1]);
+      }
+      if constexpr (R == 8) {
+        w[4] = vmul(w[2], w[2]);
+        w[5] = vmul(w[4], w[1]);
+        w[6] = vmul(w[3], w[3]);
+        w[7] = vmul(w[4], w[3]);
+      }
+#pragma unroll
+      for (int r = 1; r < R; r++) v[i * R + r] = vmul(v[i * R + r], w[r]);
+    }
+    dft_small<R, INV>(v + i * R);
+  }
+}
+
+template <int LOG2N, int PTS, int P>
+MIMO_DEV void reg_load(const v2f *buf, v2f *v, int tid) {
+  using PL = RegPlan<LOG2N, PTS>;
+  constexpr int R = PL::radix(P), NB = PL::N / R;
+#pragma unroll
+  for (int i = 0; i < PL::bt(P); i++) {
+    const int j = tid + i * PL::T;
+#pragma unroll
+    for (int r = 0; r < R; r++) v[i * R + r] = buf[lds_pad(j + r * NB)];
+  }
+}
+
+// passes P .. NP-1 of a transform whose pass P-1 outputs are in v
+template <int LOG2N, int PTS, int P, bool INV>
+MIMO_DEV void reg_rest(v2f *buf, v2f *v, const v2f *w1, int tid) {
+  using PL = RegPlan<LOG2N, PTS>;
+  if constexpr (P < PL::NP) {
+    // an opaque copy of the thread index per pass: the LDS addresses are recomputed here
+    // instead of being hoisted to the kernel start and held (spilled) across passes
+    int t = tid;
+    asm volatile("" : "+v"(t));
+    __syncthreads();
+    reg_store<LOG2N, PTS, P - 1>(buf, v, t);
+    __syncthreads();
+    reg_load<LOG2N, PTS, P>(buf, v, t);
+    reg_compute<LOG2N, PTS, P, INV>(v, w1);
+    reg_rest<LOG2N, PTS, P + 1, INV>(buf, v, w1, tid);
+  }
+}
+
+// element index held in v[s] after the last pass (and read by pass 0): j + r*N/8
+template <int LOG2N, int PTS>
+MIMO_DEV int reg_index(int tid, int s) {
+  using PL = RegPlan<LOG2N, PTS>;
+  return tid + (s / 8) * PL::T + (s % 8) * (PL::N / 8);
+}
+
+}  // namespace mimo

@@ -165,7 +165,10 @@ struct EvmArgs {
   const FrameInfo *info;
   const double *evm_part;
   double *evm_out;                 // [F][N][3]
+  double *chunk_part;              // [F][kEvmChunks][N][3]
+  uint32_t *counter;               // [F] chunks done, zero between launches (self-resetting)
 };
+constexpr uint32_t kEvmChunks = 16;
 void launch_evm(const EvmArgs &a, uint32_t n_frames, hipStream_t s);
 
 // code tables: S0/S1 -> IFFT*dn (framing.cc:1054-1111, 1214-1262) -> zero-pad FFT_F
