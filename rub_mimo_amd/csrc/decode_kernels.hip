@@ -512,7 +512,7 @@ MIMO_DEV uint32_t qam_slice(float2 y, const Qam &q, float2 &pt) {
   return (gray_enc((uint32_t)fI) << q.b) | gray_enc((uint32_t)fQ);
 }
 
-template <int LOG2M, int NA, bool SISO>
+template <int LOG2M, int NA, bool SISO, int EX = 0>
 __global__ __launch_bounds__(1 << (LOG2M - 2))
 __attribute__((amdgpu_waves_per_eu(4)))
 void decode_reg_kernel(DecodeArgs a) {
@@ -526,7 +526,7 @@ void decode_reg_kernel(DecodeArgs a) {
   const FrameInfo &I = a.info[f];
   const uint32_t n_out = (I.status == 0) ? min(I.n_sym, a.max_out) : 0u;
   if (s >= n_out) return;                  // uniform per workgroup
-  const int64_t abs0 = I.base + (int64_t)I.i0 + (int64_t)s * a.SL + a.cp;
+  const int64_t abs0 = I.base + (int64_t)I.i0 + (int64_t)((EX & 1) ? 0 : s) * a.SL + a.cp;
   const bool inb = abs0 >= 0 && abs0 + M <= (int64_t)a.frame_len;
 
   // per-thread base twiddles of passes 1..NP-1: e^{-2 pi i k/(NS R)}, k = j mod NS
@@ -555,7 +555,7 @@ void decode_reg_kernel(DecodeArgs a) {
       }
       dft_small<8, false>(v);
     }
-    reg_passes<LOG2M, 1>(lds, v, w1, tid);
+    if constexpr (!(EX & 32)) reg_passes<LOG2M, 1>(lds, v, w1, tid);
 #pragma unroll
     for (int q = 0; q < 4; q++) {
       X[g0][q] = v[q] * a.dn;              // (:561) x dft_normalizer
@@ -619,7 +619,8 @@ void decode_reg_kernel(DecodeArgs a) {
         for (int tb = 0; tb < TB; tb++)
 #pragma unroll
           for (int r = 0; r < NA; r++)
-            w[tb][r] = reinterpret_cast<const v2f *>(Wf + ((uint64_t)(t0 + tb) * NA + r) * M)[k];
+            if constexpr (EX & 64) w[tb][r] = v2f{gn[q] * (float)(tb + 1), (float)r * 1e-3f};
+            else w[tb][r] = reinterpret_cast<const v2f *>(Wf + ((uint64_t)(t0 + tb) * NA + r) * M)[(EX & 4) ? 0 : (EX & 8) ? (k & 255) : k];
 #pragma unroll
         for (int tb = 0; tb < TB; tb++) {
           const int t = t0 + tb;
@@ -639,7 +640,8 @@ void decode_reg_kernel(DecodeArgs a) {
       if (jq[q] < 0) continue;
       const float2 ye = make_float2(y[t].x, y[t].y);
       float2 sp;
-      const uint32_t d = qam_slice(ye, a.qam, sp);
+      uint32_t d;
+      if constexpr (EX & 16) { sp = ye; d = 0; } else d = qam_slice(ye, a.qam, sp);
       dpk[t] |= d << (8 * q);
       uint32_t refi = refq[t];
       if (a.ref_mode == 0) refi = d;
@@ -662,6 +664,7 @@ void decode_reg_kernel(DecodeArgs a) {
 #pragma unroll
     for (int q = 0; q < 4; q++) {
       if (jq[q] < 0) continue;
+      if ((EX & 2) && X[t][q].x != 12345.0f) continue;
       if (a.out_sym) a.out_sym[ob + jq[q]] = make_float2(X[t][q].x, X[t][q].y);
       if (a.out_idx) a.out_idx[ob + jq[q]] = (uint8_t)(dpk[t] >> (8 * q));
     }
@@ -699,7 +702,8 @@ __global__ __launch_bounds__(256) void evm_kernel(EvmArgs a) {
   const FrameInfo &I = a.info[f];
   const uint32_t n_out = (I.status == 0) ? min(I.n_sym, a.max_out) : 0u;
   const uint32_t per = a.N * 3, G = 256 / per;
-  const uint64_t n = (uint64_t)n_out * a.parts;    // (symbol, part) entries, fixed order
+  const uint64_t recs = (n_out == 0) ? 0u : (a.nrec ? (uint64_t)a.nrec[f] : (uint64_t)n_out);
+  const uint64_t n = recs * a.parts;                // (record, part) entries, fixed order
   const uint64_t lo = n * ch / kEvmChunks, hi = n * (ch + 1) / kEvmChunks;
   const uint32_t g = tid / per, c = tid % per;
   const double *src = a.evm_part + (uint64_t)f * a.max_out * a.parts * per;
@@ -749,6 +753,25 @@ static uint32_t decode_launch_na(const DecodeArgs &a, uint32_t nf, hipStream_t s
     const size_t shm = sizeof(float2) * lds_padded_len(M) * 2;
     auto kern = (a.detector == 3) ? decode_reg_kernel<LOG2M, NA, true>
                                   : decode_reg_kernel<LOG2M, NA, false>;
+    if constexpr (LOG2M == 11 && NA == 4) {   // diagnostics: RMIMO_DEC_EXPT variants
+      switch (a.expt) {
+        case 1: kern = decode_reg_kernel<LOG2M, NA, false, 1>; break;
+        case 2: kern = decode_reg_kernel<LOG2M, NA, false, 2>; break;
+        case 3: kern = decode_reg_kernel<LOG2M, NA, false, 3>; break;
+        case 4: kern = decode_reg_kernel<LOG2M, NA, false, 4>; break;
+        case 7: kern = decode_reg_kernel<LOG2M, NA, false, 7>; break;
+        case 8: kern = decode_reg_kernel<LOG2M, NA, false, 8>; break;
+        case 16: kern = decode_reg_kernel<LOG2M, NA, false, 16>; break;
+        case 32: kern = decode_reg_kernel<LOG2M, NA, false, 32>; break;
+        case 11: kern = decode_reg_kernel<LOG2M, NA, false, 11>; break;
+        case 27: kern = decode_reg_kernel<LOG2M, NA, false, 27>; break;
+        case 64: kern = decode_reg_kernel<LOG2M, NA, false, 64>; break;
+        case 67: kern = decode_reg_kernel<LOG2M, NA, false, 67>; break;
+        case 115: kern = decode_reg_kernel<LOG2M, NA, false, 115>; break;
+        case 59: kern = decode_reg_kernel<LOG2M, NA, false, 59>; break;
+        default: break;
+      }
+    }
     (void)hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)shm);
     hipLaunchKernelGGL(kern, dim3(a.max_out, nf), dim3(M / 4), shm, s, a);
@@ -803,7 +826,16 @@ static uint32_t decode_dispatch(const DecodeArgs &a, int log2M, uint32_t nf, hip
   return 0;
 }
 
-uint32_t launch_decode(const DecodeArgs &a, int log2M, uint32_t n_frames, hipStream_t s) {
+uint32_t launch_decode(const DecodeArgs &a, int log2M, uint32_t n_frames, hipStream_t s,
+                       bool *per_frame_records) {
+  *per_frame_records = false;
+  if (a.expt == 0) {
+    const uint32_t parts = launch_decode_stream(a, log2M, n_frames, s);
+    if (parts) {
+      *per_frame_records = true;
+      return parts;
+    }
+  }
   return decode_dispatch<6>(a, log2M, n_frames, s);
 }
 

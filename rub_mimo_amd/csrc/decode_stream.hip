@@ -1,0 +1,528 @@
+// rub_mimo_amd/csrc/decode_stream.hip -- streaming replay decode for gfx950: one persistent
+// 1024-thread workgroup per CU walks a contiguous range of the batch's decodable symbols.
+//
+// Reference: the replay loop of estimate_channel (framing.cc:853-868) calls
+// execute_mimo_decode (framing.cc:535-589) once per OFDM symbol: drop the CP, FFT each rx
+// antenna, x dft_normalizer, x_t = sum_r W[k][t][r] X_r[k], x normalize_gain[k]; main.cc then
+// demaps and counts symbol errors (main.cc:1394-1411).
+//
+// Why this shape (measured on MI355X at C3, 4x4, M = 2048): the one-workgroup-per-symbol
+// kernel (decode_kernels.hip) spends most of its time on per-symbol dependency chains --
+// FrameInfo -> IQ loads -> FFT -> 64 weight loads from L2 -> apply -> stores -- with only two
+// workgroups per CU to overlap them; with HBM traffic removed it still took 80% of its time.
+// Here every chain is broken:
+//   * the next symbol's samples and EVM reference indices stream into an LDS staging area by
+//     LDS-DMA (global_load_lds_dwordx4, no registers, no VGPR writeback) while the current
+//     symbol is transformed; the kernel waits for them with an explicit vmcnt at the top of
+//     the next symbol (the DMA is inline asm, invisible to the compiler's waits, which would
+//     otherwise drain it at the first barrier);
+//   * each thread owns S = 8/N subcarriers k = tid + q T and keeps W[t][r][k] * gain[k] * dn for
+//     them in registers for all symbols of a frame (64 VGPRs at 4x4): the weights are read
+//     once per workgroup and frame instead of once per symbol (4x the IQ bytes at 4x4);
+//   * complex arithmetic is issued as single VOP3P instructions (cmul_pk & co., fft.hpp) and
+//     the twiddles of every pass come from an LDS table.
+// The FFT runs on all N antennas at once, 8 points per thread per pass (radix 8, one radix
+// 2/4 pass, radix-4 last pass), exchanging through one padded LDS image per antenna; a final
+// exchange leaves the spectra in natural order so the thread reads its S subcarriers of every
+// antenna. Symbol and index stores are coalesced across the wave (512 B / 64 B per
+// instruction); symbol errors are counted per wave with a ballot (SGPRs).
+//
+// EVM/symbol-error sums are kept per thread in fp32 across the symbols of a frame segment and
+// written per wave as fp64 at segment ends into evm_part[f][j][wave] (j = the workgroup's
+// rank among those covering frame f; nrec[f] of them), so evm_kernel's fixed-order reduction
+// stays bitwise reproducible (the item partition is a pure function of the batch).
+#include <algorithm>
+#include <cstdlib>
+
+#include "fft.hpp"
+#include "kernels.hpp"
+
+namespace mimo {
+
+constexpr uint32_t kStreamMaxFrames = 256;
+constexpr uint32_t kStreamMaxQam = 256;          // constellation points (256-QAM)
+
+template <int LOG2M, int NA>
+struct StreamPlan {
+  static constexpr int M = 1 << LOG2M;
+  static constexpr int T = NA * M / 8;                 // 8 points per thread in every pass
+  static constexpr int S = 8 / NA;                     // subcarriers per thread in the apply
+  static constexpr int P8 = (LOG2M - 2) / 3;           // radix-8 passes (pass 0 included)
+  static constexpr int TAIL = (LOG2M - 2) % 3;         // then one radix-2/-4 pass if nonzero
+  static constexpr int NP = P8 + (TAIL ? 1 : 0) + 1;   // ... and a final radix-4 pass
+  static constexpr int PB = lds_padded_len(M);
+  static constexpr int radix(int p) { return p < P8 ? 8 : (p == NP - 1 ? 4 : (1 << TAIL)); }
+  static constexpr int ns(int p) {
+    int n = 1;
+    for (int q = 0; q < p; q++) n *= radix(q);
+    return n;
+  }
+  static constexpr int bt(int p) { return 8 / radix(p); }          // butterflies per thread
+  static constexpr int ntw(int p) { return (T % ns(p) == 0) ? 1 : bt(p); }
+};
+
+// butterfly i of the thread in pass P: antenna g and index j within the antenna
+template <int LOG2M, int NA, int P>
+MIMO_DEV void st_bfly(int tid, int i, int &g, int &j) {
+  using PL = StreamPlan<LOG2M, NA>;
+  constexpr int NB = PL::M / PL::radix(P);
+  const int u = tid + i * PL::T;
+  g = u / NB;
+  j = u % NB;
+}
+
+template <int LOG2M, int NA, int P>
+MIMO_DEV void st_store(v2f *buf, const v2f *v, int tid) {
+  using PL = StreamPlan<LOG2M, NA>;
+  constexpr int R = PL::radix(P), NS = PL::ns(P);
+#pragma unroll
+  for (int i = 0; i < PL::bt(P); i++) {
+    int g, j;
+    st_bfly<LOG2M, NA, P>(tid, i, g, j);
+    const int o = (j / NS) * NS * R + (j % NS);
+#pragma unroll
+    for (int r = 0; r < R; r++) buf[g * PL::PB + lds_pad(o + r * NS)] = v[i * R + r];
+  }
+}
+
+// pass P with the twiddles from the LDS table (twl: passes 1.. in order, [(r-1) NS + jm])
+template <int LOG2M, int NA, int P>
+MIMO_DEV void st_load_t(const v2f *buf, v2f *v, const v2f *twl, int tid) {
+  using PL = StreamPlan<LOG2M, NA>;
+  constexpr int R = PL::radix(P), NB = PL::M / R, NS = PL::ns(P);
+  constexpr int OFF = [] {
+    int o = 0;
+    for (int q = 1; q < P; q++) o += (PL::radix(q) - 1) * PL::ns(q);
+    return o;
+  }();
+#pragma unroll
+  for (int i = 0; i < PL::bt(P); i++) {
+    int g, j;
+    st_bfly<LOG2M, NA, P>(tid, i, g, j);
+#pragma unroll
+    for (int r = 0; r < R; r++) v[i * R + r] = buf[g * PL::PB + lds_pad(j + r * NB)];
+    const v2f *tw = twl + OFF + (j % NS);
+#pragma unroll
+    for (int r = 1; r < R; r++) v[i * R + r] = cmul_pk(v[i * R + r], tw[(r - 1) * NS]);
+    dft_fwd_pk<R>(v + i * R);
+  }
+}
+
+// passes P .. NP-1; the outputs of pass P-1 are already stored in the image
+template <int LOG2M, int NA, int P>
+MIMO_DEV void st_passes2(v2f *img, v2f *v, const v2f *twl, int tid) {
+  using PL = StreamPlan<LOG2M, NA>;
+  if constexpr (P < PL::NP) {
+    int t = tid;                            // opaque per pass: addresses are not hoisted
+    asm volatile("" : "+v"(t));
+    __syncthreads();                        // the image is complete
+    st_load_t<LOG2M, NA, P>(img, v, twl, t);
+    if constexpr (P + 1 < PL::NP) {
+      __syncthreads();                      // readers of the image are done
+      st_store<LOG2M, NA, P>(img, v, t);
+      st_passes2<LOG2M, NA, P + 1>(img, v, twl, tid);
+    }
+  }
+}
+
+MIMO_DEV uint32_t cvt_u32_sat(float x) {   // v_cvt_u32_f32: NaN and negatives -> 0, saturating
+  uint32_t r;
+  asm("v_cvt_u32_f32 %0, %1" : "=v"(r) : "v"(x));
+  return r;
+}
+
+// hard decision as qam_slice (decode_kernels.hip) / qam_demap (common.hpp): the level is
+// floor((y * inv_scale + L) * 0.5) clamped to [0, L-1] (NaN -> 0); truncation of the
+// non-negative value by v_cvt_u32_f32 with its saturation gives exactly that clamp
+MIMO_DEV uint32_t qam_slice_pk(v2f y, v2f inv_scale, v2f Lf, uint32_t Lm1, uint32_t b) {
+#pragma clang fp contract(off)
+  const v2f t = (y * inv_scale + Lf) * 0.5f;
+  const uint32_t mI = min(cvt_u32_sat(t.x), Lm1), mQ = min(cvt_u32_sat(t.y), Lm1);
+  return (gray_enc(mI) << b) | gray_enc(mQ);
+}
+
+// LDS-DMA of 16 bytes per lane (global_load_lds_dwordx4: lane l writes lds + 16 l), issued as
+// inline asm so that the compiler does not tie it to its own vmcnt waits (it waits for every
+// LDS DMA at the next barrier); the kernel waits for it explicitly (s_waitcnt vmcnt) at the
+// point of use. M0 is saved and restored around it.
+MIMO_DEV void dma16(uint32_t voff, __attribute__((address_space(1))) const void *sbase, uint32_t lds) {
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t"
+               "global_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(voff), "s"(sbase), "s"(lds) : "memory");
+}
+
+// an opaque copy: values derived from it inside the symbol loop are recomputed where they are
+// used instead of being hoisted out of the loop and held (or spilled) across it
+MIMO_DEV int opq(int x) {
+  asm volatile("" : "+v"(x));
+  return x;
+}
+MIMO_DEV uint32_t opq_s(uint32_t x) {
+  asm volatile("" : "+s"(x));
+  return x;
+}
+
+// a wave-uniform global pointer held in SGPRs (address arithmetic feeding it may sit in
+// VGPRs); global address space, so accesses through it are global_* with an SGPR base and a
+// 32-bit lane offset, not flat_* (flat stores also count on lgkmcnt: every LDS wait would
+// drain them)
+template <typename P>
+using gptr = __attribute__((address_space(1))) P *;
+template <typename P>
+MIMO_DEV gptr<P> sgpr_ptr(P *p) {
+  const uint64_t v = (uint64_t)p;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+  return (gptr<P>)(((uint64_t)hi << 32) | lo);
+}
+
+template <int LOG2M, int NA, int REF, int OUTS>
+__global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(DecodeArgs a) {
+  using PL = StreamPlan<LOG2M, NA>;
+  constexpr int M = PL::M, T = PL::T, S = PL::S, PB = PL::PB, W8 = M / 8;
+  constexpr int RS = M + 2;                       // staging row: M + 2 samples from an even start
+  constexpr int NCH = NA * (RS / 2);              // 16-byte chunks of one symbol's staging
+  constexpr int NDMA = (NCH + T - 1) / T;         // DMA instructions per thread
+  constexpr int NREF = NA * M / 16;               // 16-byte chunks of the reference indices
+  // store instructions per symbol: the wait at the top of a symbol leaves them in flight
+  constexpr int NSTORE = ((OUTS & 1) ? NA * S : 0) + ((OUTS & 2) ? NA * S : 0);
+  extern __shared__ __attribute__((aligned(16))) float2 lds_raw[];
+  v2f *img = reinterpret_cast<v2f *>(lds_raw);                     // [NA][PB] FFT exchange
+  v2f *stg = img + NA * PB;                                        // [NA][RS] next symbol
+  uint8_t *rstg = reinterpret_cast<uint8_t *>(stg + NA * RS);      // [NA][M] next references
+  v2f *twl = reinterpret_cast<v2f *>(rstg + ((REF == 1) ? NA * M : 0));   // twiddle table
+  __shared__ uint32_t pfx[kStreamMaxFrames + 1];
+  __shared__ int64_t fbody[kStreamMaxFrames];
+  __shared__ v2f ptab[kStreamMaxQam];                              // constellation by index
+  const int tid = threadIdx.x;
+  const uint32_t wv = __builtin_amdgcn_readfirstlane((uint32_t)tid >> 6);
+  for (uint32_t e = tid; e < a.qam.L * a.qam.L; e += T) {
+    const float2 p = qam_point(e, a.qam);
+    ptab[e] = v2f{p.x, p.y};
+  }
+
+  // twiddles of passes 1..NP-1: twl[off(p) + (r-1) NS + jm] = e^{-2 pi i jm r / (NS R)}
+  {
+    int off = 0;
+#pragma unroll
+    for (int p = 1; p < PL::NP; p++) {
+      const int R = PL::radix(p), NS = PL::ns(p);
+      for (int e = tid; e < (R - 1) * NS; e += T) {
+        const int r = e / NS + 1, jm = e % NS;
+        twl[off + e] = twiddle<false>(a.tw, ((jm * r) % (NS * R)) * (kTwN / (NS * R)));
+      }
+      off += (R - 1) * NS;
+    }
+  }
+  // decodable symbols of frames < f (status OK, min(n_sym, max_out) each), and each frame's
+  // first data-symbol body (held in LDS: FrameInfo reads in the loop would be vector loads
+  // whose waits also drain the symbol stores in flight)
+  for (uint32_t f0 = 0; f0 <= a.n_frames; f0 += T) {
+    const uint32_t f = f0 + tid;
+    uint32_t v = 0;
+    if (f < a.n_frames) {
+      const FrameInfo &I = a.info[f];
+      v = (I.status == 0) ? min(I.n_sym, a.max_out) : 0u;
+      fbody[f] = I.base + (int64_t)I.i0 + (int64_t)a.cp;
+    }
+    if (f <= a.n_frames) pfx[f] = v;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    uint32_t acc = 0;
+    for (uint32_t f = 0; f <= a.n_frames; f++) {
+      const uint32_t v = pfx[f];
+      pfx[f] = acc;
+      acc += v;
+    }
+  }
+  __syncthreads();
+  const uint32_t total = pfx[a.n_frames];
+  const uint32_t chunk = (total + gridDim.x - 1) / gridDim.x;
+  const uint32_t i_begin = blockIdx.x * chunk;
+  const uint32_t i_end = min(i_begin + chunk, total);
+  if (i_begin >= i_end) return;                       // uniform
+
+  uint32_t f = 0;                                     // largest f with pfx[f] <= i_begin
+  {
+    uint32_t lo = 0, hi = a.n_frames;
+    while (hi - lo > 1) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (pfx[mid] <= i_begin) lo = mid; else hi = mid;
+    }
+    f = lo;
+  }
+  f = __builtin_amdgcn_readfirstlane(f);
+  uint32_t s = __builtin_amdgcn_readfirstlane(i_begin - pfx[f]);
+  uint32_t n_out_f = __builtin_amdgcn_readfirstlane(pfx[f + 1] - pfx[f]);
+
+  const v2f inv_sc = v2f{a.qam.inv_scale, a.qam.inv_scale};
+  const v2f Lf = v2f{(float)a.qam.L, (float)a.qam.L};
+  const uint32_t Lm1 = a.qam.L - 1;
+  const uint32_t stg_base = (uint32_t)(uintptr_t)stg;
+  const uint32_t rstg_base = (uint32_t)(uintptr_t)rstg;
+
+  // staging of symbol (ff, ss): rows of M + 2 samples from the even sample a0 <= abs0, so
+  // that every lane moves one aligned 16-byte pair; returns the odd offset abs0 - a0
+  auto fetch = [&](uint32_t ff, uint32_t ss) -> int {
+    const int64_t b0 = fbody[ff];
+    const int64_t abs0 = (int64_t)((((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)b0)) |
+                                    ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)((uint64_t)b0 >> 32)) << 32))) +
+                         (int64_t)ss * a.SL;
+    const int64_t a0 = abs0 & ~(int64_t)1;
+    const float2 *xf = a.iq + (uint64_t)ff * NA * a.stride;
+    const int t0 = opq(tid);
+    if (a0 >= 0 && a0 + RS <= (int64_t)a.frame_len && ((uintptr_t)a.iq & 15u) == 0 &&
+        (a.stride & 1u) == 0) {
+      const auto xa = sgpr_ptr(xf + a0);
+#pragma unroll
+      for (int u = 0; u < NDMA; u++) {
+        const int c = u * T + t0;
+        const uint32_t dst = __builtin_amdgcn_readfirstlane(stg_base + (uint32_t)(u * T + wv * 64) * 16u);
+        if (u < NCH / T || c < NCH) {
+          const uint32_t g = (uint32_t)c / (RS / 2), q = (uint32_t)c % (RS / 2);
+          dma16((g * (uint32_t)a.stride + 2 * q) * 8u, xa, dst);
+        }
+      }
+    } else {                                          // edge of the capture: guarded loads
+      for (int c = t0; c < NA * RS; c += T) {
+        const int g = c / RS, q = c % RS;
+        const int64_t n = a0 + q;
+        stg[c] = (n >= 0 && n < (int64_t)a.frame_len) ? reinterpret_cast<const v2f *>(xf + (uint64_t)g * a.stride)[n]
+                                                      : v2f{0.0f, 0.0f};
+      }
+    }
+    if constexpr (REF == 1) {
+      if (t0 < NREF) {
+        const uint32_t dst = __builtin_amdgcn_readfirstlane(rstg_base + (uint32_t)(wv * 64) * 16u);
+        const uint32_t t = (uint32_t)t0 / (M / 16), q = (uint32_t)t0 % (M / 16);
+        const auto rb = sgpr_ptr(a.ref_idx + ((uint64_t)ff * NA * a.max_out + ss) * a.M_occ);
+        dma16(t * (uint32_t)(a.max_out * a.M_occ) + 16 * q, rb, dst);
+      }
+    }
+    return (int)(abs0 - a0);
+  };
+
+  // this frame's weights * gain * dn for the thread's subcarriers k = tid + q T
+  v2f Wr[NA][NA][S];
+  auto load_w = [&](uint32_t ff) {
+    const int t0 = opq(tid);
+    const v2f *Wf = reinterpret_cast<const v2f *>(a.W) + (uint64_t)ff * NA * NA * M + t0;
+    const float *gf = a.gain + (uint64_t)ff * M + t0;
+    float gs[S];
+#pragma unroll
+    for (int q = 0; q < S; q++) gs[q] = gf[q * T] * a.dn;
+#pragma unroll
+    for (int t = 0; t < NA; t++)
+#pragma unroll
+      for (int r = 0; r < NA; r++)
+#pragma unroll
+        for (int q = 0; q < S; q++) Wr[t][r][q] = Wf[(t * NA + r) * M + q * T] * gs[q];
+  };
+
+  // EVM sums: per-thread fp32 error and reference energies, per-wave symbol-error counts
+  float e_num[NA], e_den[NA];
+  uint32_t n_err[NA];
+#pragma unroll
+  for (int t = 0; t < NA; t++) {
+    e_num[t] = e_den[t] = 0.0f;
+    n_err[t] = 0;
+  }
+  auto flush = [&](uint32_t ff) {      // per-wave EVM partials of this frame segment
+    const int t0 = opq(tid), lane = t0 & 63;
+    const uint32_t ch = opq_s(chunk);
+    const uint32_t jrec = blockIdx.x - pfx[ff] / ch;
+    if (t0 == 0 && pfx[ff] >= i_begin)             // first workgroup of the frame
+      a.nrec[ff] = (pfx[ff + 1] - 1) / ch - pfx[ff] / ch + 1;
+#pragma unroll
+    for (int t = 0; t < NA; t++) {
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) {
+        e_num[t] += __shfl_xor(e_num[t], off);
+        e_den[t] += __shfl_xor(e_den[t], off);
+      }
+    }
+    double *ep = a.evm_part + ((((uint64_t)ff * a.max_out + jrec) * (T / 64) + wv) * NA) * 3;
+    if (lane < NA * 3) {
+      const int t = lane / 3, c = lane % 3;
+      float v = 0.0f;
+#pragma unroll
+      for (int u = 0; u < NA; u++)
+        if (u == t) v = c == 0 ? e_num[u] : (c == 1 ? e_den[u] : (float)n_err[u]);
+      ep[lane] = (double)v;
+    }
+#pragma unroll
+    for (int t = 0; t < NA; t++) {
+      e_num[t] = e_den[t] = 0.0f;
+      n_err[t] = 0;
+    }
+  };
+
+  load_w(f);
+  int odd = fetch(f, s);
+  // the first symbol's staging (issued after the weight loads: the counted wait in the loop
+  // assumes only stores behind the DMA)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();                                    // twiddle table and guarded staging
+  for (uint32_t i = i_begin; i < i_end; i++) {
+    // this symbol's staging has landed (the previous symbol's stores may still be in flight)
+    asm volatile("s_waitcnt vmcnt(%0)" :: "n"(NSTORE) : "memory");
+    __syncthreads();
+    v2f v[8];
+    {
+      const int t0 = opq(tid);
+      const v2f *x = stg + (t0 / W8) * RS + odd + (t0 % W8);
+#pragma unroll
+      for (int r = 0; r < 8; r++) v[r] = x[r * W8];
+    }
+    uint32_t cref[(NA * S + 3) / 4];                  // reference indices, byte (t S + q)
+    if constexpr (REF == 1) {
+      const int t0 = opq(tid);
+#pragma unroll
+      for (int w = 0; w < (NA * S + 3) / 4; w++) cref[w] = 0;
+#pragma unroll
+      for (int t = 0; t < NA; t++)
+#pragma unroll
+        for (int q = 0; q < S; q++) {
+          const int e = t * S + q;
+          cref[e / 4] |= (uint32_t)rstg[t * M + t0 + q * T] << (8 * (e % 4));
+        }
+    }
+    dft_fwd_pk<8>(v);
+    __syncthreads();                                  // staging consumed by every wave
+    // the item after this one (uniform) and its staging, in flight during this symbol
+    uint32_t fn = f, sn = s + 1, n_out_n = n_out_f;
+    int odd_n = 0;
+    if (i + 1 < i_end) {
+      if (sn >= n_out_f) {
+        do { fn++; } while (pfx[fn + 1] == pfx[fn]);
+        sn = 0;
+        n_out_n = pfx[fn + 1] - pfx[fn];
+      }
+      fn = __builtin_amdgcn_readfirstlane(fn);
+      sn = __builtin_amdgcn_readfirstlane(sn);
+      n_out_n = __builtin_amdgcn_readfirstlane(n_out_n);
+      odd_n = fetch(fn, sn);
+    }
+    // passes 1 .. NP-1 through the LDS images (pass 1 needs no leading barrier: the previous
+    // symbol's image readers finished before the barrier at the top), then the exchange that
+    // leaves the spectra in natural order
+    st_store<LOG2M, NA, 0>(img, v, opq(tid));
+    st_passes2<LOG2M, NA, 1>(img, v, twl, tid);
+    {
+      int t = tid;
+      asm volatile("" : "+v"(t));
+      __syncthreads();
+      st_store<LOG2M, NA, PL::NP - 1>(img, v, t);
+      __syncthreads();
+    }
+
+    // apply, demap, EVM, stores: subcarrier k = tid + q T of every stream
+    const uint64_t frame_id = a.frame_id0 + f;
+#pragma unroll
+    for (int q = 0; q < S; q++) {
+      const uint32_t k = (uint32_t)opq(tid) + q * T;
+      v2f X[NA];
+#pragma unroll
+      for (int r = 0; r < NA; r++) X[r] = img[r * PB + lds_pad(k)];
+#pragma unroll
+      for (int t = 0; t < NA; t++) {
+        // uniform row bases (SGPRs): the stores take a 32-bit per-lane offset
+        const uint64_t ob = (((uint64_t)f * NA + t) * a.max_out + s) * a.M_occ;
+        const auto osym = sgpr_ptr(reinterpret_cast<v2f *>(a.out_sym + ob));
+        const auto oidx = sgpr_ptr(a.out_idx + ob);
+        v2f acc = v2f{0.0f, 0.0f};
+#pragma unroll
+        for (int r = 0; r < NA; r++) acc = cmac_pk(acc, Wr[t][r][q], X[r]);
+        const uint32_t d = qam_slice_pk(acc, inv_sc, Lf, Lm1, a.qam.b);
+        uint32_t refi;
+        if constexpr (REF == 1) refi = (cref[(t * S + q) / 4] >> (8 * ((t * S + q) % 4))) & 0xFFu;
+        else if constexpr (REF == 2)
+          refi = (uint32_t)(hash5(a.ref_seed, DOM_DATA, frame_id, t, (uint64_t)s * a.M_occ + k) &
+                            (uint64_t)(a.qam.L * a.qam.L - 1));
+        else refi = d;
+        // the reference point (the transmitted one: a decision error costs its distance)
+        n_err[t] += (uint32_t)__builtin_popcountll(__builtin_amdgcn_ballot_w64(refi != d));
+        const v2f sp = ptab[refi];
+        const v2f er = acc - sp;
+        e_num[t] = __builtin_fmaf(er.x, er.x, __builtin_fmaf(er.y, er.y, e_num[t]));
+        e_den[t] = __builtin_fmaf(sp.x, sp.x, __builtin_fmaf(sp.y, sp.y, e_den[t]));
+        if constexpr (OUTS & 1) osym[k] = acc;
+        if constexpr (OUTS & 2) oidx[k] = (uint8_t)d;
+      }
+    }
+
+    const bool last = (i + 1 == i_end);
+    if (last || fn != f) {
+      flush(f);
+      if (!last) {
+        n_out_f = n_out_n;
+        load_w(fn);
+      }
+    }
+    f = __builtin_amdgcn_readfirstlane(fn);
+    s = __builtin_amdgcn_readfirstlane(sn);
+    odd = __builtin_amdgcn_readfirstlane(odd_n);
+  }
+}
+
+// returns the EVM partial sets per record (waves per workgroup), 0 when the configuration is
+// not handled here (the caller then uses the per-symbol kernels)
+template <int LOG2M, int NA>
+static size_t stream_lds_bytes(int ref_mode) {
+  using PL = StreamPlan<LOG2M, NA>;
+  size_t tw = 0;
+  for (int p = 1; p < PL::NP; p++) tw += (size_t)(PL::radix(p) - 1) * PL::ns(p);
+  return sizeof(float2) * ((size_t)PL::PB * NA + (size_t)(PL::M + 2) * NA + tw) +
+         (ref_mode == 1 ? (size_t)NA * PL::M : 0);
+}
+
+template <int LOG2M, int NA>
+static uint32_t stream_launch(const DecodeArgs &a, hipStream_t s) {
+  using PL = StreamPlan<LOG2M, NA>;
+  const size_t shm = stream_lds_bytes<LOG2M, NA>(a.ref_mode);
+  auto pick_out = [&](auto ref) -> void (*)(DecodeArgs) {
+    constexpr int R = decltype(ref)::value;
+    const int outs = (a.out_sym ? 1 : 0) | (a.out_idx ? 2 : 0);
+    switch (outs) {
+      case 3: return decode_stream_kernel<LOG2M, NA, R, 3>;
+      case 2: return decode_stream_kernel<LOG2M, NA, R, 2>;
+      case 1: return decode_stream_kernel<LOG2M, NA, R, 1>;
+      default: return decode_stream_kernel<LOG2M, NA, R, 0>;
+    }
+  };
+  auto kern = a.ref_mode == 1 ? pick_out(std::integral_constant<int, 1>{})
+            : a.ref_mode == 2 ? pick_out(std::integral_constant<int, 2>{})
+                              : pick_out(std::integral_constant<int, 0>{});
+  if (hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+                          (int)shm) != hipSuccess)
+    return 0;
+  int per_cu = 1;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, PL::T, shm) != hipSuccess ||
+      per_cu < 1)
+    per_cu = 1;
+  const uint32_t grid = a.n_cu * (uint32_t)per_cu;
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(PL::T), shm, s, a);
+  return PL::T / 64;
+}
+
+uint32_t launch_decode_stream(const DecodeArgs &a, int log2M, uint32_t n_frames, hipStream_t s) {
+  static const bool off = [] { const char *e = getenv("RMIMO_DECODE_STREAM"); return e && e[0] == '0'; }();
+  if (off || a.detector == 3 || !a.all_occ || !a.nrec || n_frames > kStreamMaxFrames ||
+      a.qam.L * a.qam.L > kStreamMaxQam)
+    return 0;
+  if (a.ref_mode == 1 && ((uintptr_t)a.ref_idx & 3u)) return 0;
+  if (a.ref_mode == 1 && ((uintptr_t)a.ref_idx & 15u)) return 0;
+  // 32-bit DMA offsets within one frame's antennas and one frame's reference rows
+  if ((uint64_t)a.N * a.stride * sizeof(float2) >= (1ull << 32) ||
+      (uint64_t)a.N * a.max_out * a.M_occ >= (1ull << 32))
+    return 0;
+  if (a.N == 4 && log2M == 11) return stream_launch<11, 4>(a, s);
+  if (a.N == 4 && log2M == 10) return stream_launch<10, 4>(a, s);
+  if (a.N == 2 && log2M == 12) return stream_launch<12, 2>(a, s);
+  if (a.N == 2 && log2M == 11) return stream_launch<11, 2>(a, s);
+  return 0;
+}
+
+}  // namespace mimo

@@ -221,10 +221,13 @@ struct mimo_rx {
   DevBuf<float> gain;
   DevBuf<double> nvp, evm_part, evm_out, lspart, evm_chunk;
   DevBuf<uint32_t> evm_cnt;             // per-frame chunk counters of evm_kernel (self-resetting)
+  DevBuf<uint32_t> nrec;                // per-frame EVM records of the streaming decode
   size_t cap_lspart = 0;
   DevBuf<unsigned long long> n_exact;   // S&C exact fp32 recomputes (diagnostic)
   DevBuf<uint32_t> queue;               // S&C work-queue head, hot-item count
   DevBuf<ScHot> hot;                    // S&C items awaiting exact resolution
+  DevBuf<uint32_t> scr_flag;            // S&C screen: chunk listed [F][nchunks]
+  DevBuf<unsigned long long> scr_min, scr_max;   // first / last unproven position per chunk
   uint32_t cap_hot = 0;
   DevBuf<unsigned long long> sc_prof;   // RMIMO_SC_PROF=1 cycle counters
   uint32_t last_frames = 0, last_max_out = 0;
@@ -278,6 +281,7 @@ int ensure_workspace(mimo_rx *h, uint32_t F, uint64_t chunks, uint64_t evm_entri
     HIPCHK(h->evm_out.ensure((size_t)nf * h->N * 3));
     HIPCHK(h->evm_chunk.ensure((size_t)nf * kEvmChunks * h->N * 3));
     HIPCHK(h->evm_cnt.ensure(nf));
+    HIPCHK(h->nrec.ensure(nf));
     HIPCHK(hipMemset(h->evm_cnt.p, 0, sizeof(uint32_t) * nf));
     h->cap_frames = nf;
     HIPCHK(h->rec.ensure((size_t)nf * h->cap_chunks));
@@ -338,10 +342,27 @@ int run_sync(mimo_rx *h, const float2 *iq, uint64_t stride, uint32_t F, uint64_t
     HIPCHK(hipMemsetAsync(h->queue.p, 0, 2 * sizeof(uint32_t), s));
     a.queue = h->queue.p;
     a.hot_count = h->queue.p + 1;
-    const uint32_t hot_cap = 8 * F + 32;
+    // screened path (default when the geometry allows it; RMIMO_SC_LEGACY=1 selects the
+    // per-chunk item kernel): one hot item per listed chunk
+    static const bool legacy = [] { const char *e = getenv("RMIMO_SC_LEGACY"); return e && e[0] == '1'; }();
+    const bool screen = !legacy && sc_screen_ok(h->M);
+    const uint64_t n_list = (nchunks - chunk_lo) * (uint64_t)F;
+    const uint32_t hot_cap = screen ? (uint32_t)n_list : 8 * F + 32;
     if (hot_cap > h->cap_hot) {
       HIPCHK(h->hot.ensure(hot_cap));
       h->cap_hot = hot_cap;
+    }
+    a.nchunks = nchunks;
+    if (screen) {
+      const size_t nf = (size_t)F * nchunks;
+      HIPCHK(h->scr_flag.ensure(nf));
+      HIPCHK(h->scr_min.ensure(nf));
+      HIPCHK(h->scr_max.ensure(nf));
+      HIPCHK(hipMemsetAsync(h->scr_flag.p, 0, sizeof(uint32_t) * nf, s));
+      HIPCHK(hipMemsetAsync(h->scr_min.p, 0xFF, sizeof(unsigned long long) * nf, s));
+      HIPCHK(hipMemsetAsync(h->scr_max.p, 0, sizeof(unsigned long long) * nf, s));
+      a.fmin = h->scr_min.p;
+      a.fmax = h->scr_max.p;
     }
     a.hot = h->hot.p;
     a.hot_cap = hot_cap;
@@ -353,7 +374,19 @@ int run_sync(mimo_rx *h, const float2 *iq, uint64_t stride, uint32_t F, uint64_t
       a.prof = h->sc_prof.p;
     }
     hipEvent_t e = h->timer.begin(s);
-    launch_sc(a, F, h->n_cu, s);
+    if (screen) {
+      ScreenArgs sa{};
+      sa.iq = iq; sa.stride = stride; sa.frame_len = frame_len;
+      sa.N = h->N; sa.M = h->M;
+      sa.thr_screen = h->thr - 0.01;
+      sa.chunk_len = K; sa.chunk_lo = chunk_lo; sa.nchunks = nchunks;
+      sa.flag = h->scr_flag.p; sa.fmin = h->scr_min.p; sa.fmax = h->scr_max.p;
+      sa.count = a.hot_count; sa.hot = a.hot; sa.cap = a.hot_cap;
+      launch_sc_screen(sa, F, s);
+      launch_sc_exact(a, s);
+    } else {
+      launch_sc(a, F, h->n_cu, s);
+    }
     launch_sc_hot(a, s);
     h->timer.end(0, e, s);
     if (prof_env) {   // diagnostics: per-item cycle split of the S&C kernel
@@ -446,6 +479,8 @@ int run_decode(mimo_rx *h, const float2 *iq, uint64_t stride, uint32_t F, uint64
   // RMIMO_DECODE_GRID=1 forces the one-workgroup-per-symbol grid (A/B against the persistent form)
   static const bool grid_only = [] { const char *e = getenv("RMIMO_DECODE_GRID"); return e && e[0] == '1'; }();
   d.all_occ = (h->M_occ == h->M && !grid_only) ? 1 : 0;
+  static const int expt = [] { const char *e = getenv("RMIMO_DEC_EXPT"); return e ? atoi(e) : 0; }();
+  d.expt = expt;
   static const bool dprof = [] { const char *e = getenv("RMIMO_DEC_PROF"); return e && e[0] == '1'; }();
   if (dprof) {
     if (!h->sc_prof.p) HIPCHK(h->sc_prof.ensure(20));
@@ -453,7 +488,9 @@ int run_decode(mimo_rx *h, const float2 *iq, uint64_t stride, uint32_t F, uint64
     d.prof = h->sc_prof.p;
   }
   hipEvent_t e = h->timer.begin(s);
-  const uint32_t parts = launch_decode(d, h->log2M, F, s);
+  d.nrec = h->nrec.p;
+  bool per_frame = false;
+  const uint32_t parts = launch_decode(d, h->log2M, F, s, &per_frame);
   h->timer.end(5, e, s);
   if (dprof) {   // diagnostics: per-item cycle split of the decode kernel
     unsigned long long v[5];
@@ -469,6 +506,7 @@ int run_decode(mimo_rx *h, const float2 *iq, uint64_t stride, uint32_t F, uint64
   ea.evm_out = h->evm_out.p;
   ea.chunk_part = h->evm_chunk.p;
   ea.counter = h->evm_cnt.p;
+  ea.nrec = per_frame ? h->nrec.p : nullptr;
   e = h->timer.begin(s);
   launch_evm(ea, F, s);
   h->timer.end(6, e, s);

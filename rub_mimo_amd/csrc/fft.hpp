@@ -32,6 +32,70 @@ MIMO_DEV v2f vmulc(v2f a, v2f b) {         // a * conj(b)
   return __builtin_elementwise_fma(b.yy, as, b.xx * a);
 }
 
+// The same operations as single VOP3P instructions with the swizzle and the sign folded into
+// op_sel / neg modifiers (the compiler materialises {-b.y, b.x} with a v_xor and a v_mov
+// first). Results are bitwise those of vmul / rot_mi forms above.
+MIMO_DEV v2f cmul_pk(v2f a, v2f b) {     // a * b: (a.x b.x - a.y b.y, a.x b.y + a.y b.x)
+  v2f t, r;
+  asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[0,1]" : "=v"(t) : "v"(a), "v"(b));
+  asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_lo:[0,1,0]"
+      : "=v"(r) : "v"(a), "v"(b), "v"(t));
+  return r;
+}
+MIMO_DEV v2f cmac_pk(v2f y, v2f w, v2f x) {   // y + w * x, as fma(w.xx, x, y) then fma(w.yy, ix, .)
+  v2f t, r;
+  asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel_hi:[0,1,1]" : "=v"(t) : "v"(w), "v"(x), "v"(y));
+  asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_lo:[0,1,0]"
+      : "=v"(r) : "v"(w), "v"(x), "v"(t));
+  return r;
+}
+MIMO_DEV v2f add_mi(v2f a, v2f b) {      // a + b * (-i) = (a.x + b.y, a.y - b.x)
+  v2f r;
+  asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0] neg_hi:[0,1]" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+MIMO_DEV v2f sub_mi(v2f a, v2f b) {      // a - b * (-i) = (a.x - b.y, a.y + b.x)
+  v2f r;
+  asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0] neg_lo:[0,1]" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+MIMO_DEV v2f rot_m_b(v2f b) {            // b * (-i) - b = (b.y - b.x, -b.x - b.y)
+  v2f r;
+  asm("v_pk_add_f32 %0, %1, %1 op_sel:[1,0] op_sel_hi:[0,1] neg_lo:[0,1] neg_hi:[1,1]" : "=v"(r) : "v"(b));
+  return r;
+}
+
+// forward radix-2/4/8 DFTs on the packed forms (same arithmetic as dft_small<R, false>)
+template <int R>
+MIMO_DEV void dft_fwd_pk(v2f *a) {
+  if constexpr (R == 2) {
+    const v2f t0 = a[0] + a[1], t1 = a[0] - a[1];
+    a[0] = t0; a[1] = t1;
+  } else if constexpr (R == 4) {
+    const v2f b0 = a[0] + a[2], b1 = a[0] - a[2];
+    const v2f b2 = a[1] + a[3], d3 = a[1] - a[3];
+    a[0] = b0 + b2; a[2] = b0 - b2;
+    a[1] = add_mi(b1, d3); a[3] = sub_mi(b1, d3);
+  } else {
+    static_assert(R == 8, "radix");
+    const float c = 0.70710678118654752f;
+    const v2f b0 = a[0] + a[4], b4 = a[0] - a[4];
+    const v2f b1 = a[1] + a[5], b5r = a[1] - a[5];
+    const v2f b2 = a[2] + a[6], b6 = a[2] - a[6];
+    const v2f b3 = a[3] + a[7], b7r = a[3] - a[7];
+    const v2f b5 = c * add_mi(b5r, b5r);                 // * W8^1
+    const v2f b7 = c * rot_m_b(b7r);                     // * W8^3
+    const v2f c0 = b0 + b2, c2 = b0 - b2;
+    const v2f c1 = b1 + b3, d3 = b1 - b3;
+    const v2f c4 = add_mi(b4, b6), c6 = sub_mi(b4, b6);  // b6 * W8^2 = -i
+    const v2f c5 = b5 + b7, d7 = b5 - b7;
+    a[0] = c0 + c1; a[4] = c0 - c1;
+    a[2] = add_mi(c2, d3); a[6] = sub_mi(c2, d3);
+    a[1] = c4 + c5; a[5] = c4 - c5;
+    a[3] = add_mi(c6, d7); a[7] = sub_mi(c6, d7);
+  }
+}
+
 template <bool INV>
 MIMO_DEV v2f twiddle(const float2 *__restrict__ tw, int idx) {
   const float2 w = tw[idx];

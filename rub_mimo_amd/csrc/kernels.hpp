@@ -57,7 +57,33 @@ struct ScArgs {
   uint32_t hot_cap;
   unsigned long long *prof; // diagnostics: [items, antenna passes, row, words, resolve, total
                             // cycles, skipped items] (null: off)
+  // screened path: chunk geometry and the screen's first/last unproven position per chunk
+  uint64_t nchunks;
+  const unsigned long long *fmin, *fmax;   // [F][nchunks]
 };
+
+// S&C screen over antenna 0 (sc_screen_kernel): blocks of kScrB positions, kScrSpan positions
+// per workgroup plus 2D blocks of history (D = M/2 / kScrB <= kScrMaxD)
+constexpr int kScrT = 256;
+constexpr int kScrB = 128;
+constexpr int kScrSpan = 16384;
+constexpr int kScrMaxD = 32;               // M <= 8192
+struct ScreenArgs {
+  const float2 *iq;
+  uint64_t stride, frame_len;
+  uint32_t N, M;
+  double thr_screen;                       // thr - 0.01
+  uint64_t chunk_len, chunk_lo, nchunks;
+  uint32_t *flag;                          // [F][nchunks] chunk listed
+  unsigned long long *fmin, *fmax;         // [F][nchunks] first / last unproven position
+  uint32_t *count;                         // listed chunks (= hot items)
+  ScHot *hot;                              // [cap] one per listed chunk
+  uint32_t cap;
+};
+// true when the geometry allows the screen (M/2 a multiple of kScrB, M <= 8192)
+inline bool sc_screen_ok(uint32_t M) { return M / 2 >= (uint32_t)kScrB && (M / 2) % kScrB == 0 && M / 2 / kScrB <= (uint32_t)kScrMaxD; }
+void launch_sc_screen(const ScreenArgs &a, uint32_t n_frames, hipStream_t s);
+void launch_sc_exact(const ScArgs &a, hipStream_t s);
 // persistent grid of n_cu x (resident blocks per CU) over the F x chunks items
 void launch_sc(const ScArgs &a, uint32_t n_frames, uint32_t n_cu, hipStream_t s);
 void launch_sc_hot(const ScArgs &a, hipStream_t s);   // resolve + finalize the hot items
@@ -154,9 +180,16 @@ struct DecodeArgs {
   int all_occ;                     // every subcarrier occupied (j == k): vector stores
   uint32_t n_cu;                   // compute units (persistent grid size)
   unsigned long long *prof;        // diagnostics: [items, load, fft, apply, reduce] cycles
+  uint32_t *nrec;                  // [F] EVM records per frame (decode_stream_kernel) or null
+  int expt;                        // diagnostics (RMIMO_DEC_EXPT): bit 0 IQ from one symbol,
+                                   // bit 1 no output stores, bit 2 weights of subcarrier 0
 };
-// returns the number of EVM partial sets written per symbol (see EvmArgs::parts)
-uint32_t launch_decode(const DecodeArgs &a, int log2M, uint32_t n_frames, hipStream_t s);
+// returns the number of EVM partial sets written per symbol (see EvmArgs::parts); sets
+// *per_frame_records when the streaming kernel wrote nrec[f] records per frame instead
+uint32_t launch_decode(const DecodeArgs &a, int log2M, uint32_t n_frames, hipStream_t s,
+                       bool *per_frame_records);
+// decode_stream.hip: persistent streaming form (0 when the configuration is not handled)
+uint32_t launch_decode_stream(const DecodeArgs &a, int log2M, uint32_t n_frames, hipStream_t s);
 constexpr uint32_t kMaxEvmParts = 16;
 
 struct EvmArgs {
@@ -167,6 +200,7 @@ struct EvmArgs {
   double *evm_out;                 // [F][N][3]
   double *chunk_part;              // [F][kEvmChunks][N][3]
   uint32_t *counter;               // [F] chunks done, zero between launches (self-resetting)
+  const uint32_t *nrec;            // [F] records per frame (streaming decode) or null: n_sym
 };
 constexpr uint32_t kEvmChunks = 16;
 void launch_evm(const EvmArgs &a, uint32_t n_frames, hipStream_t s);

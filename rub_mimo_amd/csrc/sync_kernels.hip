@@ -764,23 +764,26 @@ __global__ __launch_bounds__(kScT) void sc_resolve_kernel(ScArgs a) {
   __shared__ uint8_t ant[kAmbMax];
   __shared__ ResolveLds rl;
   __shared__ int s_n;
-  const uint32_t h = blockIdx.x, s = blockIdx.y;
+  const uint32_t s = blockIdx.y;
   const uint32_t count = min(*a.hot_count, a.hot_cap);
-  if (h >= count) return;
-  ScHot *hp = a.hot + h;
-  if (s >= hp->n_done) return;
-  if (threadIdx.x == 0) s_n = 0;
-  __syncthreads();
-  for (int i = threadIdx.x; i < (int)hp->namb; i += kScT)
-    if (hp->amb_s[i] == s) {
-      const int j = atomicAdd(&s_n, 1);
-      pos[j] = pos0[j] = hp->amb_n[i];
-      ant[j] = (uint8_t)s;
-    }
-  __syncthreads();
-  if (s_n == 0) return;
-  resolve_pending(a, hp->f, hp->w0, pos, pos0, ant, s_n, hp->wbits, tables,
-                  (int)(sizeof(float2) * ring_pad((int)a.M + kScIt)), rl);
+  for (uint32_t h = blockIdx.x; h < count; h += gridDim.x) {
+    ScHot *hp = a.hot + h;
+    if (s >= hp->n_done) continue;
+    if (threadIdx.x == 0) s_n = 0;
+    __syncthreads();
+    const int namb = (int)min(hp->namb, (uint32_t)kAmbMax);
+    for (int i = threadIdx.x; i < namb; i += kScT)
+      if (hp->amb_s[i] == s) {
+        const int j = atomicAdd(&s_n, 1);
+        pos[j] = pos0[j] = hp->amb_n[i];
+        ant[j] = (uint8_t)s;
+      }
+    __syncthreads();
+    if (s_n != 0)
+      resolve_pending(a, hp->f, hp->w0, pos, pos0, ant, s_n, hp->wbits, tables,
+                      (int)(sizeof(float2) * ring_pad((int)a.M + kScIt)), rl);
+    __syncthreads();
+  }
 }
 
 // hot items, stage 2: plateau rule on the corrected words, candidate, record, trigger
@@ -790,21 +793,22 @@ __global__ __launch_bounds__(kScT) void sc_finalize_kernel(ScArgs a) {
   __shared__ long long run_ws[2][kScT / 64];
   __shared__ long long lo[kMaxStreams];
   __shared__ unsigned long long s_min;
-  const uint32_t h = blockIdx.x;
   const uint32_t count = min(*a.hot_count, a.hot_cap);
-  if (h >= count) return;
-  const ScHot *hp = a.hot + h;
-  const uint32_t n_done = hp->n_done;
-  const uint32_t *src = reinterpret_cast<const uint32_t *>(hp->wbits);
-  uint32_t *dst = reinterpret_cast<uint32_t *>(wb);
-  for (int i = threadIdx.x; i < (int)n_done * kScIters * kScT / 2; i += kScT) dst[i] = src[i];
-  if (threadIdx.x < n_done) lo[threadIdx.x] = hp->lo[threadIdx.x];
-  if (threadIdx.x == 0) s_min = ~0ull;
-  __syncthreads();
-  int par = 0;
-  const int any = item_conditions(wb, acond, n_done, hp->w0, hp->c0, hp->cend, (int64_t)a.cp,
-                                  run_ws, par);
-  if (any) item_record(a, hp->f, hp->chunk, hp->w0, wb, acond, lo, s_min);
+  for (uint32_t h = blockIdx.x; h < count; h += gridDim.x) {
+    const ScHot *hp = a.hot + h;
+    const uint32_t n_done = hp->n_done;
+    const uint32_t *src = reinterpret_cast<const uint32_t *>(hp->wbits);
+    uint32_t *dst = reinterpret_cast<uint32_t *>(wb);
+    for (int i = threadIdx.x; i < (int)n_done * kScIters * kScT / 2; i += kScT) dst[i] = src[i];
+    if (threadIdx.x < n_done) lo[threadIdx.x] = hp->lo[threadIdx.x];
+    if (threadIdx.x == 0) s_min = ~0ull;
+    __syncthreads();
+    int par = 0;
+    const int any = item_conditions(wb, acond, n_done, hp->w0, hp->c0, hp->cend,
+                                    (int64_t)a.cp, run_ws, par);
+    if (any) item_record(a, hp->f, hp->chunk, hp->w0, wb, acond, lo, s_min);
+    __syncthreads();
+  }
 }
 
 // run starts (from the trigger chunk's record, exact backward scan where the run began
@@ -877,6 +881,281 @@ __global__ __launch_bounds__(64) void plateau_kernel(PlateauArgs a) {
   }
 }
 
+// ======================================================================================
+// Screened S&C (default path). The per-chunk item kernel above scans every chunk of every
+// frame and walks the antennas of a plateau chunk one after another in one workgroup; here
+//  1. sc_screen_kernel streams antenna 0 once and proves, per block of B positions, that
+//     y[n] < thr for every n of the block, from block sums alone: with Sp, Sz, Ap the block
+//     sums of p = conj(x[k-M/2]) x[k], |x[k]|^2 and |Re p| + |Im p| (M/2 = D*B),
+//       |P[n]| <= |sum_{j=1..D} Sp[b-j]| + Ap[b] + Ap[b-D]
+//       2R[n]  >= sum_{j=1..2D-1} Sz[b-j]
+//     (fp32 block sums: the bounds are widened by 1e-4 of the absolute sums and the test
+//     uses thr - 0.01, far outside the fp32 error of both the sums and the oracle's y).
+//     Chunks whose candidate range meets an unproven block are appended to a work list
+//     with the first/last unproven position;
+//  2. sc_exact_kernel evaluates every (listed chunk, antenna) in parallel, exactly as the item
+//     kernel does for one antenna (fp64 running sums, band, deferred near-threshold samples),
+//     over the iterations that cover the unproven range and its cp+2 run history;
+//  3. sc_resolve_kernel / sc_finalize_kernel (above) resolve the deferred samples and apply
+//     the plateau rule per chunk; plateau_kernel completes run starts and the sync index.
+// Positions outside the evaluated iterations carry zero bits: for antenna 0 that is exact
+// (proven), for the others it only affects run starts, which item_record / plateau_kernel
+// then take from an exact backward scan, as for a run that began before a chunk's halo.
+// ======================================================================================
+
+// block sums of antenna 0 over a span, the screen test, and the chunk list
+__global__ __launch_bounds__(kScrT) void sc_screen_kernel(ScreenArgs a) {
+  constexpr int B = kScrB;
+  __shared__ float4 recs[kScrSpan / B + 2 * (kScrMaxD)];
+  const uint32_t f = blockIdx.y;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int D = (int)(a.M / 2) / B, RL = (int)a.M / 2;
+  const int64_t L = (int64_t)a.frame_len;
+  const int64_t q0 = (int64_t)a.chunk_lo * (int64_t)a.chunk_len + (int64_t)blockIdx.x * kScrSpan;
+  if (q0 >= L) return;
+  const int NB = kScrSpan / B + 2 * D;
+  const int64_t h0 = q0 - (int64_t)2 * D * B;     // first block of the history
+  const float2 *__restrict__ x = a.iq + (uint64_t)f * a.N * a.stride;   // antenna 0
+  const bool vec = ((uintptr_t)x & 15u) == 0;
+  // block sums: a wave per block, two positions per lane (B = 128)
+  for (int j = wv; j < NB; j += kScrT / 64) {
+    const int64_t n = h0 + (int64_t)j * B + 2 * lane;
+    const float4 cur = ld_pair(x, n, L, vec), del = ld_pair(x, n - RL, L, vec);
+    const float2 c0 = make_float2(cur.x, cur.y), c1 = make_float2(cur.z, cur.w);
+    const float2 d0 = make_float2(del.x, del.y), d1 = make_float2(del.z, del.w);
+    const float2 p0 = cj_mul(d0, c0), p1 = cj_mul(d1, c1);
+    float spr = p0.x + p1.x, spi = p0.y + p1.y;
+    float sz = (c0.x * c0.x + c0.y * c0.y) + (c1.x * c1.x + c1.y * c1.y);
+    float ap = (fabsf(p0.x) + fabsf(p0.y)) + (fabsf(p1.x) + fabsf(p1.y));
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+      spr += __shfl_xor(spr, off);
+      spi += __shfl_xor(spi, off);
+      sz += __shfl_xor(sz, off);
+      ap += __shfl_xor(ap, off);
+    }
+    if (lane == 0) recs[j] = make_float4(spr, spi, sz, ap);
+  }
+  __syncthreads();
+  const int64_t K = (int64_t)a.chunk_len;
+  const int64_t lo_all = (int64_t)a.chunk_lo * K;
+  for (int j = 2 * D + tid; j < NB; j += kScrT) {
+    const int64_t n0 = h0 + (int64_t)j * B;
+    if (n0 >= L) break;
+    double pr = 0.0, pi = 0.0, apw = 0.0, rz = 0.0, azw = 0.0;
+    for (int u = 1; u <= D; u++) {
+      const float4 r = recs[j - u];
+      pr += (double)r.x;
+      pi += (double)r.y;
+      apw += (double)r.w;
+    }
+    for (int u = 1; u < 2 * D; u++) rz += (double)recs[j - u].z;
+    for (int u = 1; u <= 2 * D; u++) azw += (double)recs[j - u].z;
+    const double ab = (double)recs[j].w, ad = (double)recs[j - D].w;
+    const double pup = sqrt(pr * pr + pi * pi) + ab + ad + 1e-4 * (apw + ab + ad);
+    const double rlow = 0.5 * (rz - 1e-4 * (azw + (double)recs[j].z));
+    const bool proven = rlow > 0.0 && pup * pup < a.thr_screen * (rlow * rlow);
+    if (proven) continue;
+    // unproven block: its positions in [lo_all, L) may be candidates
+    const int64_t s0 = n0 < lo_all ? lo_all : n0;
+    const int64_t s1 = (n0 + B < L ? n0 + B : L) - 1;
+    if (s1 < s0) continue;
+    for (int64_t c = s0 / K; c <= s1 / K; c++) {
+      const uint64_t ci = (uint64_t)f * a.nchunks + (uint64_t)c;
+      const int64_t u0 = s0 > c * K ? s0 : c * K, u1 = s1 < (c + 1) * K - 1 ? s1 : (c + 1) * K - 1;
+      atomicMin(&a.fmin[ci], (unsigned long long)u0);
+      atomicMax(&a.fmax[ci], (unsigned long long)u1);
+      if (atomicOr(&a.flag[ci], 1u) == 0u) {
+        const uint32_t slot = atomicAdd(a.count, 1u);
+        if (slot < a.cap) {
+          ScHot *hp = a.hot + slot;
+          hp->f = f;
+          hp->n_done = a.N;
+          hp->namb = 0;
+          hp->chunk = (uint64_t)c;
+          hp->c0 = c * K;
+          hp->w0 = c * K - ((int64_t)kScSpan - K);
+          hp->cend = (c + 1) * K < L ? (c + 1) * K : L;
+        }
+      }
+    }
+  }
+}
+
+// one (listed chunk, antenna): the item kernel's antenna pass over the iterations covering the
+// chunk's unproven range (and its cp+2 run history); bits and deferred samples -> the hot item
+__global__ __launch_bounds__(kScT) __attribute__((amdgpu_waves_per_eu(2)))
+void sc_exact_kernel(ScArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char sc_dyn[];
+  const int M = (int)a.M, RL = M / 2, RING = M + kScIt;
+  float2 *ring = reinterpret_cast<float2 *>(sc_dyn);
+  __shared__ double scan_ws[2][5][kScT / 64];
+  const uint32_t count = min(*a.hot_count, a.hot_cap);
+  const uint32_t s = blockIdx.y;
+  for (uint32_t slot = blockIdx.x; slot < count; slot += gridDim.x) {
+  ScHot *hp = a.hot + slot;
+  const int tid = threadIdx.x;
+  const uint32_t f = hp->f;
+  const int64_t L = (int64_t)a.frame_len;
+  const int64_t w0 = hp->w0;
+  const uint64_t ci = (uint64_t)f * a.nchunks + hp->chunk;
+  const int64_t fmin = (int64_t)a.fmin[ci], fmax = (int64_t)a.fmax[ci];
+  int it_lo = (int)std::max<int64_t>(0, (fmin - (int64_t)a.cp - 2 - w0) / kScIt);
+  int it_hi = (int)std::min<int64_t>(kScIters - 1, (fmax - w0) / kScIt);
+  const float2 *__restrict__ x = a.iq + ((uint64_t)f * a.N + s) * a.stride;
+  const bool vec = ((uintptr_t)x & 15u) == 0;
+  const int64_t ib_lo = w0 + (int64_t)it_lo * kScIt;   // first evaluated position
+  if (tid == 0) hp->lo[s] = ib_lo;
+  for (int it = 0; it < kScIters; it++)
+    if (it < it_lo || it > it_hi) hp->wbits[((int)s * kScIters + it) * kScT + tid] = 0;
+  // history [ib_lo - M, ib_lo) -> its ring slots; the first block in flight behind it
+  const int wb = (kScIt * it_lo) % RING;
+  for (int j = tid; 2 * j < M; j += kScT) {
+    int sl = wb + 2 * j;
+    if (sl >= RING) sl -= RING;
+    *reinterpret_cast<float4 *>(ring + ring_pad(sl)) = ld_pair(x, ib_lo - M + 2 * j, L, vec);
+  }
+  float4 pre[kScIt / (2 * kScT)];
+  bool pf = fetch_block(pre, x, ib_lo, L, vec);
+  __syncthreads();
+  // window sums ending at ib_lo - 1: P over the last M/2, 2R and the nonzero count over M
+  double c[4] = {0.0, 0.0, 0.0, 0.0}, t4[4], tot[5];
+  for (int k = tid; k < M; k += kScT) {
+    int sl = wb + k;
+    if (sl >= RING) sl -= RING;
+    const float2 v = ring[ring_pad(sl)];
+    const float z = v.x * v.x + v.y * v.y;
+    c[2] += (double)z;
+    c[3] += (z != 0.0f) ? 1.0 : 0.0;
+    if (k >= RL) {
+      int sd = sl - RL;
+      if (sd < 0) sd += RING;
+      const float2 pp = cj_mul(ring[ring_pad(sd)], v);
+      c[0] += (double)pp.x;
+      c[1] += (double)pp.y;
+    }
+  }
+  int par = 0;
+  block_scan<4>(c, t4, scan_ws[par]);
+  par ^= 1;
+  double Pc_re = t4[0], Pc_im = t4[1], Zc = t4[2], Cc = t4[3], Ac = t4[2];
+#pragma unroll 1
+  for (int it = it_lo; it <= it_hi; it++) {
+    const int64_t ib = w0 + (int64_t)it * kScIt;
+    {
+      const int sl0 = (M + it * kScIt) % RING + 2 * tid;
+      if (pf) {
+#pragma unroll
+        for (int j = 0; j < kScIt / (2 * kScT); j++) {
+          int sl = sl0 + 2 * kScT * j;
+          if (sl >= RING) sl -= RING;
+          *reinterpret_cast<float4 *>(ring + ring_pad(sl)) = pre[j];
+        }
+      } else {   // frame edges: guarded loads straight into the ring
+#pragma unroll 1
+        for (int j = 0; j < kScIt / (2 * kScT); j++) {
+          int sl = sl0 + 2 * kScT * j;
+          if (sl >= RING) sl -= RING;
+          *reinterpret_cast<float4 *>(ring + ring_pad(sl)) =
+              ld_pair(x, ib + 2 * (tid + kScT * j), L, vec);
+        }
+      }
+    }
+    __syncthreads();
+    if (it + 1 <= it_hi) pf = fetch_block(pre, x, ib + kScIt, L, vec);
+    const float2 *xn = ring + ring_pad((M + it * kScIt + kScS * tid) % RING);
+    const float2 *xr = ring + ring_pad((RL + it * kScIt + kScS * tid) % RING);
+    const float2 *xm = ring + ring_pad((it * kScIt + kScS * tid) % RING);
+    double d[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
+    float bp = 0.0f, bz = 0.0f;
+    int dc = 0;
+#pragma unroll 2
+    for (int i = 0; i < kScS; i += 2) {
+      const float4 vn = *reinterpret_cast<const float4 *>(xn + i);
+      const float4 vr = *reinterpret_cast<const float4 *>(xr + i);
+      const float4 vm = *reinterpret_cast<const float4 *>(xm + i);
+#pragma unroll
+      for (int h = 0; h < 2; h++) {
+        const float2 n_ = h ? make_float2(vn.z, vn.w) : make_float2(vn.x, vn.y);
+        const float2 r_ = h ? make_float2(vr.z, vr.w) : make_float2(vr.x, vr.y);
+        const float2 m_ = h ? make_float2(vm.z, vm.w) : make_float2(vm.x, vm.y);
+        const float2 pn = cj_mul(r_, n_), pl = cj_mul(m_, r_);
+        const float zn = n_.x * n_.x + n_.y * n_.y, zl = m_.x * m_.x + m_.y * m_.y;
+        const double zn64 = (double)zn;
+        d[0] += (double)pn.x - (double)pl.x;
+        d[1] += (double)pn.y - (double)pl.y;
+        d[2] += zn64 - (double)zl;
+        d[4] += zn64;
+        dc += (zn != 0.0f ? 1 : 0) - (zl != 0.0f ? 1 : 0);
+        bp += (fabsf(pn.x) + fabsf(pn.y)) + (fabsf(pl.x) + fabsf(pl.y));
+        bz += zl;
+      }
+    }
+    d[3] = (double)dc;
+    block_scan<5>(d, tot, scan_ws[par]);
+    par ^= 1;
+    double Pre = Pc_re + d[0], Pim = Pc_im + d[1], Z = Zc + d[2], C = Cc + d[3];
+    const double Aend = Ac + tot[4];
+    const double zfloor = 1e-6 * Aend;
+    const int64_t sb = ib + kScS * tid;
+    uint32_t bits = 0, ovf = 0;
+    bool walk = true;
+    {
+      const double pmax = sqrt(Pre * Pre + Pim * Pim) + 1.001 * (double)bp;
+      const double rmin = 0.5 * (Z - 1.001 * (double)bz);
+      if (rmin > 0.0 && Z > 16.0 * zfloor && pmax * pmax < (a.thr - 2.0 * a.band) * (rmin * rmin))
+        walk = false;
+    }
+#pragma unroll 1
+    for (int i = 0; walk && i < kScS; i += 2) {
+      const float4 vn = *reinterpret_cast<const float4 *>(xn + i);
+      const float4 vr = *reinterpret_cast<const float4 *>(xr + i);
+      const float4 vm = *reinterpret_cast<const float4 *>(xm + i);
+#pragma unroll
+      for (int h = 0; h < 2; h++) {
+        const float2 n_ = h ? make_float2(vn.z, vn.w) : make_float2(vn.x, vn.y);
+        const float2 r_ = h ? make_float2(vr.z, vr.w) : make_float2(vr.x, vr.y);
+        const float2 m_ = h ? make_float2(vm.z, vm.w) : make_float2(vm.x, vm.y);
+        const float2 pn = cj_mul(r_, n_), pl = cj_mul(m_, r_);
+        const float zn = n_.x * n_.x + n_.y * n_.y, zl = m_.x * m_.x + m_.y * m_.y;
+        Pre += (double)pn.x - (double)pl.x;
+        Pim += (double)pn.y - (double)pl.y;
+        Z += (double)zn - (double)zl;
+        C += ((zn != 0.0f) ? 1.0 : 0.0) - ((zl != 0.0f) ? 1.0 : 0.0);
+        const int64_t n = sb + i + h;
+        bool b = false;
+        if (n >= 0 && n < L && C > 0.5) {
+          const double R = 0.5 * Z, R2 = R * R;
+          const double q = Pre * Pre + Pim * Pim - a.thr * R2;
+          if (fabs(q) <= a.band * R2 || Z <= zfloor) {
+            const uint32_t k = atomicAdd(&hp->namb, 1u);
+            if (k < (uint32_t)kAmbMax) {
+              hp->amb_n[k] = n;
+              hp->amb_s[k] = (uint8_t)s;
+              b = true;
+            } else {
+              ovf |= 1u << (i + h);   // list full: this lane recomputes it below
+            }
+          } else {
+            b = q > 0.0;
+          }
+        }
+        bits |= (b ? 1u : 0u) << (i + h);
+      }
+    }
+    while (ovf) {   // overflow of the deferred list (pathological input): exact here
+      const int i = __ffs((int)ovf) - 1;
+      ovf &= ovf - 1u;
+      if (!((double)sc_exact(x, sb + i, a.M) > a.thr)) bits &= ~(1u << i);
+      if (a.n_exact) atomicAdd(a.n_exact, 1ull);
+    }
+    Pc_re += tot[0]; Pc_im += tot[1]; Zc += tot[2]; Cc += tot[3]; Ac = Aend;
+    hp->wbits[((int)s * kScIters + it) * kScT + tid] = (uint16_t)bits;
+    __syncthreads();   // every lane's phase B reads of the ring precede the next block's writes
+  }
+  }
+}
+
 size_t sc_lds_bytes(uint32_t M, uint32_t N) {
   const int ring = (int)M + kScIt;
   return sizeof(float2) * (size_t)(ring + ((ring >> 5) << 1)) +
@@ -915,8 +1194,27 @@ void launch_sc_hot(const ScArgs &a, hipStream_t s) {
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
     set_shm = shm;
   }
-  hipLaunchKernelGGL(sc_resolve_kernel, dim3(a.hot_cap, a.N), dim3(kScT), shm, s, a);
-  hipLaunchKernelGGL(sc_finalize_kernel, dim3(a.hot_cap), dim3(kScT), 0, s, a);
+  const uint32_t gx = std::min<uint32_t>(a.hot_cap, 256);
+  hipLaunchKernelGGL(sc_resolve_kernel, dim3(gx, a.N), dim3(kScT), shm, s, a);
+  hipLaunchKernelGGL(sc_finalize_kernel, dim3(gx), dim3(kScT), 0, s, a);
+}
+
+void launch_sc_screen(const ScreenArgs &a, uint32_t n_frames, hipStream_t s) {
+  const uint64_t span = (uint64_t)a.frame_len - std::min<uint64_t>(a.frame_len, a.chunk_lo * a.chunk_len);
+  const uint32_t gx = (uint32_t)((span + kScrSpan - 1) / kScrSpan);
+  if (gx) hipLaunchKernelGGL(sc_screen_kernel, dim3(gx, n_frames), dim3(kScrT), 0, s, a);
+}
+
+void launch_sc_exact(const ScArgs &a, hipStream_t s) {
+  const size_t shm = sc_table_bytes(a.M);
+  static size_t set_shm = 0;
+  if (shm != set_shm) {
+    (void)hipFuncSetAttribute((const void *)sc_exact_kernel,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
+    set_shm = shm;
+  }
+  hipLaunchKernelGGL(sc_exact_kernel, dim3(std::min<uint32_t>(a.hot_cap, 256), a.N), dim3(kScT),
+                     shm, s, a);
 }
 
 void launch_plateau(const PlateauArgs &a, uint32_t n_frames, hipStream_t s) {
