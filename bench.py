@@ -51,6 +51,20 @@ def parse():
     return ap.parse_args()
 
 
+def decode_kernel_name(M, N, args):
+    """The decode kernel launch_decode picks for this configuration (decode_stream.hip /
+    decode_kernels.hip dispatch rules; all-carrier allocation, 16-byte aligned buffers)."""
+    lg = M.bit_length() - 1
+    stream_ok = (os.environ.get("RMIMO_DECODE_STREAM", "1") != "0" and args.detector != "siso"
+                 and args.frames <= 256 and args.qam <= 256
+                 and (N, lg) in ((4, 11), (4, 10), (2, 12), (2, 11)))
+    if stream_ok:
+        return "decode_stream_kernel<%d,%d>" % (lg, N)
+    if 512 <= M <= 4096 and N in (2, 4):
+        return "decode_reg_kernel<%d,%d>" % (lg, N)
+    return "decode_persistent_kernel"
+
+
 def main():
     args = parse()
     import torch
@@ -152,8 +166,9 @@ def main():
         try:
             pm = json.load(open(args.pmc_json))
             cfgm = pm.get("config", {})
-            if (cfgm.get("M"), cfgm.get("streams"), cfgm.get("frames"), cfgm.get("pid"),
-                    cfgm.get("ref_mode")) == (M, N, F, pid, args.ref_mode):
+            if ((cfgm.get("M"), cfgm.get("streams"), cfgm.get("frames"), cfgm.get("pid"),
+                    cfgm.get("ref_mode")) == (M, N, F, pid, args.ref_mode)
+                    and pm.get("kernel") == decode_kernel_name(M, N, args).split("<")[0]):
                 traffic = pm.get("decode_hbm_bytes_per_launch")
         except Exception:
             traffic = None
@@ -212,8 +227,7 @@ def main():
                    "parallelism": "frames sharded across %d GPU(s), no collective" % world},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "kernel": ("decode_reg_kernel<%d,%d>" % (M.bit_length() - 1, N))
-                     if 512 <= M <= 4096 else "decode_persistent_kernel",
+                     "kernel": decode_kernel_name(M, N, args),
                      "bytes_per_launch": dec_bytes,
                      "symbols_per_launch": n_dec, "bytes_per_symbol": per_sym,
                      "avg_launch_ms": dec_avg_s * 1e3},

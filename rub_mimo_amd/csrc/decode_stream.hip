@@ -61,35 +61,49 @@ struct StreamPlan {
   static constexpr int ntw(int p) { return (T % ns(p) == 0) ? 1 : bt(p); }
 };
 
-// butterfly i of the thread in pass P: antenna g and index j within the antenna
-template <int LOG2M, int NA, int P>
-MIMO_DEV void st_bfly(int tid, int i, int &g, int &j) {
-  using PL = StreamPlan<LOG2M, NA>;
-  constexpr int NB = PL::M / PL::radix(P);
-  const int u = tid + i * PL::T;
-  g = u / NB;
-  j = u % NB;
+// an opaque copy: values derived from it inside the symbol loop are recomputed where they are
+// used instead of being hoisted out of the loop and held (or spilled) across it
+MIMO_DEV int opq(int x) {
+  asm volatile("" : "+v"(x));
+  return x;
+}
+MIMO_DEV uint32_t opq_s(uint32_t x) {
+  asm volatile("" : "+s"(x));
+  return x;
 }
 
+// LDS addressing. The images are padded one slot per 32 (lds_pad). For every pass the
+// elements a thread touches sit at compile-time offsets from one padded base:
+//   store: lds_pad(o + r NS) = lds_pad(o) + r NS + floor(r NS / 32), o = (j/NS) NS R + j%NS
+//          (for NS >= 32 r NS is a multiple of 32; for NS < 32 the NS R-aligned group that
+//          holds o .. o + (R-1) NS never straddles a multiple of 32, and j%NS + r NS < 32
+//          wherever NS R >= 32);
+//   load:  lds_pad(j + r NB) = lds_pad(j) + r NB + r NB / 32 (NB = M/R a multiple of 32).
+// So each butterfly costs one address computation and its R accesses use immediate offsets.
+template <int NS, int R>
+constexpr int st_off(int r) { return r * NS + (r * NS) / 32; }
+
 template <int LOG2M, int NA, int P>
-MIMO_DEV void st_store(v2f *buf, const v2f *v, int tid) {
+MIMO_DEV void st_store(v2f *buf, const v2f *v, uint32_t tid) {
   using PL = StreamPlan<LOG2M, NA>;
-  constexpr int R = PL::radix(P), NS = PL::ns(P);
+  constexpr uint32_t R = PL::radix(P), NS = PL::ns(P), NB = PL::M / R;
+  static_assert(NB % 32 == 0 && (NS >= 32 || (32 % (NS * R) == 0) || (NS * R) % 32 == 0),
+                "padded-offset identity");
 #pragma unroll
   for (int i = 0; i < PL::bt(P); i++) {
-    int g, j;
-    st_bfly<LOG2M, NA, P>(tid, i, g, j);
-    const int o = (j / NS) * NS * R + (j % NS);
+    const uint32_t u = tid + i * PL::T, g = u / NB, j = u % NB;
+    const uint32_t o = (j / NS) * NS * R + (j % NS);
+    v2f *bp = buf + g * PL::PB + lds_pad((int)o);
 #pragma unroll
-    for (int r = 0; r < R; r++) buf[g * PL::PB + lds_pad(o + r * NS)] = v[i * R + r];
+    for (int r = 0; r < (int)R; r++) bp[st_off<NS, R>(r)] = v[i * R + r];
   }
 }
 
 // pass P with the twiddles from the LDS table (twl: passes 1.. in order, [(r-1) NS + jm])
 template <int LOG2M, int NA, int P>
-MIMO_DEV void st_load_t(const v2f *buf, v2f *v, const v2f *twl, int tid) {
+MIMO_DEV void st_load_t(const v2f *buf, v2f *v, const v2f *twl, uint32_t tid) {
   using PL = StreamPlan<LOG2M, NA>;
-  constexpr int R = PL::radix(P), NB = PL::M / R, NS = PL::ns(P);
+  constexpr uint32_t R = PL::radix(P), NB = PL::M / R, NS = PL::ns(P);
   constexpr int OFF = [] {
     int o = 0;
     for (int q = 1; q < P; q++) o += (PL::radix(q) - 1) * PL::ns(q);
@@ -97,24 +111,23 @@ MIMO_DEV void st_load_t(const v2f *buf, v2f *v, const v2f *twl, int tid) {
   }();
 #pragma unroll
   for (int i = 0; i < PL::bt(P); i++) {
-    int g, j;
-    st_bfly<LOG2M, NA, P>(tid, i, g, j);
+    const uint32_t u = tid + i * PL::T, g = u / NB, j = u % NB;
+    const v2f *bp = buf + g * PL::PB + lds_pad((int)j);
 #pragma unroll
-    for (int r = 0; r < R; r++) v[i * R + r] = buf[g * PL::PB + lds_pad(j + r * NB)];
+    for (int r = 0; r < (int)R; r++) v[i * R + r] = bp[r * NB + (r * NB) / 32];
     const v2f *tw = twl + OFF + (j % NS);
 #pragma unroll
-    for (int r = 1; r < R; r++) v[i * R + r] = cmul_pk(v[i * R + r], tw[(r - 1) * NS]);
+    for (int r = 1; r < (int)R; r++) v[i * R + r] = cmul_pk(v[i * R + r], tw[(r - 1) * NS]);
     dft_fwd_pk<R>(v + i * R);
   }
 }
 
 // passes P .. NP-1; the outputs of pass P-1 are already stored in the image
 template <int LOG2M, int NA, int P>
-MIMO_DEV void st_passes2(v2f *img, v2f *v, const v2f *twl, int tid) {
+MIMO_DEV void st_passes2(v2f *img, v2f *v, const v2f *twl, uint32_t tid) {
   using PL = StreamPlan<LOG2M, NA>;
   if constexpr (P < PL::NP) {
-    int t = tid;                            // opaque per pass: addresses are not hoisted
-    asm volatile("" : "+v"(t));
+    const uint32_t t = (uint32_t)opq((int)tid);   // opaque per pass: addresses not hoisted
     __syncthreads();                        // the image is complete
     st_load_t<LOG2M, NA, P>(img, v, twl, t);
     if constexpr (P + 1 < PL::NP) {
@@ -150,17 +163,6 @@ MIMO_DEV void dma16(uint32_t voff, __attribute__((address_space(1))) const void 
   asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t"
                "global_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
                : "=&s"(keep) : "v"(voff), "s"(sbase), "s"(lds) : "memory");
-}
-
-// an opaque copy: values derived from it inside the symbol loop are recomputed where they are
-// used instead of being hoisted out of the loop and held (or spilled) across it
-MIMO_DEV int opq(int x) {
-  asm volatile("" : "+v"(x));
-  return x;
-}
-MIMO_DEV uint32_t opq_s(uint32_t x) {
-  asm volatile("" : "+s"(x));
-  return x;
 }
 
 // a wave-uniform global pointer held in SGPRs (address arithmetic feeding it may sit in
@@ -408,11 +410,10 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
     // passes 1 .. NP-1 through the LDS images (pass 1 needs no leading barrier: the previous
     // symbol's image readers finished before the barrier at the top), then the exchange that
     // leaves the spectra in natural order
-    st_store<LOG2M, NA, 0>(img, v, opq(tid));
+    st_store<LOG2M, NA, 0>(img, v, (uint32_t)opq(tid));
     st_passes2<LOG2M, NA, 1>(img, v, twl, tid);
     {
-      int t = tid;
-      asm volatile("" : "+v"(t));
+      const uint32_t t = (uint32_t)opq(tid);
       __syncthreads();
       st_store<LOG2M, NA, PL::NP - 1>(img, v, t);
       __syncthreads();
@@ -424,8 +425,9 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
     for (int q = 0; q < S; q++) {
       const uint32_t k = (uint32_t)opq(tid) + q * T;
       v2f X[NA];
+      const v2f *xp = img + lds_pad((int)(uint32_t)opq(tid)) + q * (T + T / 32);
 #pragma unroll
-      for (int r = 0; r < NA; r++) X[r] = img[r * PB + lds_pad(k)];
+      for (int r = 0; r < NA; r++) X[r] = xp[r * PB];
 #pragma unroll
       for (int t = 0; t < NA; t++) {
         // uniform row bases (SGPRs): the stores take a 32-bit per-lane offset
@@ -448,7 +450,8 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
         const v2f er = acc - sp;
         e_num[t] = __builtin_fmaf(er.x, er.x, __builtin_fmaf(er.y, er.y, e_num[t]));
         e_den[t] = __builtin_fmaf(sp.x, sp.x, __builtin_fmaf(sp.y, sp.y, e_den[t]));
-        if constexpr (OUTS & 1) osym[k] = acc;
+        if constexpr (OUTS & 1)
+          *(gptr<v2f>)((gptr<char>)osym + k * (uint32_t)sizeof(v2f)) = acc;
         if constexpr (OUTS & 2) oidx[k] = (uint8_t)d;
       }
     }

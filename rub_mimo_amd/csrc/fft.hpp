@@ -36,18 +36,18 @@ MIMO_DEV v2f vmulc(v2f a, v2f b) {         // a * conj(b)
 // op_sel / neg modifiers (the compiler materialises {-b.y, b.x} with a v_xor and a v_mov
 // first). Results are bitwise those of vmul / rot_mi forms above.
 MIMO_DEV v2f cmul_pk(v2f a, v2f b) {     // a * b: (a.x b.x - a.y b.y, a.x b.y + a.y b.x)
-  v2f t, r;
-  asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[0,1]" : "=v"(t) : "v"(a), "v"(b));
-  asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_lo:[0,1,0]"
-      : "=v"(r) : "v"(a), "v"(b), "v"(t));
+  v2f r;
+  // one asm block: the compiler pads between separate inline-asm VALU blocks with s_nop
+  asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[0,1]\n\t"
+      "v_pk_fma_f32 %0, %1, %2, %0 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_lo:[0,1,0]"
+      : "=&v"(r) : "v"(a), "v"(b));
   return r;
 }
 MIMO_DEV v2f cmac_pk(v2f y, v2f w, v2f x) {   // y + w * x, as fma(w.xx, x, y) then fma(w.yy, ix, .)
-  v2f t, r;
-  asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel_hi:[0,1,1]" : "=v"(t) : "v"(w), "v"(x), "v"(y));
-  asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_lo:[0,1,0]"
-      : "=v"(r) : "v"(w), "v"(x), "v"(t));
-  return r;
+  asm("v_pk_fma_f32 %0, %1, %2, %0 op_sel_hi:[0,1,1]\n\t"
+      "v_pk_fma_f32 %0, %1, %2, %0 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_lo:[0,1,0]"
+      : "+v"(y) : "v"(w), "v"(x));
+  return y;
 }
 MIMO_DEV v2f add_mi(v2f a, v2f b) {      // a + b * (-i) = (a.x + b.y, a.y - b.x)
   v2f r;
