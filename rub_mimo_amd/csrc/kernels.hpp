@@ -68,6 +68,7 @@ constexpr int kScrT = 256;
 constexpr int kScrB = 128;
 constexpr int kScrSpan = 16384;
 constexpr int kScrMaxD = 32;               // M <= 8192
+constexpr int kScrBPI = 4;                 // blocks per wave iteration (loads in flight)
 struct ScreenArgs {
   const float2 *iq;
   uint64_t stride, frame_len;

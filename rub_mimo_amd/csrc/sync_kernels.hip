@@ -60,6 +60,7 @@ constexpr int kScIters = kScSpan / kScIt;
 constexpr int kAmbMax = kScAmbMax;      // provisional samples per item
 static_assert(kScIt == kScIterLen, "iteration length");
 constexpr int kResGroup = kScT / 2;     // samples per resolve pass (two lanes each)
+constexpr int kResWin = 4;              // resolve workgroups per (item, antenna): windows in parallel
 static_assert(kScSpan % kScIt == 0, "item span");
 
 // LDS ring slot -> padded float2 index: 2 float2 of padding per 32 keeps the 16-byte reads
@@ -336,6 +337,10 @@ MIMO_DEV void resolve_pending(const ScArgs &a, uint32_t f, int64_t w0, long long
     }
     __syncthreads();
     const int ng = rl.ng < kResGroup ? rl.ng : kResGroup;
+    if (a.prof && tid == 0) {                     // diagnostics (RMIMO_SC_PROF=1)
+      atomicAdd(&a.prof[17], 1ull);
+      atomicAdd(&a.prof[19], (unsigned long long)ng);
+    }
     {
       const int g = lane + 64 * (wv >> 1);
       if (g < ng) {
@@ -363,6 +368,59 @@ MIMO_DEV void resolve_pending(const ScArgs &a, uint32_t f, int64_t w0, long long
     }
     __syncthreads();
   }
+}
+
+// Exact fp32 recompute of one window's samples sorted[0 .. cnt) of antenna s (ascending,
+// sorted[cnt-1] - sorted[0] <= WCAP - M): the same table and chains as resolve_pending, for a
+// window chosen by the caller, so that the windows of one antenna run in parallel workgroups
+MIMO_DEV void resolve_window(const ScArgs &a, uint32_t f, int64_t w0, int s,
+                             const long long *sorted, int cnt, uint16_t *wbits,
+                             unsigned char *tables, int table_bytes, ResolveLds &rl) {
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int M = (int)a.M, RL = M / 2;
+  const int64_t L = (int64_t)a.frame_len;
+  const int WCAP = (table_bytes / 12) & ~3;
+  float *tz = reinterpret_cast<float *>(tables);
+  float2 *tp = reinterpret_cast<float2 *>(tables + sizeof(float) * WCAP);
+  const int64_t nmin = sorted[0];
+  const int64_t q0 = nmin - M + 1;         // table index i <-> sample q0 + i
+  const float2 *__restrict__ x = a.iq + ((uint64_t)f * a.N + s) * a.stride;
+  for (int i = tid; i < WCAP; i += kScT) {
+    const int64_t k = q0 + i;
+    const float2 v = (k >= 0 && k < L) ? x[k] : make_float2(0.0f, 0.0f);
+    const float2 dd = (k - RL >= 0 && k - RL < L) ? x[k - RL] : make_float2(0.0f, 0.0f);
+    float z = v.x * v.x + v.y * v.y;
+    tz[i] = 0.5f * z;
+    const float2 pp = cj_mul(dd, v);
+    tp[i] = make_float2((-1.0f) * pp.x, (-1.0f) * pp.y);
+  }
+  __syncthreads();
+  {
+    const int g = lane + 64 * (wv >> 1);
+    if (g < cnt) {
+      const int r = (int)(sorted[g] - nmin);
+      if ((wv & 1) == 0) {          // R over i = r .. r + M - 1
+        rl.res_v[0][g] = seq_sum(tz + r, M);
+      } else {                      // P over i = r + M/2 .. r + M - 1
+        const float2 P = seq_sum2(tp + r + RL, RL);
+        rl.res_v[1][g] = P.x;
+        rl.res_v[2][g] = P.y;
+      }
+    }
+  }
+  __syncthreads();
+  if (tid < cnt) {
+    const float Pr = rl.res_v[1][tid], Pi = rl.res_v[2][tid], R = rl.res_v[0][tid];
+    const float y32 = (Pr * Pr + Pi * Pi) / (R * R);
+    if (!((double)y32 > a.thr)) {
+      const int64_t o = sorted[tid] - w0;
+      const int it = (int)(o / kScIt), t = (int)((o % kScIt) / kScS);
+      const int bit = (int)(o % kScS) + 16 * (t & 1);
+      uint32_t *w32 = reinterpret_cast<uint32_t *>(wbits) + ((s * kScIters + it) * kScT + t) / 2;
+      atomicAnd(w32, ~(1u << bit));
+    }
+  }
+  __syncthreads();
 }
 
 // plateau rule for antennas [0, n_done) from their words into acond (candidates only in
@@ -760,28 +818,54 @@ __global__ __launch_bounds__(kScT) __attribute__((amdgpu_waves_per_eu(2))) void 
 // against the capture and clears the failing bits of the item's saved plateau words
 __global__ __launch_bounds__(kScT) void sc_resolve_kernel(ScArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char tables[];
-  __shared__ long long pos[kAmbMax], pos0[kAmbMax];
-  __shared__ uint8_t ant[kAmbMax];
+  __shared__ long long pos[kAmbMax], sorted[kAmbMax];
+  __shared__ int wstart[kAmbMax + 1];
   __shared__ ResolveLds rl;
-  __shared__ int s_n;
+  __shared__ int s_n, s_nw;
   const uint32_t s = blockIdx.y;
+  const int tid = threadIdx.x;
+  const int table_bytes = (int)(sizeof(float2) * ring_pad((int)a.M + kScIt));
+  const int WCAP = (table_bytes / 12) & ~3;
   const uint32_t count = min(*a.hot_count, a.hot_cap);
   for (uint32_t h = blockIdx.x; h < count; h += gridDim.x) {
     ScHot *hp = a.hot + h;
     if (s >= hp->n_done) continue;
-    if (threadIdx.x == 0) s_n = 0;
+    if (tid == 0) s_n = 0;
     __syncthreads();
     const int namb = (int)min(hp->namb, (uint32_t)kAmbMax);
-    for (int i = threadIdx.x; i < namb; i += kScT)
-      if (hp->amb_s[i] == s) {
-        const int j = atomicAdd(&s_n, 1);
-        pos[j] = pos0[j] = hp->amb_n[i];
-        ant[j] = (uint8_t)s;
-      }
+    for (int i = tid; i < namb; i += kScT)
+      if (hp->amb_s[i] == s) pos[atomicAdd(&s_n, 1)] = hp->amb_n[i];
     __syncthreads();
-    if (s_n != 0)
-      resolve_pending(a, hp->f, hp->w0, pos, pos0, ant, s_n, hp->wbits, tables,
-                      (int)(sizeof(float2) * ring_pad((int)a.M + kScIt)), rl);
+    const int n = s_n;
+    if (n == 0) continue;                          // block-uniform
+    if (tid == 0 && a.n_exact && blockIdx.z == 0) atomicAdd(a.n_exact, (unsigned long long)n);
+    // ascending order (positions of one antenna are distinct), then greedy windows: a window
+    // opens at its smallest sample and takes the next ones within WCAP - M, at most kResGroup;
+    // every workgroup of this (item, antenna) derives the same windows and takes every
+    // gridDim.z-th of them
+    for (int i = tid; i < n; i += kScT) {
+      int rank = 0;
+      for (int j = 0; j < n; j++) rank += (pos[j] < pos[i]) ? 1 : 0;
+      sorted[rank] = pos[i];
+    }
+    __syncthreads();
+    if (tid == 0) {
+      int nw = 0, k = 0;
+      while (k < n) {
+        wstart[nw++] = k;
+        const long long lo = sorted[k];
+        int e = k + 1;
+        while (e < n && e - k < kResGroup && sorted[e] - lo <= (long long)(WCAP - (int)a.M)) e++;
+        k = e;
+      }
+      wstart[nw] = n;
+      s_nw = nw;
+    }
+    __syncthreads();
+    const int nw = s_nw;
+    for (int w = (int)blockIdx.z; w < nw; w += (int)gridDim.z)
+      resolve_window(a, hp->f, hp->w0, (int)s, sorted + wstart[w], wstart[w + 1] - wstart[w],
+                     hp->wbits, tables, table_bytes, rl);
     __syncthreads();
   }
 }
@@ -903,8 +987,21 @@ __global__ __launch_bounds__(64) void plateau_kernel(PlateauArgs a) {
 // then take from an exact backward scan, as for a run that began before a chunk's halo.
 // ======================================================================================
 
+// one step of the transposing butterfly: of v[0 .. N) a lane keeps the half selected by its
+// lane bit OFF and adds the partner's copy of that half (compile-time indices throughout)
+template <int OFF, int N>
+MIMO_DEV void tr_reduce_step(float *v, int lane) {
+  const bool up = (lane & OFF) != 0;
+#pragma unroll
+  for (int i = 0; i < N / 2; i++) {
+    const float send = up ? v[i] : v[i + N / 2];
+    const float keep = up ? v[i + N / 2] : v[i];
+    v[i] = keep + __shfl_xor(send, OFF);
+  }
+}
+
 // block sums of antenna 0 over a span, the screen test, and the chunk list
-__global__ __launch_bounds__(kScrT) void sc_screen_kernel(ScreenArgs a) {
+__global__ __launch_bounds__(kScrT) __attribute__((amdgpu_waves_per_eu(6))) void sc_screen_kernel(ScreenArgs a) {
   constexpr int B = kScrB;
   __shared__ float4 recs[kScrSpan / B + 2 * (kScrMaxD)];
   const uint32_t f = blockIdx.y;
@@ -917,24 +1014,55 @@ __global__ __launch_bounds__(kScrT) void sc_screen_kernel(ScreenArgs a) {
   const int64_t h0 = q0 - (int64_t)2 * D * B;     // first block of the history
   const float2 *__restrict__ x = a.iq + (uint64_t)f * a.N * a.stride;   // antenna 0
   const bool vec = ((uintptr_t)x & 15u) == 0;
-  // block sums: a wave per block, two positions per lane (B = 128)
-  for (int j = wv; j < NB; j += kScrT / 64) {
-    const int64_t n = h0 + (int64_t)j * B + 2 * lane;
-    const float4 cur = ld_pair(x, n, L, vec), del = ld_pair(x, n - RL, L, vec);
-    const float2 c0 = make_float2(cur.x, cur.y), c1 = make_float2(cur.z, cur.w);
-    const float2 d0 = make_float2(del.x, del.y), d1 = make_float2(del.z, del.w);
-    const float2 p0 = cj_mul(d0, c0), p1 = cj_mul(d1, c1);
-    float spr = p0.x + p1.x, spi = p0.y + p1.y;
-    float sz = (c0.x * c0.x + c0.y * c0.y) + (c1.x * c1.x + c1.y * c1.y);
-    float ap = (fabsf(p0.x) + fabsf(p0.y)) + (fabsf(p1.x) + fabsf(p1.y));
+  // block sums: a wave per block, two positions per lane (B = 128); kScrBPI blocks per wave
+  // iteration with all their loads issued before the first use (one memory latency per
+  // iteration instead of per block)
+  for (int j0 = wv * kScrBPI; j0 < NB; j0 += (kScrT / 64) * kScrBPI) {
+    float4 cur[kScrBPI], del[kScrBPI];
+    const int64_t nb = h0 + (int64_t)j0 * B;
+    if (vec && nb - RL >= 0 && nb + (int64_t)kScrBPI * B <= L && j0 + kScrBPI <= NB) {
+      const float4 *xc = reinterpret_cast<const float4 *>(x + nb) + lane;
+      const float4 *xd = reinterpret_cast<const float4 *>(x + nb - RL) + lane;
 #pragma unroll
-    for (int off = 32; off > 0; off >>= 1) {
-      spr += __shfl_xor(spr, off);
-      spi += __shfl_xor(spi, off);
-      sz += __shfl_xor(sz, off);
-      ap += __shfl_xor(ap, off);
+      for (int b = 0; b < kScrBPI; b++) {
+        cur[b] = xc[b * (B / 2)];
+        del[b] = xd[b * (B / 2)];
+      }
+    } else {
+#pragma unroll
+      for (int b = 0; b < kScrBPI; b++) {
+        const int64_t n = nb + (int64_t)b * B + 2 * lane;
+        cur[b] = ld_pair(x, n, L, vec);
+        del[b] = ld_pair(x, n - RL, L, vec);
+      }
     }
-    if (lane == 0) recs[j] = make_float4(spr, spi, sz, ap);
+    // per-lane partials v[4 b + c] (c: Re P, Im P, |x|^2, |Re p| + |Im p|), then a transposing
+    // butterfly: at offsets 32, 16, 8, 4 a lane keeps half of its values and adds the
+    // partner's copy of them (8 + 4 + 2 + 1 exchanges for 16 sums instead of 16 x 6); lanes
+    // then hold value (lane >> 2) summed over their 16-lane group, and offsets 2, 1 finish it
+    float v[4 * kScrBPI];
+#pragma unroll
+    for (int b = 0; b < kScrBPI; b++) {
+      const float2 c0 = make_float2(cur[b].x, cur[b].y), c1 = make_float2(cur[b].z, cur[b].w);
+      const float2 d0 = make_float2(del[b].x, del[b].y), d1 = make_float2(del[b].z, del[b].w);
+      const float2 p0 = cj_mul(d0, c0), p1 = cj_mul(d1, c1);
+      v[4 * b + 0] = p0.x + p1.x;
+      v[4 * b + 1] = p0.y + p1.y;
+      v[4 * b + 2] = (c0.x * c0.x + c0.y * c0.y) + (c1.x * c1.x + c1.y * c1.y);
+      v[4 * b + 3] = (fabsf(p0.x) + fabsf(p0.y)) + (fabsf(p1.x) + fabsf(p1.y));
+    }
+    static_assert(4 * kScrBPI == 16, "transposing reduction of 16 values over 64 lanes");
+    tr_reduce_step<32, 16>(v, lane);
+    tr_reduce_step<16, 8>(v, lane);
+    tr_reduce_step<8, 4>(v, lane);
+    tr_reduce_step<4, 2>(v, lane);
+    float tot = v[0];
+    tot += __shfl_xor(tot, 2);
+    tot += __shfl_xor(tot, 1);
+    {
+      const int q = lane >> 2, b = q >> 2, c = q & 3;   // value q = 4 b + c
+      if ((lane & 3) == 0 && j0 + b < NB) reinterpret_cast<float *>(&recs[j0 + b])[c] = tot;
+    }
   }
   __syncthreads();
   const int64_t K = (int64_t)a.chunk_len;
@@ -1195,8 +1323,14 @@ void launch_sc_hot(const ScArgs &a, hipStream_t s) {
     set_shm = shm;
   }
   const uint32_t gx = std::min<uint32_t>(a.hot_cap, 256);
-  hipLaunchKernelGGL(sc_resolve_kernel, dim3(gx, a.N), dim3(kScT), shm, s, a);
-  hipLaunchKernelGGL(sc_finalize_kernel, dim3(gx), dim3(kScT), 0, s, a);
+  static const int diag = [] { const char *e = getenv("RMIMO_SC_DIAG"); return e ? atoi(e) : 0; }();
+  ScArgs ad = a;
+  if (diag & 4) ad.hot_cap = 0;      // diagnostics: same grid, every workgroup exits at once
+  // (item slot, antenna, window slot): the windows of one antenna in parallel
+  const uint32_t gxr = std::min<uint32_t>(a.hot_cap, 64);
+  if (!(diag & 1))
+    hipLaunchKernelGGL(sc_resolve_kernel, dim3(gxr, a.N, kResWin), dim3(kScT), shm, s, ad);
+  if (!(diag & 2)) hipLaunchKernelGGL(sc_finalize_kernel, dim3(gx), dim3(kScT), 0, s, a);
 }
 
 void launch_sc_screen(const ScreenArgs &a, uint32_t n_frames, hipStream_t s) {
