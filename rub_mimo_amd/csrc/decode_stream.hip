@@ -160,7 +160,9 @@ MIMO_DEV uint32_t qam_slice_pk(v2f y, v2f inv_scale, v2f Lf, uint32_t Lm1, uint3
 // point of use. M0 is saved and restored around it.
 MIMO_DEV void dma16(uint32_t voff, __attribute__((address_space(1))) const void *sbase, uint32_t lds) {
   uint32_t keep;
-  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t"
+  // s_nop 4 first: sbase may come straight from a v_readfirstlane (VALU-written SGPR read as
+  // a VMEM base needs wait states the compiler does not insert inside an asm statement)
+  asm volatile("s_nop 4\n\ts_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t"
                "global_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
                : "=&s"(keep) : "v"(voff), "s"(sbase), "s"(lds) : "memory");
 }

@@ -248,7 +248,7 @@ struct mimo_rx {
   hipStream_t g_stream = nullptr;
   bool g_valid = false;
   hipGraphExec_t g_exec = nullptr;
-  std::array<const void *, 16> g_sig{};
+  std::array<const void *, 20> g_sig{};
 };
 
 struct mimo_tx {
@@ -321,7 +321,15 @@ int run_sync(mimo_rx *h, const float2 *iq, uint64_t stride, uint32_t F, uint64_t
   const uint64_t nchunks = (frame_len + K - 1) / K;
   int rc = ensure_workspace(h, F, nchunks, 0);
   if (rc) return rc;
-  if (reset_trig) HIPCHK(hipMemsetAsync(h->trig.p, 0xFF, sizeof(unsigned long long) * F, s));
+  FillArgs fa{};
+  auto add_fill = [&fa](void *p, uint64_t bytes, uint32_t v) {
+    fa.p[fa.count] = reinterpret_cast<uint32_t *>(p);
+    fa.n[fa.count] = bytes / 4;
+    fa.v[fa.count] = v;
+    fa.count++;
+  };
+  if (reset_trig) add_fill(h->trig.p, sizeof(unsigned long long) * F, 0xFFFFFFFFu);
+  if (chunk_lo >= nchunks) launch_fill(fa, s);
   if (chunk_lo < nchunks) {
     ScArgs a{};
     a.iq = iq; a.stride = stride; a.frame_len = frame_len;
@@ -339,7 +347,7 @@ int run_sync(mimo_rx *h, const float2 *iq, uint64_t stride, uint32_t F, uint64_t
     }
     a.n_exact = h->n_exact.p;
     if (!h->queue.p) HIPCHK(h->queue.ensure(2));
-    HIPCHK(hipMemsetAsync(h->queue.p, 0, 2 * sizeof(uint32_t), s));
+    add_fill(h->queue.p, 2 * sizeof(uint32_t), 0u);
     a.queue = h->queue.p;
     a.hot_count = h->queue.p + 1;
     // screened path (default when the geometry allows it; RMIMO_SC_LEGACY=1 selects the
@@ -358,14 +366,15 @@ int run_sync(mimo_rx *h, const float2 *iq, uint64_t stride, uint32_t F, uint64_t
       HIPCHK(h->scr_flag.ensure(nf));
       HIPCHK(h->scr_min.ensure(nf));
       HIPCHK(h->scr_max.ensure(nf));
-      HIPCHK(hipMemsetAsync(h->scr_flag.p, 0, sizeof(uint32_t) * nf, s));
-      HIPCHK(hipMemsetAsync(h->scr_min.p, 0xFF, sizeof(unsigned long long) * nf, s));
-      HIPCHK(hipMemsetAsync(h->scr_max.p, 0, sizeof(unsigned long long) * nf, s));
+      add_fill(h->scr_flag.p, sizeof(uint32_t) * nf, 0u);
+      add_fill(h->scr_min.p, sizeof(unsigned long long) * nf, 0xFFFFFFFFu);
+      add_fill(h->scr_max.p, sizeof(unsigned long long) * nf, 0u);
       a.fmin = h->scr_min.p;
       a.fmax = h->scr_max.p;
     }
     a.hot = h->hot.p;
     a.hot_cap = hot_cap;
+    launch_fill(fa, s);   // trigger words, queue heads and screen flags in one launch
     static const bool prof_env = [] { const char *e = getenv("RMIMO_SC_PROF"); return e && e[0] == '1'; }();
     if (prof_env) {
       if (!h->sc_prof.p) HIPCHK(h->sc_prof.ensure(20));
@@ -911,10 +920,10 @@ static int run_batch(mimo_rx *h, const mimo_batch *b, hipStream_t s) {
 // the configuration and F (S&C items and hot items are pulled from device-side queues), so
 // the graph stays valid. Not used while stage timing or a diagnostic counter is on.
 // every device pointer a captured batch bakes into its kernels' arguments
-static std::array<const void *, 16> ws_signature(const mimo_rx *h) {
+static std::array<const void *, 20> ws_signature(const mimo_rx *h) {
   return {h->trig.p, h->keys.p, h->rec.p, h->info.p, h->G.p, h->W.p, h->gain.p, h->nvp.p,
           h->evm_part.p, h->evm_out.p, h->n_exact.p, h->queue.p, h->hot.p, h->lspart.p,
-          h->tw, h->codes.codespec.p};
+          h->tw, h->codes.codespec.p, h->scr_flag.p, h->scr_min.p, h->scr_max.p, h->nrec.p};
 }
 
 static bool same_batch(const mimo_batch &x, const mimo_batch &y) {

@@ -81,6 +81,16 @@ struct ScreenArgs {
   ScHot *hot;                              // [cap] one per listed chunk
   uint32_t cap;
 };
+// several small 32-bit-word fills in one launch (the per-batch resets of the S&C queues,
+// flags and trigger words: one kernel instead of one memset node each)
+constexpr int kMaxFill = 8;
+struct FillArgs {
+  uint32_t *p[kMaxFill];
+  uint64_t n[kMaxFill];       // words
+  uint32_t v[kMaxFill];
+  int count;
+};
+void launch_fill(const FillArgs &a, hipStream_t s);
 // true when the geometry allows the screen (M/2 a multiple of kScrB, M <= 8192)
 inline bool sc_screen_ok(uint32_t M) { return M / 2 >= (uint32_t)kScrB && (M / 2) % kScrB == 0 && M / 2 / kScrB <= (uint32_t)kScrMaxD; }
 void launch_sc_screen(const ScreenArgs &a, uint32_t n_frames, hipStream_t s);

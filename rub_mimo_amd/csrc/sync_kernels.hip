@@ -281,6 +281,39 @@ MIMO_DEV float2 cj_mul(float2 d, float2 v) {
   return make_float2(d.x * v.x - (-d.y) * v.y, d.x * v.y + (-d.y) * v.x);
 }
 
+// the recompute tables of one window: tz[i] = 0.5 |x[q0+i]|^2, tp[i] = -conj(x[q0+i-M/2]) x[q0+i]
+// (the oracle's tap products, same fp32 operations). Loads are unconditional from clamped
+// addresses and masked afterwards: a per-element "load or zero" select makes hipcc branch
+// around each load and wait for it before the next (one memory latency per element);
+// kTabU iterations' loads are in flight together
+constexpr int kTabU = 8;
+MIMO_DEV void table_fill(const float2 *__restrict__ x, int64_t q0, int64_t L, int RL, int WCAP,
+                         float *tz, float2 *tp) {
+  const int tid = threadIdx.x;
+  for (int i0 = 0; i0 < WCAP; i0 += kScT * kTabU) {
+    float2 v[kTabU], dd[kTabU];
+#pragma unroll
+    for (int u = 0; u < kTabU; u++) {
+      const int64_t k = q0 + i0 + u * kScT + tid, kd = k - RL;
+      v[u] = x[k < 0 ? 0 : (k >= L ? L - 1 : k)];
+      dd[u] = x[kd < 0 ? 0 : (kd >= L ? L - 1 : kd)];
+    }
+#pragma unroll
+    for (int u = 0; u < kTabU; u++) {
+      const int i = i0 + u * kScT + tid;
+      const int64_t k = q0 + i, kd = k - RL;
+      const float2 vv = (k >= 0 && k < L) ? v[u] : make_float2(0.0f, 0.0f);
+      const float2 dv = (kd >= 0 && kd < L) ? dd[u] : make_float2(0.0f, 0.0f);
+      if (i < WCAP) {
+        float z = vv.x * vv.x + vv.y * vv.y;
+        tz[i] = 0.5f * z;
+        const float2 pp = cj_mul(dv, vv);
+        tp[i] = make_float2((-1.0f) * pp.x, (-1.0f) * pp.y);
+      }
+    }
+  }
+}
+
 struct ResolveLds {            // LDS scratch of the exact recompute
   unsigned long long key;
   int ng;
@@ -318,15 +351,7 @@ MIMO_DEV void resolve_pending(const ScArgs &a, uint32_t f, int64_t w0, long long
     const int64_t nmin = (int64_t)(key & ((1ull << 48) - 1));
     const int64_t q0 = nmin - M + 1;       // table index i <-> sample q0 + i
     const float2 *__restrict__ x = a.iq + ((uint64_t)f * a.N + s) * a.stride;
-    for (int i = tid; i < WCAP; i += kScT) {
-      const int64_t k = q0 + i;
-      const float2 v = (k >= 0 && k < L) ? x[k] : make_float2(0.0f, 0.0f);
-      const float2 dd = (k - RL >= 0 && k - RL < L) ? x[k - RL] : make_float2(0.0f, 0.0f);
-      float z = v.x * v.x + v.y * v.y;
-      tz[i] = 0.5f * z;
-      const float2 pp = cj_mul(dd, v);
-      tp[i] = make_float2((-1.0f) * pp.x, (-1.0f) * pp.y);
-    }
+    table_fill(x, q0, L, RL, WCAP, tz, tp);
     // this window's samples (at most kResGroup per pass; the rest wait for the next pass)
     for (int i = tid; i < namb; i += kScT) {
       const int64_t n = pos[i];
@@ -385,15 +410,7 @@ MIMO_DEV void resolve_window(const ScArgs &a, uint32_t f, int64_t w0, int s,
   const int64_t nmin = sorted[0];
   const int64_t q0 = nmin - M + 1;         // table index i <-> sample q0 + i
   const float2 *__restrict__ x = a.iq + ((uint64_t)f * a.N + s) * a.stride;
-  for (int i = tid; i < WCAP; i += kScT) {
-    const int64_t k = q0 + i;
-    const float2 v = (k >= 0 && k < L) ? x[k] : make_float2(0.0f, 0.0f);
-    const float2 dd = (k - RL >= 0 && k - RL < L) ? x[k - RL] : make_float2(0.0f, 0.0f);
-    float z = v.x * v.x + v.y * v.y;
-    tz[i] = 0.5f * z;
-    const float2 pp = cj_mul(dd, v);
-    tp[i] = make_float2((-1.0f) * pp.x, (-1.0f) * pp.y);
-  }
+  table_fill(x, q0, L, RL, WCAP, tz, tp);
   __syncthreads();
   {
     const int g = lane + 64 * (wv >> 1);
@@ -1331,6 +1348,24 @@ void launch_sc_hot(const ScArgs &a, hipStream_t s) {
   if (!(diag & 1))
     hipLaunchKernelGGL(sc_resolve_kernel, dim3(gxr, a.N, kResWin), dim3(kScT), shm, s, ad);
   if (!(diag & 2)) hipLaunchKernelGGL(sc_finalize_kernel, dim3(gx), dim3(kScT), 0, s, a);
+}
+
+__global__ __launch_bounds__(256) void fill_kernel(FillArgs a) {
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (int k = 0; k < a.count; k++) {
+    uint32_t *p = a.p[k];
+    const uint32_t v = a.v[k];
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < a.n[k]; i += stride)
+      p[i] = v;
+  }
+}
+
+void launch_fill(const FillArgs &a, hipStream_t s) {
+  uint64_t mx = 0;
+  for (int k = 0; k < a.count; k++) mx = std::max<uint64_t>(mx, a.n[k]);
+  if (!mx) return;
+  const uint32_t grid = (uint32_t)std::min<uint64_t>((mx + 255) / 256, 1024);
+  hipLaunchKernelGGL(fill_kernel, dim3(grid), dim3(256), 0, s, a);
 }
 
 void launch_sc_screen(const ScreenArgs &a, uint32_t n_frames, hipStream_t s) {
