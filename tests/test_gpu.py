@@ -370,3 +370,47 @@ def test_c4_batched_full_size_properties():
     SL = M + cp
     good = (np.diff(ci.astype(np.int64), axis=2) == SL).mean()
     assert good > 0.9
+
+
+def test_stream_decode_batch_equals_single_frames():
+    """decode_stream_kernel (C3 geometry, decode_stream.hip): in a batch the persistent
+    workgroups' symbol ranges straddle frames (PID 331 is prime to every range length), yet
+    symbols and indices equal one-frame-per-call runs bit for bit; the indices are the hard
+    decisions of the symbols and the per-frame EVM / symbol-error sums equal a float64
+    recount from the outputs (ref_mode 1: transmitted indices read from HBM)."""
+    import torch
+    from rub_mimo_amd.receiver import Synthesizer, SynthParams
+    M, cp, N, nac, pid, qam, F = 2048, 152, 4, 20, 331, 64, 4
+    sp = SynthParams(M=M, cp_len=cp, num_streams=N, num_access_codes=nac, pid=pid,
+                     qam_order=qam, seed=77, snr_db=30.0)
+    syn = Synthesizer(sp)
+    L = sp.max_frame_len()
+    dev = torch.device("cuda", 0)
+    iq = torch.empty((F, N, L), dtype=torch.complex64, device=dev)
+    tx = torch.empty((F, N, pid, M), dtype=torch.uint8, device=dev)
+    syn.generate(iq, L, L, F, frame_id0=0, tx_idx=tx)
+    P = RxParams(M=M, cp_len=cp, num_streams=N, num_access_codes=nac, pid_max=pid,
+                 detector=_lib.DET_MMSE, qam_order=qam)
+    rx = Receiver(P)
+    sym = torch.zeros((F, N, pid, M), dtype=torch.complex64, device=dev)
+    idx = torch.zeros((F, N, pid, M), dtype=torch.uint8, device=dev)
+    rx.process(iq, L, L, F, max_out=pid, out_sym=sym, out_idx=idx, ref_mode=1, ref_idx=tx)
+    torch.cuda.synchronize()
+    res = rx.results(F)
+    ok = [f for f in range(F) if res[f]["status"] == _lib.FRAME_OK]
+    assert len(ok) >= 2, [r["status"] for r in res]
+    for f in ok:
+        s1 = torch.zeros((1, N, pid, M), dtype=torch.complex64, device=dev)
+        i1 = torch.zeros((1, N, pid, M), dtype=torch.uint8, device=dev)
+        r1 = Receiver(P)
+        r1.process(iq[f:f + 1], L, L, 1, max_out=pid, out_sym=s1, out_idx=i1, ref_mode=1,
+                   ref_idx=tx[f:f + 1])
+        torch.cuda.synchronize()
+        assert torch.equal(s1[0], sym[f]) and torch.equal(i1[0], idx[f]), f
+        ys = sym[f].cpu().numpy()
+        dec, num, den, err = ref.demap_evm(ys.transpose(1, 0, 2), qam, tx[f].cpu().numpy())
+        assert np.array_equal(dec, idx[f].cpu().numpy()), f
+        r = res[f]
+        assert np.array_equal(r["errors"], err.astype(np.int64)), (r["errors"], err)
+        assert np.allclose(r["evm_num"], num, rtol=1e-4), (r["evm_num"], num)
+        assert np.allclose(r["evm_den"], den, rtol=1e-5), (r["evm_den"], den)
