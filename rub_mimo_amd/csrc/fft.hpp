@@ -23,14 +23,6 @@ constexpr int lds_padded_len(int n) { return n + (n >> 5); }
 // negations folded into op_sel / neg modifiers
 typedef float v2f __attribute__((ext_vector_type(2)));
 
-MIMO_DEV v2f vmul(v2f a, v2f b) {          // a * b
-  const v2f bs = {-b.y, b.x};
-  return __builtin_elementwise_fma(a.yy, bs, a.xx * b);
-}
-MIMO_DEV v2f vmulc(v2f a, v2f b) {         // a * conj(b)
-  const v2f as = {a.y, -a.x};
-  return __builtin_elementwise_fma(b.yy, as, b.xx * a);
-}
 
 // The same operations as single VOP3P instructions with the swizzle and the sign folded into
 // op_sel / neg modifiers (the compiler materialises {-b.y, b.x} with a v_xor and a v_mov
@@ -65,6 +57,23 @@ MIMO_DEV v2f rot_m_b(v2f b) {            // b * (-i) - b = (b.y - b.x, -b.x - b.
   return r;
 }
 
+MIMO_DEV v2f rot_p_b(v2f b) {            // b * (+i) - b = (-b.y - b.x, b.x - b.y)
+  v2f r;
+  asm("v_pk_add_f32 %0, %1, %1 op_sel:[1,0] op_sel_hi:[0,1] neg_lo:[1,1] neg_hi:[0,1]" : "=v"(r) : "v"(b));
+  return r;
+}
+
+// a * b = fma(a.yy, {-b.y, b.x}, a.xx * b) and a * conj(b) = fma(b.yy, {a.y, -a.x}, b.xx * a),
+// each as two VOP3P instructions
+MIMO_DEV v2f vmul(v2f a, v2f b) { return cmul_pk(a, b); }
+MIMO_DEV v2f vmulc(v2f a, v2f b) {
+  v2f r;
+  asm("v_pk_mul_f32 %0, %2, %1 op_sel_hi:[0,1]\n\t"
+      "v_pk_fma_f32 %0, %2, %1, %0 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_hi:[0,1,0]"
+      : "=&v"(r) : "v"(a), "v"(b));
+  return r;
+}
+
 // forward radix-2/4/8 DFTs on the packed forms (same arithmetic as dft_small<R, false>)
 template <int R>
 MIMO_DEV void dft_fwd_pk(v2f *a) {
@@ -96,6 +105,37 @@ MIMO_DEV void dft_fwd_pk(v2f *a) {
   }
 }
 
+// inverse radix-2/4/8 DFTs on the packed forms (same arithmetic as the rot_mi<true> forms)
+template <int R>
+MIMO_DEV void dft_inv_pk(v2f *a) {
+  if constexpr (R == 2) {
+    const v2f t0 = a[0] + a[1], t1 = a[0] - a[1];
+    a[0] = t0; a[1] = t1;
+  } else if constexpr (R == 4) {
+    const v2f b0 = a[0] + a[2], b1 = a[0] - a[2];
+    const v2f b2 = a[1] + a[3], d3 = a[1] - a[3];
+    a[0] = b0 + b2; a[2] = b0 - b2;
+    a[1] = sub_mi(b1, d3); a[3] = add_mi(b1, d3);
+  } else {
+    static_assert(R == 8, "radix");
+    const float c = 0.70710678118654752f;
+    const v2f b0 = a[0] + a[4], b4 = a[0] - a[4];
+    const v2f b1 = a[1] + a[5], b5r = a[1] - a[5];
+    const v2f b2 = a[2] + a[6], b6 = a[2] - a[6];
+    const v2f b3 = a[3] + a[7], b7r = a[3] - a[7];
+    const v2f b5 = c * sub_mi(b5r, b5r);                 // * conj(W8^1)
+    const v2f b7 = c * rot_p_b(b7r);                     // * conj(W8^3)
+    const v2f c0 = b0 + b2, c2 = b0 - b2;
+    const v2f c1 = b1 + b3, d3 = b1 - b3;
+    const v2f c4 = sub_mi(b4, b6), c6 = add_mi(b4, b6);  // b6 * (+i)
+    const v2f c5 = b5 + b7, d7 = b5 - b7;
+    a[0] = c0 + c1; a[4] = c0 - c1;
+    a[2] = sub_mi(c2, d3); a[6] = add_mi(c2, d3);
+    a[1] = c4 + c5; a[5] = c4 - c5;
+    a[3] = sub_mi(c6, d7); a[7] = add_mi(c6, d7);
+  }
+}
+
 template <bool INV>
 MIMO_DEV v2f twiddle(const float2 *__restrict__ tw, int idx) {
   const float2 w = tw[idx];
@@ -110,7 +150,9 @@ MIMO_DEV v2f rot_mi(v2f a) {
 
 template <int R, bool INV>
 MIMO_DEV void dft_small(v2f *a) {
-  if constexpr (R == 2) {
+  if constexpr (true) {                     // single-instruction packed forms, same arithmetic
+    if constexpr (INV) dft_inv_pk<R>(a); else dft_fwd_pk<R>(a);
+  } else if constexpr (R == 2) {
     const v2f t0 = a[0] + a[1], t1 = a[0] - a[1];
     a[0] = t0; a[1] = t1;
   } else if constexpr (R == 4) {
