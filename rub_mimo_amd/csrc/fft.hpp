@@ -204,8 +204,14 @@ MIMO_DEV void fft_pass(float2 *buf, const float2 *__restrict__ tw, int tid) {
     if ((TOT % T == 0) || g < TOT) {
       const int b = g / NB, j = g % NB;
       const v2f *base = vb + b * PB;
+      if constexpr (NB % 32 == 0) {          // one padded base + compile-time offsets
+        const v2f *bp = base + lds_pad(j);
 #pragma unroll
-      for (int r = 0; r < R; r++) a[q][r] = base[lds_pad(j + r * NB)];
+        for (int r = 0; r < R; r++) a[q][r] = bp[r * NB + (r * NB) / 32];
+      } else {
+#pragma unroll
+        for (int r = 0; r < R; r++) a[q][r] = base[lds_pad(j + r * NB)];
+      }
       if constexpr (NS > 1) {
         // one table read per butterfly; the other R-2 twiddles are products of it
         // (<= 3 roundings deep, well inside the fp32 FFT error budget)
@@ -237,9 +243,9 @@ MIMO_DEV void fft_pass(float2 *buf, const float2 *__restrict__ tw, int tid) {
       const int b = g / NB, j = g % NB;
       const int k = j % NS;
       const int o = (j / NS) * NS * R + k;
-      v2f *base = vb + b * PB;
+      v2f *bp = vb + b * PB + lds_pad(o);     // lds_pad(o + r NS) = lds_pad(o) + r NS + r NS / 32
 #pragma unroll
-      for (int r = 0; r < R; r++) base[lds_pad(o + r * NS)] = a[q][r];
+      for (int r = 0; r < R; r++) bp[r * NS + (r * NS) / 32] = a[q][r];
     }
   }
   __syncthreads();

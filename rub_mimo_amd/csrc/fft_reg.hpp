@@ -60,16 +60,20 @@ MIMO_DEV void reg_twiddles(v2f *w1, const float2 *__restrict__ tw, int tid) {
   }
 }
 
+// padded addresses as one base plus compile-time offsets: lds_pad(o + r NS) = lds_pad(o) +
+// r NS + floor(r NS / 32) (NS R a power of two: the NS R-aligned group holding o .. o+(R-1)NS
+// never straddles a multiple of 32 when NS < 32), lds_pad(j + r NB) = lds_pad(j) + r NB + r NB/32
 template <int LOG2N, int PTS, int P>
 MIMO_DEV void reg_store(v2f *buf, const v2f *v, int tid) {
   using PL = RegPlan<LOG2N, PTS>;
   constexpr int R = PL::radix(P), NS = PL::ns(P);
 #pragma unroll
   for (int i = 0; i < PL::bt(P); i++) {
-    const int j = tid + i * PL::T;
-    const int o = (j / NS) * NS * R + (j % NS);
+    const uint32_t j = (uint32_t)tid + i * PL::T;
+    const uint32_t o = (j / NS) * NS * R + (j % NS);
+    v2f *bp = buf + lds_pad((int)o);
 #pragma unroll
-    for (int r = 0; r < R; r++) buf[lds_pad(o + r * NS)] = v[i * R + r];
+    for (int r = 0; r < R; r++) bp[r * NS + (r * NS) / 32] = v[i * R + r];
   }
 }
 
@@ -105,11 +109,13 @@ template <int LOG2N, int PTS, int P>
 MIMO_DEV void reg_load(const v2f *buf, v2f *v, int tid) {
   using PL = RegPlan<LOG2N, PTS>;
   constexpr int R = PL::radix(P), NB = PL::N / R;
+  static_assert(NB % 32 == 0, "padded-offset identity");
 #pragma unroll
   for (int i = 0; i < PL::bt(P); i++) {
-    const int j = tid + i * PL::T;
+    const uint32_t j = (uint32_t)tid + i * PL::T;
+    const v2f *bp = buf + lds_pad((int)j);
 #pragma unroll
-    for (int r = 0; r < R; r++) v[i * R + r] = buf[lds_pad(j + r * NB)];
+    for (int r = 0; r < R; r++) v[i * R + r] = bp[r * NB + (r * NB) / 32];
   }
 }
 
