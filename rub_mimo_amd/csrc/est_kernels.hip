@@ -140,10 +140,19 @@ void search_reg_kernel(SearchArgs a) {
   const v2f *__restrict__ x = reinterpret_cast<const v2f *>(a.iq + ((uint64_t)f * a.N + r) * a.stride);
   const bool inb = abs0 >= 0 && abs0 + F <= L;
   v2f v[PTS], cs[PTS];
+  // unconditional loads from clamped indices, masked afterwards: a per-element "load or zero"
+  // select makes hipcc branch around each load and wait for it (one latency per element)
 #pragma unroll
   for (int e = 0; e < PTS; e++) {
     const int64_t n = abs0 + reg_index<LOG2F, PTS>(tid, e);
-    v[e] = (inb || (n >= 0 && n < L)) ? x[n] : v2f{0.0f, 0.0f};
+    v[e] = x[inb ? n : (n < 0 ? 0 : (n >= L ? L - 1 : n))];
+  }
+  if (!inb) {
+#pragma unroll
+    for (int e = 0; e < PTS; e++) {
+      const int64_t n = abs0 + reg_index<LOG2F, PTS>(tid, e);
+      if (n < 0 || n >= L) v[e] = v2f{0.0f, 0.0f};
+    }
   }
   v2f w1[PL::NTW > 0 ? PL::NTW : 1];
   reg_twiddles<LOG2F, PTS>(w1, a.tw, tid);
@@ -206,20 +215,41 @@ __global__ __launch_bounds__(T) void ls_kernel(LsArgs a) {
   const int64_t L = (int64_t)a.frame_len;
   const uint32_t c0 = grp * CB;
   const uint32_t nb = min((uint32_t)CB, a.nac - c0);
+  // every code's window start first, then all 16-byte loads in flight together, then the LDS
+  // writes (a load -> ds_write loop waits out one memory latency per iteration)
+  constexpr int P2 = (M / 2 + T - 1) / T;        // 16-byte pairs per thread per code
+  int64_t abs0[CB];
+  bool fast[CB];
+#pragma unroll
   for (int b = 0; b < CB; b++) {
-    int64_t abs0 = 0;
+    abs0[b] = 0;
     if (b < (int)nb) {
       const uint32_t ac = (c0 + b) * a.N + t;
-      abs0 = I.base + key_index(a.keys[((uint64_t)f * a.N + r) * a.n_slots + 1 + ac]);
+      abs0[b] = I.base + key_index(a.keys[((uint64_t)f * a.N + r) * a.n_slots + 1 + ac]);
     }
-    const bool inb = b < (int)nb && abs0 >= 0 && abs0 + M <= L;
-    if (inb && (abs0 & 1) == 0) {   // 16-byte loads of two samples
-      const float4 *x4 = reinterpret_cast<const float4 *>(x + abs0);
-      for (int i = tid; i < M / 2; i += T)
-        *reinterpret_cast<float4 *>(lds + b * PB + lds_pad(2 * i)) = x4[i];
+    fast[b] = b < (int)nb && abs0[b] >= 0 && abs0[b] + M <= L && (abs0[b] & 1) == 0;
+  }
+  float4 stg[CB][P2];
+#pragma unroll
+  for (int b = 0; b < CB; b++) {
+    const float4 *x4 = reinterpret_cast<const float4 *>(x + (fast[b] ? abs0[b] : 0));
+#pragma unroll
+    for (int u = 0; u < P2; u++) {
+      const int i = tid + u * T;
+      stg[b][u] = (fast[b] && i < M / 2) ? x4[i] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    }
+  }
+#pragma unroll
+  for (int b = 0; b < CB; b++) {
+    if (fast[b]) {                   // 16-byte loads of two samples
+#pragma unroll
+      for (int u = 0; u < P2; u++) {
+        const int i = tid + u * T;
+        if (i < M / 2) *reinterpret_cast<float4 *>(lds + b * PB + lds_pad(2 * i)) = stg[b][u];
+      }
     } else {
       for (int i = tid; i < M; i += T) {
-        const int64_t n = abs0 + i;
+        const int64_t n = abs0[b] + i;
         lds[b * PB + lds_pad(i)] =
             (b < (int)nb && n >= 0 && n < L) ? x[n] : make_float2(0.0f, 0.0f);
       }
