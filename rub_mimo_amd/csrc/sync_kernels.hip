@@ -270,9 +270,14 @@ MIMO_DEV bool fetch_block(float4 (&pre)[kScIt / (2 * kScT)], const float2 *__res
                           int64_t q0, int64_t L, bool vec) {
   const bool ok = vec && q0 >= 0 && q0 + kScIt <= L;
   const float4 *p = reinterpret_cast<const float4 *>(x + (ok ? q0 : 0)) + threadIdx.x;
+  // one branch around all loads (a per-element select makes hipcc wait for each load in turn)
+  if (ok) {
 #pragma unroll
-  for (int j = 0; j < kScIt / (2 * kScT); j++)
-    pre[j] = ok ? p[kScT * j] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    for (int j = 0; j < kScIt / (2 * kScT); j++) pre[j] = p[kScT * j];
+  } else {
+#pragma unroll
+    for (int j = 0; j < kScIt / (2 * kScT); j++) pre[j] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+  }
   return ok;
 }
 
@@ -1155,10 +1160,32 @@ void sc_exact_kernel(ScArgs a) {
     if (it < it_lo || it > it_hi) hp->wbits[((int)s * kScIters + it) * kScT + tid] = 0;
   // history [ib_lo - M, ib_lo) -> its ring slots; the first block in flight behind it
   const int wb = (kScIt * it_lo) % RING;
-  for (int j = tid; 2 * j < M; j += kScT) {
-    int sl = wb + 2 * j;
-    if (sl >= RING) sl -= RING;
-    *reinterpret_cast<float4 *>(ring + ring_pad(sl)) = ld_pair(x, ib_lo - M + 2 * j, L, vec);
+  if (vec && ib_lo - M >= 0 && ib_lo <= L) {
+    // all history pairs in flight together, then the ring writes
+    constexpr int HU = 4;
+    for (int j0 = 0; 2 * j0 < M; j0 += kScT * HU) {
+      float4 hv[HU];
+#pragma unroll
+      for (int u = 0; u < HU; u++) {
+        const int j = j0 + u * kScT + tid;
+        hv[u] = *reinterpret_cast<const float4 *>(x + ib_lo - M + 2 * (2 * j < M ? j : 0));
+      }
+#pragma unroll
+      for (int u = 0; u < HU; u++) {
+        const int j = j0 + u * kScT + tid;
+        if (2 * j < M) {
+          int sl = wb + 2 * j;
+          if (sl >= RING) sl -= RING;
+          *reinterpret_cast<float4 *>(ring + ring_pad(sl)) = hv[u];
+        }
+      }
+    }
+  } else {
+    for (int j = tid; 2 * j < M; j += kScT) {
+      int sl = wb + 2 * j;
+      if (sl >= RING) sl -= RING;
+      *reinterpret_cast<float4 *>(ring + ring_pad(sl)) = ld_pair(x, ib_lo - M + 2 * j, L, vec);
+    }
   }
   float4 pre[kScIt / (2 * kScT)];
   bool pf = fetch_block(pre, x, ib_lo, L, vec);
