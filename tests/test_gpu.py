@@ -414,3 +414,24 @@ def test_stream_decode_batch_equals_single_frames():
         assert np.array_equal(r["errors"], err.astype(np.int64)), (r["errors"], err)
         assert np.allclose(r["evm_num"], num, rtol=1e-4), (r["evm_num"], num)
         assert np.allclose(r["evm_den"], den, rtol=1e-5), (r["evm_den"], den)
+
+
+def test_capture_files_replay_matches_golden(tmp_path):
+    """main.cc's file round trip (rx worker appends rx<ch>.dat, main re-reads it and runs
+    framesync, results land in rx_sig<ch>.dat), with the capture memory-mapped from disk."""
+    from rub_mimo_amd import logfiles as lf
+    g = load(GOLDEN[0])
+    N = int(g["N"])
+    with lf.CaptureWriter(N, str(tmp_path)) as w:
+        for pos in range(0, g["rx"].shape[1], 4096):
+            w.write([r[pos:pos + 4096] for r in g["rx"]])
+    cap = lf.read_rx_capture(N, str(tmp_path))
+    fs, got = gpu_framesync(g)
+    assert fs.execute(cap) == fr.STATE_MIMO
+    assert_sync_equal(fs, g)
+    syms = np.stack(got)                               # [callbacks][N][M_occ]
+    rx_sig = [syms[:, t, :].reshape(-1) for t in range(N)]
+    lf.write_rx_logs(rx_sig, [np.zeros(len(s), np.uint32) for s in rx_sig], str(tmp_path))
+    back = [np.fromfile(tmp_path / f"rx_sig{t + 1}.dat", np.complex64) for t in range(N)]
+    assert evm_delta(np.stack(back), np.stack([g["symbols"][:, t, :].reshape(-1)
+                                               for t in range(N)])) <= SYM_TOL
