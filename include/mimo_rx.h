@@ -205,6 +205,13 @@ int mimo_dev_free(void *ptr);
 int mimo_memcpy_h2d(void *dst, const void *src, size_t bytes, void *hip_stream);
 int mimo_memcpy_d2h(void *dst, const void *src, size_t bytes, void *hip_stream);
 int mimo_memset_d(void *dst, int value, size_t bytes, void *hip_stream);
+/* Capture ingest at the wire format (UHD sc16, mimo/config.h:52) instead of the host fc32
+ * the reference's rx worker receives (mimo/main.cc:837-848). d_sc16 holds n_arrays rows of n
+ * interleaved int16 I/Q samples, src_stride samples apart; row r is widened to complex64
+ * float(i16)*scale at d_fc32 + r*dst_stride (complex units), i.e. straight into the planar
+ * layout of mimo_batch. Rows must not overlap. Asynchronous on hip_stream. */
+int mimo_ingest_sc16(const void *d_sc16, uint64_t src_stride, void *d_fc32, uint64_t dst_stride,
+                     uint32_t n_arrays, uint64_t n, float scale, void *hip_stream);
 int mimo_stream_sync(void *hip_stream);
 int mimo_device_count(int *n);
 const char *mimo_last_error(void);

@@ -1357,6 +1357,18 @@ int mimo_memset_d(void *dst, int value, size_t bytes, void *s) {
   HIPCHK(hipMemsetAsync(dst, value, bytes, (hipStream_t)s));
   return MIMO_OK;
 }
+int mimo_ingest_sc16(const void *src, uint64_t src_stride, void *dst, uint64_t dst_stride,
+                     uint32_t n_arrays, uint64_t n, float scale, void *s) {
+  if (n == 0 || n_arrays == 0) return MIMO_OK;
+  if (!src || !dst) return fail(MIMO_ERR_ARG, "mimo_ingest_sc16: null buffer");
+  if (n_arrays > 1 && (src_stride < n || dst_stride < n))
+    return fail(MIMO_ERR_ARG, "mimo_ingest_sc16: stride shorter than a row");
+  if (!launch_sc16_to_fc32(src, src_stride, dst, dst_stride, n_arrays, n, scale,
+                           (hipStream_t)s))
+    return fail(MIMO_ERR_ARG, "mimo_ingest_sc16: too many rows or samples for one launch");
+  HIPCHK(hipGetLastError());
+  return MIMO_OK;
+}
 int mimo_stream_sync(void *s) {
   HIPCHK(hipStreamSynchronize((hipStream_t)s));
   return MIMO_OK;

@@ -260,4 +260,9 @@ struct MixArgs {
 };
 void launch_mix(const MixArgs &a, uint32_t n_frames, hipStream_t s);
 
+// sc16 wire samples (interleaved int16 I/Q) -> planar complex64 rows (ingest_kernels.hip);
+// false when the grid would not fit
+bool launch_sc16_to_fc32(const void *src, uint64_t src_stride, void *dst, uint64_t dst_stride,
+                         uint32_t rows, uint64_t n, float scale, hipStream_t s);
+
 }  // namespace mimo

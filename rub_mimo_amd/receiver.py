@@ -68,6 +68,17 @@ def _ptr(x):
     raise TypeError("expected a device pointer")
 
 
+SC16_SCALE = 1.0 / 32768.0     # int16 full scale -> [-1, 1); the caller may pass UHD's own
+
+
+def ingest_sc16(src, src_stride, dst, dst_stride, n_arrays, n, scale=SC16_SCALE, stream=None):
+    """Widen n_arrays rows of n sc16 wire samples (interleaved int16 I/Q, UHD's wire format,
+    mimo/config.h:52) on the device into planar complex64 rows of the batch layout
+    (mimo_ingest_sc16, ingest_kernels.hip). Strides are in samples."""
+    check(lib().mimo_ingest_sc16(_ptr(src), src_stride, _ptr(dst), dst_stride, n_arrays, n,
+                                 scale, stream), "mimo_ingest_sc16")
+
+
 class Receiver:
     def __init__(self, params: RxParams, stream=None):
         self.params = params

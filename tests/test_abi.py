@@ -167,3 +167,11 @@ static inline int argc_dummy() { return 0; }
                            "-L", libdir, "-lrub_mimo_amd", "-Wl,-rpath," + libdir])
     out = subprocess.check_output([str(exe)], text=True)
     assert abs(float(out.split()[-1]) - 1.0 / abs(1 - 0.5) ** 2) < 1e-5
+
+
+def test_ingest_sc16_argument_errors_without_gpu():
+    L = _lib.lib()
+    assert L.mimo_ingest_sc16(None, 0, None, 0, 0, 0, 1.0, None) == 0       # empty: no-op
+    assert L.mimo_ingest_sc16(None, 8, None, 8, 2, 8, 1.0, None) == -1      # null buffers
+    assert L.mimo_ingest_sc16(16, 4, 16, 8, 2, 8, 1.0, None) == -1          # rows overlap
+    assert b"stride" in L.mimo_last_error()

@@ -435,3 +435,33 @@ def test_capture_files_replay_matches_golden(tmp_path):
     back = [np.fromfile(tmp_path / f"rx_sig{t + 1}.dat", np.complex64) for t in range(N)]
     assert evm_delta(np.stack(back), np.stack([g["symbols"][:, t, :].reshape(-1)
                                                for t in range(N)])) <= SYM_TOL
+
+
+@pytest.mark.parametrize("rows,n,src_stride,dst_stride,off", [
+    (4, 100003, 100004, 100008, 0),     # vector path with a ragged tail
+    (3, 4099, 4101, 4099, 0),           # odd strides: scalar path
+    (2, 1024, 1024, 1024, 1),           # misaligned source: scalar path
+    (1, 0, 0, 0, 0),                    # empty
+])
+def test_ingest_sc16_bit_exact(rows, n, src_stride, dst_stride, off):
+    import torch
+    from rub_mimo_amd.receiver import SC16_SCALE, ingest_sc16
+    rng = np.random.default_rng(rows * 7 + n)
+    src = rng.integers(-32768, 32768, (rows * max(src_stride, 1) + off) * 2, dtype=np.int16)
+    if n >= 2:
+        src[off * 2: off * 2 + 4] = [-32768, 32767, 0, -1]   # full-scale ends
+    d_src = torch.from_numpy(src).cuda()
+    d_dst = torch.full((rows * max(dst_stride, 1) * 2 + 64,), 7.0, dtype=torch.float32,
+                       device="cuda")
+    ingest_sc16(d_src.data_ptr() + off * 4, src_stride, d_dst, dst_stride, rows, n,
+                stream=torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    out = d_dst.cpu().numpy()
+    for r in range(rows):
+        s = src[(off + r * src_stride) * 2:(off + r * src_stride + n) * 2]
+        want = s.astype(np.float32) * np.float32(SC16_SCALE)
+        got = out[r * dst_stride * 2:(r * dst_stride + n) * 2]
+        assert np.array_equal(got.view(np.uint32), want.view(np.uint32))
+        gap_end = min((r + 1) * dst_stride, rows * dst_stride) * 2
+        assert np.all(out[(r * dst_stride + n) * 2:gap_end] == 7.0)   # no writes past a row
+    assert np.all(out[rows * max(dst_stride, 1) * 2:] == 7.0)
