@@ -212,6 +212,15 @@ int mimo_memset_d(void *dst, int value, size_t bytes, void *hip_stream);
  * layout of mimo_batch. Rows must not overlap. Asynchronous on hip_stream. */
 int mimo_ingest_sc16(const void *d_sc16, uint64_t src_stride, void *d_fc32, uint64_t dst_stride,
                      uint32_t n_arrays, uint64_t n, float scale, void *hip_stream);
+/* Carrier-frequency offset (absent from the reference: FIXME at framing.cc:486). Over the S0
+ * body starting at sample `start` of each antenna row (period M/2, framing.cc:1054-1111),
+ * P = sum_{n<M/2} conj(x[start+n]) x[start+n+M/2]; eps = arg(P)/pi in subcarrier spacings.
+ * eps[0..n_ant-1] per antenna, eps[n_ant] from the sum of the antennas' P. Synchronous. */
+int mimo_cfo_estimate(const void *d_iq, uint64_t stride, uint32_t n_ant, uint64_t start,
+                      uint32_t M, double *eps, void *hip_stream);
+/* x[n] *= exp(-j 2 pi (eps/M) (n - n0)) for n < n on every row, in place. Asynchronous. */
+int mimo_cfo_derotate(void *d_iq, uint64_t stride, uint32_t n_ant, uint64_t n, int64_t n0,
+                      double eps, uint32_t M, void *hip_stream);
 int mimo_stream_sync(void *hip_stream);
 int mimo_device_count(int *n);
 const char *mimo_last_error(void);

@@ -104,6 +104,8 @@ SIGNATURES = {
     "mimo_memcpy_h2d": (C.c_int, [_vp, _vp, C.c_size_t, _vp]),
     "mimo_memcpy_d2h": (C.c_int, [_vp, _vp, C.c_size_t, _vp]),
     "mimo_memset_d": (C.c_int, [_vp, C.c_int, C.c_size_t, _vp]),
+    "mimo_cfo_estimate": (C.c_int, [_vp, _u64, _u32, _u64, _u32, _P(C.c_double), _vp]),
+    "mimo_cfo_derotate": (C.c_int, [_vp, _u64, _u32, _u64, C.c_int64, C.c_double, _u32, _vp]),
     "mimo_ingest_sc16": (C.c_int, [_vp, _u64, _vp, _u64, _u32, _u64, C.c_float, _vp]),
     "mimo_stream_sync": (C.c_int, [_vp]),
     "mimo_device_count": (C.c_int, [_P(C.c_int)]),

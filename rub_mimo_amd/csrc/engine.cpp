@@ -1369,6 +1369,44 @@ int mimo_ingest_sc16(const void *src, uint64_t src_stride, void *dst, uint64_t d
   HIPCHK(hipGetLastError());
   return MIMO_OK;
 }
+int mimo_cfo_estimate(const void *x, uint64_t stride, uint32_t n_ant, uint64_t start,
+                      uint32_t M, double *eps, void *s) {
+  if (!x || !eps || n_ant == 0) return fail(MIMO_ERR_ARG, "mimo_cfo_estimate: null argument");
+  if (M < 2 || (M & 1)) return fail(MIMO_ERR_ARG, "mimo_cfo_estimate: M must be even");
+  if (n_ant > 1 && stride < start + M)
+    return fail(MIMO_ERR_ARG, "mimo_cfo_estimate: window runs past the row stride");
+  double *d = nullptr;
+  HIPCHK(hipMalloc(&d, sizeof(double) * 2 * n_ant));
+  std::vector<double> h(2 * n_ant);
+  const hipStream_t st = (hipStream_t)s;
+  bool ok = launch_cfo_corr(x, stride, n_ant, start, M / 2, d, st);
+  hipError_t e = ok ? hipGetLastError() : hipSuccess;
+  if (ok && e == hipSuccess) e = hipMemcpyAsync(h.data(), d, sizeof(double) * 2 * n_ant,
+                                                hipMemcpyDeviceToHost, st);
+  if (ok && e == hipSuccess) e = hipStreamSynchronize(st);
+  (void)hipFree(d);
+  if (!ok) return fail(MIMO_ERR_ARG, "mimo_cfo_estimate: too many antenna rows");
+  if (e != hipSuccess) return fail(MIMO_ERR_HIP, std::string("mimo_cfo_estimate: ") +
+                                                     hipGetErrorString(e));
+  double re = 0.0, im = 0.0;
+  for (uint32_t r = 0; r < n_ant; ++r) {
+    eps[r] = std::atan2(h[2 * r + 1], h[2 * r]) / M_PI;
+    re += h[2 * r];
+    im += h[2 * r + 1];
+  }
+  eps[n_ant] = std::atan2(im, re) / M_PI;
+  return MIMO_OK;
+}
+int mimo_cfo_derotate(void *x, uint64_t stride, uint32_t n_ant, uint64_t n, int64_t n0,
+                      double eps, uint32_t M, void *s) {
+  if (n == 0 || n_ant == 0) return MIMO_OK;
+  if (!x || M == 0) return fail(MIMO_ERR_ARG, "mimo_cfo_derotate: null buffer or M");
+  if (n_ant > 1 && stride < n) return fail(MIMO_ERR_ARG, "mimo_cfo_derotate: stride < n");
+  if (!launch_cfo_derotate(x, stride, n_ant, n, n0, eps / M, (hipStream_t)s))
+    return fail(MIMO_ERR_ARG, "mimo_cfo_derotate: too many rows or samples for one launch");
+  HIPCHK(hipGetLastError());
+  return MIMO_OK;
+}
 int mimo_stream_sync(void *s) {
   HIPCHK(hipStreamSynchronize((hipStream_t)s));
   return MIMO_OK;

@@ -262,6 +262,12 @@ void launch_mix(const MixArgs &a, uint32_t n_frames, hipStream_t s);
 
 // sc16 wire samples (interleaved int16 I/Q) -> planar complex64 rows (ingest_kernels.hip);
 // false when the grid would not fit
+// CFO (cfo_kernels.hip): per-row sum conj(x[n]) x[n+half] over [start, start+half) into
+// d_out[2*row..], fp64; derotation by exp(-j 2 pi nu (n - n0))
+bool launch_cfo_corr(const void *x, uint64_t stride, uint32_t rows, uint64_t start,
+                     uint32_t half, double *d_out, hipStream_t s);
+bool launch_cfo_derotate(void *x, uint64_t stride, uint32_t rows, uint64_t n, int64_t n0,
+                         double nu, hipStream_t s);
 bool launch_sc16_to_fc32(const void *src, uint64_t src_stride, void *dst, uint64_t dst_stride,
                          uint32_t rows, uint64_t n, float scale, hipStream_t s);
 

@@ -79,6 +79,21 @@ def ingest_sc16(src, src_stride, dst, dst_stride, n_arrays, n, scale=SC16_SCALE,
                                  scale, stream), "mimo_ingest_sc16")
 
 
+def cfo_estimate(iq, stride, n_ant, start, M, stream=None):
+    """CFO over the S0 body at `start` (mimo_cfo_estimate): eps per antenna and combined, in
+    subcarrier spacings. Absent from the reference (framing.cc:486 FIXME); opt-in."""
+    eps = (C.c_double * (n_ant + 1))()
+    check(lib().mimo_cfo_estimate(_ptr(iq), stride, n_ant, start, M, eps, stream),
+          "mimo_cfo_estimate")
+    return np.array(eps[:n_ant]), float(eps[n_ant])
+
+
+def cfo_derotate(iq, stride, n_ant, n, n0, eps, M, stream=None):
+    """In-place x[n] *= exp(-j 2 pi (eps/M) (n - n0)) on every antenna row (mimo_cfo_derotate)."""
+    check(lib().mimo_cfo_derotate(_ptr(iq), stride, n_ant, n, n0, eps, M, stream),
+          "mimo_cfo_derotate")
+
+
 class Receiver:
     def __init__(self, params: RxParams, stream=None):
         self.params = params

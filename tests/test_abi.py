@@ -175,3 +175,14 @@ def test_ingest_sc16_argument_errors_without_gpu():
     assert L.mimo_ingest_sc16(None, 8, None, 8, 2, 8, 1.0, None) == -1      # null buffers
     assert L.mimo_ingest_sc16(16, 4, 16, 8, 2, 8, 1.0, None) == -1          # rows overlap
     assert b"stride" in L.mimo_last_error()
+
+
+def test_cfo_argument_errors_without_gpu():
+    L = _lib.lib()
+    eps = (C.c_double * 3)()
+    assert L.mimo_cfo_estimate(None, 0, 2, 0, 64, eps, None) == -1          # null rows
+    assert L.mimo_cfo_estimate(16, 64, 2, 0, 63, eps, None) == -1           # odd M
+    assert L.mimo_cfo_estimate(16, 64, 2, 8, 64, eps, None) == -1           # window past stride
+    assert b"stride" in L.mimo_last_error()
+    assert L.mimo_cfo_derotate(None, 0, 0, 0, 0, 0.1, 64, None) == 0        # empty: no-op
+    assert L.mimo_cfo_derotate(16, 10, 2, 20, 0, 0.1, 64, None) == -1       # stride < n

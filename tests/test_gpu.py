@@ -465,3 +465,35 @@ def test_ingest_sc16_bit_exact(rows, n, src_stride, dst_stride, off):
         gap_end = min((r + 1) * dst_stride, rows * dst_stride) * 2
         assert np.all(out[(r * dst_stride + n) * 2:gap_end] == 7.0)   # no writes past a row
     assert np.all(out[rows * max(dst_stride, 1) * 2:] == 7.0)
+
+
+@pytest.mark.parametrize("M,eps_true", [(2048, 0.0), (2048, 0.3137), (1024, -0.71), (64, 0.05)])
+def test_cfo_estimate_and_derotate(M, eps_true):
+    """Opt-in CFO (absent from the reference): a period-M/2 preamble rotated by eps subcarrier
+    spacings is estimated to 1e-6 (noise-free) against numpy fp64, and derotation restores the
+    samples to fp32 rounding. Parity unpinned against the reference (it has no CFO)."""
+    import torch
+    from rub_mimo_amd.receiver import cfo_derotate, cfo_estimate
+    rng = np.random.default_rng(M)
+    N, start, n = 3, 1000, 1000 + 3 * M
+    stride = n + 64
+    half = (rng.standard_normal((N, M // 2)) + 1j * rng.standard_normal((N, M // 2)))
+    x = (rng.standard_normal((N, n)) + 1j * rng.standard_normal((N, n))) * 0.1
+    x[:, start:start + M] = np.concatenate([half, half], axis=1)
+    rot = np.exp(2j * np.pi * eps_true / M * (np.arange(n) - 17))
+    xr = (x * rot).astype(np.complex64)
+    buf = np.zeros((N, stride), np.complex64)
+    buf[:, :n] = xr
+    d = torch.from_numpy(buf.view(np.float32)).cuda()
+    s = torch.cuda.current_stream().cuda_stream
+    per, comb = cfo_estimate(d, stride, N, start, M, stream=s)
+    xd = xr.astype(np.complex128)
+    P = np.sum(np.conj(xd[:, start:start + M // 2]) * xd[:, start + M // 2:start + M], axis=1)
+    assert np.allclose(per, np.angle(P) / np.pi, atol=1e-9, rtol=0)
+    assert abs(comb - np.angle(P.sum()) / np.pi) < 1e-9
+    assert abs(comb - eps_true) < 1e-5
+    cfo_derotate(d, stride, N, n, 17, comb, M, stream=s)
+    torch.cuda.synchronize()
+    back = d.cpu().numpy().view(np.complex64)
+    assert np.abs(back[:, :n] - x).max() < 1e-4 * np.abs(x).max()
+    assert np.all(back[:, n:] == 0)                                   # nothing past n
