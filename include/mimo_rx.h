@@ -43,8 +43,12 @@ enum { MIMO_STATE_SEEK_PLATEAU = 0, MIMO_STATE_SAVE_ACCESS_CODES = 1, MIMO_STATE
  * ZF / MMSE = NxN in fp64, stored fp32; SISO = X/G[rx][tx] on one stream (framing.cc:508-533) */
 enum { MIMO_DET_ZF2 = 0, MIMO_DET_ZF = 1, MIMO_DET_MMSE = 2, MIMO_DET_SISO = 3 };
 
-/* per-frame status of the batched path */
-enum { MIMO_FRAME_OK = 0, MIMO_FRAME_NO_SYNC = 1, MIMO_FRAME_INCOMPLETE = 2 };
+/* per-frame status of the batched path. RESCAN (back-to-back streams only): the re-arm at this
+ * frame's origin could not be proven equal to a fresh framesync there (a plateau or window
+ * reaching back across the re-arm point); the caller resumes the capture at `origin` as a
+ * fresh capture. NONE: an unused frame slot after the end of a stream. */
+enum { MIMO_FRAME_OK = 0, MIMO_FRAME_NO_SYNC = 1, MIMO_FRAME_INCOMPLETE = 2,
+       MIMO_FRAME_RESCAN = 3, MIMO_FRAME_NONE = 4 };
 
 /* subcarrier types, liquid OFDMFRAME_SCTYPE_{NULL,PILOT,DATA} */
 enum { MIMO_SC_NULL = 0, MIMO_SC_PILOT = 1, MIMO_SC_DATA = 2 };
@@ -108,7 +112,15 @@ int mimo_rx_get_m_occ(const mimo_rx *h, uint32_t *m_occ);
  * n_frames independent captures, each num_streams planar antenna arrays of frame_len
  * complex64 at d_iq + (f*num_streams + s)*stride (complex units). Every frame runs the whole
  * receive chain (S&C + plateau, access-code search, LS, weights, decode, demap, EVM) with
- * no host synchronisation. */
+ * no host synchronisation.
+ *
+ * frames_per_capture = K > 1 makes each capture a stream of back-to-back frames (a live
+ * 20 MS/s stream, BASELINE config C5): frame k + 1 is what a fresh framesync (framing.cc:268)
+ * finds in the samples after frame k, i.e. starting at origin
+ *   r_{k+1} = r_k + get_num_samples_processed()   (framing.cc:471-506, r_0 = 0).
+ * The reference itself stops at STATE_MIMO and its reset() keeps stale filter state
+ * (framing.cc:461-464, 494-496), so this re-arm is defined as that fresh construction. Frame
+ * slots are then [capture][K]: outputs, results and d_ref_idx rows are per slot. */
 typedef struct mimo_batch {
   const void *d_iq;
   uint64_t stride;        /* complex samples between antenna arrays (>= frame_len) */
@@ -121,8 +133,17 @@ typedef struct mimo_batch {
   const void *d_ref_idx;  /* ref_mode 1: same layout as d_out_idx */
   uint64_t ref_seed;      /* ref_mode 2: seed of mimo_synth_frames */
   uint64_t frame_id0;     /* ref_mode 2: frame id of frame 0 */
+  uint32_t frames_per_capture;  /* 0 or 1: one frame per capture; K > 1: back-to-back streams */
+  uint32_t ref_stride;          /* entries per capture in d_ref_starts (0: frames_per_capture) */
+  /* streams with ref_mode 1/2, or NULL: [n_frames][ref_stride] capture sample where each
+   * transmitted frame starts (UINT64_MAX after the last). A decoded frame whose sync index
+   * lies in [start_j, start_{j+1}) takes reference row / frame id capture*ref_stride + j;
+   * NULL: its slot. */
+  const uint64_t *d_ref_starts;
 } mimo_batch;
 
+/* Positions are those a framesync started at `origin` reports (origin 0 for one frame per
+ * capture): add origin for the capture sample. */
 typedef struct mimo_frame_result {
   int32_t status;                          /* MIMO_FRAME_* */
   uint32_t n_sym;                          /* decode callbacks (PID+2 in the reference) */
@@ -136,10 +157,14 @@ typedef struct mimo_frame_result {
   double evm_num[MIMO_MAX_STREAMS];        /* sum |y - s|^2 over kept symbols */
   double evm_den[MIMO_MAX_STREAMS];        /* sum |s|^2 */
   uint64_t errors[MIMO_MAX_STREAMS];       /* symbol errors (ref_mode 1/2) */
+  uint64_t origin;                         /* capture sample where this frame's framesync began */
+  uint32_t capture;                        /* capture (stream) index */
+  uint32_t ref_frame;                      /* reference row / frame id offset used for the EVM */
 } mimo_frame_result;
 
 int mimo_rx_process_batch(mimo_rx *h, const mimo_batch *b, void *hip_stream);
-/* copies the last batch's per-frame results to host (synchronises the stream) */
+/* copies the last batch's per-frame results to host (synchronises the stream); n_frames
+ * counts frame slots (captures x frames_per_capture) */
 int mimo_rx_batch_results(mimo_rx *h, mimo_frame_result *out, uint32_t n_frames);
 /* per-frame detail of the last batch, host copies: corr [F][N][N*nac], G [F][M][N][N] */
 int mimo_rx_batch_corr(mimo_rx *h, uint32_t *corr_idx, uint32_t *s0_idx, uint32_t n_frames);
@@ -204,6 +229,7 @@ int mimo_dev_alloc(void **ptr, size_t bytes);
 int mimo_dev_free(void *ptr);
 int mimo_memcpy_h2d(void *dst, const void *src, size_t bytes, void *hip_stream);
 int mimo_memcpy_d2h(void *dst, const void *src, size_t bytes, void *hip_stream);
+int mimo_memcpy_d2d(void *dst, const void *src, size_t bytes, void *hip_stream);
 int mimo_memset_d(void *dst, int value, size_t bytes, void *hip_stream);
 /* Capture ingest at the wire format (UHD sc16, mimo/config.h:52) instead of the host fc32
  * the reference's rx worker receives (mimo/main.cc:837-848). d_sc16 holds n_arrays rows of n

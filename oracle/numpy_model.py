@@ -185,3 +185,19 @@ def receive(rx, M, cp, N, nac, pid_max, s0_bits, s1_bits, p=None, detector="zf2"
                 sync_index=sync, base=base, corr_idx=corr_idx, s0_idx=s0_idx, G=G, W=W,
                 gain=gain, noise_var=nv_est, symbols=syms, y=ys,
                 num_samples_processed=n_e + 2 if n_e + 1 < rx.shape[1] else n_e + 1)
+
+
+def receive_stream(rx, M, cp, N, nac, pid_max, s0_bits, s1_bits, max_frames=None, **kw):
+    """Back-to-back frames: `receive` on the samples after each frame, from origin
+    r_{k+1} = r_k + num_samples_processed (a fresh framesync per frame; see oracle/ref.py
+    stream_ref). Returns [(origin, receive() dict)] for the frames that complete."""
+    L = rx.shape[1]
+    r = 0
+    out = []
+    while r < L and (max_frames is None or len(out) < max_frames):
+        d = receive(rx[:, r:], M, cp, N, nac, pid_max, s0_bits, s1_bits, **kw)
+        if d is None:
+            break
+        out.append((r, d))
+        r += d["num_samples_processed"]
+    return out

@@ -351,3 +351,56 @@ def demap_evm(sym, qam, tx_idx=None):
                         den.ctypes.data_as(C.POINTER(C.c_double)),
                         err.ctypes.data_as(C.POINTER(C.c_uint64)))
     return rx_idx, num, den, err
+
+
+def stream_ref(rx, M, cp, N, nac, pid_max=1000, max_frames=None, **kw):
+    """Back-to-back frames in one capture, received the way a caller of the reference API
+    would: a fresh framesync (framing.cc:268-436) is constructed for the samples after each
+    frame, starting at origin r_{k+1} = r_k + get_num_samples_processed() (framing.cc:471-506;
+    the reference's own STATE_MIMO is terminal, :494-496, and reset() keeps stale filter
+    state, :461-464). Positions in each record are those that framesync reports (relative to
+    its origin). Stops at the first frame that does not reach STATE_MIMO.
+
+    Returns a list of dicts: origin, state, num_samples_processed and, once synced,
+    sync_index, plateau_start/end, corr_idx, s0_idx, G, noise_var, symbols."""
+    rx = np.ascontiguousarray(rx, np.complex64)
+    L = rx.shape[1]
+    r = 0
+    out = []
+    while r < L and (max_frames is None or len(out) < max_frames):
+        fs = FrameSyncRef(M, cp, N, nac, pid_max=pid_max, **kw)
+        st = fs.execute([row[r:] for row in rx])
+        d = dict(origin=r, state=st, num_samples_processed=fs.get_num_samples_processed())
+        if st != STATE_SEEK_PLATEAU:
+            d.update(sync_index=fs.get_sync_index(),
+                     plateau_start=[fs.get_plateau_start(s) for s in range(N)],
+                     plateau_end=[fs.get_plateau_end(s) for s in range(N)])
+        if st == STATE_MIMO:
+            ci, _, si, _ = fs.get_corr()
+            d.update(corr_idx=ci, s0_idx=si, G=fs.get_G(), noise_var=fs.get_noise_var(),
+                     symbols=fs.symbols())
+        out.append(d)
+        if st != STATE_MIMO:
+            break
+        r += d["num_samples_processed"]
+    return out
+
+
+def stream_ref_file(path, M, cp, N, nac, pid_max, max_frames, detector, max_syms, qam,
+                    tx_path=None, frame_starts=None):
+    """stream_ref on a capture saved with numpy.save (worker entry for parallel checks):
+    returns the records with symbols cut to max_syms and, with tx_path ([frames][N][pid][M_occ]
+    transmitted indices) and frame_starts, each frame's EVM sums over those symbols."""
+    rx = np.load(path, mmap_mode="r")
+    recs = stream_ref(np.asarray(rx), M, cp, N, nac, pid_max=pid_max, max_frames=max_frames,
+                      detector=detector)
+    tx = np.load(tx_path, mmap_mode="r") if tx_path else None
+    for r in recs:
+        if r["state"] == STATE_MIMO:
+            r["symbols"] = r["symbols"][:max_syms]
+            r.pop("G", None)
+            if tx is not None:
+                j = int(np.searchsorted(frame_starts, r["origin"] + r["sync_index"], "right")) - 1
+                _, num, den, err = demap_evm(r["symbols"], qam, np.asarray(tx[j][:, :max_syms]))
+                r.update(tx_frame=j, evm_num=num, evm_den=den, errors=err)
+    return recs

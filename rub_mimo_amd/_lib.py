@@ -20,7 +20,7 @@ STAGE_NAMES = ("sc", "plateau", "search", "ls", "weights", "decode", "evm")
 
 STATE_SEEK_PLATEAU, STATE_SAVE_ACCESS_CODES, STATE_WAIT, STATE_MIMO = 0, 1, 2, 3
 DET_ZF2, DET_ZF, DET_MMSE, DET_SISO = 0, 1, 2, 3
-FRAME_OK, FRAME_NO_SYNC, FRAME_INCOMPLETE = 0, 1, 2
+FRAME_OK, FRAME_NO_SYNC, FRAME_INCOMPLETE, FRAME_RESCAN, FRAME_NONE = 0, 1, 2, 3, 4
 
 
 class RxConfig(C.Structure):
@@ -37,7 +37,9 @@ class Batch(C.Structure):
     _fields_ = [("d_iq", C.c_void_p), ("stride", C.c_uint64), ("frame_len", C.c_uint64),
                 ("n_frames", C.c_uint32), ("max_out_syms", C.c_uint32),
                 ("d_out_sym", C.c_void_p), ("d_out_idx", C.c_void_p), ("ref_mode", C.c_int32),
-                ("d_ref_idx", C.c_void_p), ("ref_seed", C.c_uint64), ("frame_id0", C.c_uint64)]
+                ("d_ref_idx", C.c_void_p), ("ref_seed", C.c_uint64), ("frame_id0", C.c_uint64),
+                ("frames_per_capture", C.c_uint32), ("ref_stride", C.c_uint32),
+                ("d_ref_starts", C.c_void_p)]
 
 
 class FrameResult(C.Structure):
@@ -46,7 +48,8 @@ class FrameResult(C.Structure):
                 ("plateau_start", C.c_uint64 * MAX_STREAMS),
                 ("plateau_end", C.c_uint64 * MAX_STREAMS), ("noise_var", C.c_float),
                 ("pad_", C.c_float), ("evm_num", C.c_double * MAX_STREAMS),
-                ("evm_den", C.c_double * MAX_STREAMS), ("errors", C.c_uint64 * MAX_STREAMS)]
+                ("evm_den", C.c_double * MAX_STREAMS), ("errors", C.c_uint64 * MAX_STREAMS),
+                ("origin", C.c_uint64), ("capture", C.c_uint32), ("ref_frame", C.c_uint32)]
 
 
 class SynthConfig(C.Structure):
@@ -103,6 +106,7 @@ SIGNATURES = {
     "mimo_dev_free": (C.c_int, [_vp]),
     "mimo_memcpy_h2d": (C.c_int, [_vp, _vp, C.c_size_t, _vp]),
     "mimo_memcpy_d2h": (C.c_int, [_vp, _vp, C.c_size_t, _vp]),
+    "mimo_memcpy_d2d": (C.c_int, [_vp, _vp, C.c_size_t, _vp]),
     "mimo_memset_d": (C.c_int, [_vp, C.c_int, C.c_size_t, _vp]),
     "mimo_cfo_estimate": (C.c_int, [_vp, _u64, _u32, _u64, _u32, _P(C.c_double), _vp]),
     "mimo_cfo_derotate": (C.c_int, [_vp, _u64, _u32, _u64, C.c_int64, C.c_double, _u32, _vp]),
@@ -142,6 +146,10 @@ def check(rc, what=""):
         msg = lib().mimo_last_error().decode(errors="replace")
         raise MimoError("%s failed (%d): %s" % (what, rc, msg))
     return rc
+
+
+def memcpy_d2d(dst, src, nbytes, stream=None):
+    check(lib().mimo_memcpy_d2d(dst, src, nbytes, stream), "d2d")
 
 
 def device_count():

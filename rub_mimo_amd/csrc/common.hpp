@@ -102,6 +102,10 @@ struct FrameInfo {
   uint64_t plateau_end[kMaxStreams];
   float noise_var;
   uint32_t i0;             // replay start, window index corr[N-1][last] + M
+  uint64_t origin;         // capture sample where this frame's framesync started (0, or the
+                           // re-arm point of a back-to-back stream); positions are absolute
+  uint32_t cap;            // capture holding the frame (f when each capture is one frame)
+  uint32_t ref;            // reference frame (ref_mode 1 index row, ref_mode 2 frame id - id0)
 };
 
 }  // namespace mimo

@@ -61,7 +61,7 @@ __global__ __launch_bounds__(T) void decode_kernel(DecodeArgs a) {
     if (g0 > 0) __syncthreads();
 #pragma unroll
     for (int rr = 0; rr < GA; rr++) {
-      const float2 *__restrict__ x = a.iq + ((uint64_t)f * NA + g0 + rr) * a.stride;
+      const float2 *__restrict__ x = a.iq + ((uint64_t)I.cap * NA + g0 + rr) * a.stride;
       const bool inb = (abs0 >= 0) && (abs0 + M <= L);
       if (inb) {
         // 16-byte loads: two complex samples per lane per instruction
@@ -114,7 +114,7 @@ __global__ __launch_bounds__(T) void decode_kernel(DecodeArgs a) {
   double e_num[NA], e_den[NA], e_err[NA];
 #pragma unroll
   for (int t = 0; t < NA; t++) e_num[t] = e_den[t] = e_err[t] = 0.0;
-  const uint64_t frame_id = a.frame_id0 + f;
+  const uint64_t frame_id = a.frame_id0 + I.ref;
 #pragma unroll
   for (int q = 0; q < PER; q++) {
     const int k = tid + q * T;
@@ -127,7 +127,7 @@ __global__ __launch_bounds__(T) void decode_kernel(DecodeArgs a) {
       const uint32_t d = qam_demap(y, a.qam);
       uint32_t ref = d;
       if (a.ref_mode == 1)
-        ref = a.ref_idx[(((uint64_t)f * NA + t) * a.max_out + s) * a.M_occ + j];
+        ref = a.ref_idx[(((uint64_t)I.ref * NA + t) * a.max_out + s) * a.M_occ + j];
       else if (a.ref_mode == 2)
         ref = (uint32_t)(hash5(a.ref_seed, DOM_DATA, frame_id, t,
                                (uint64_t)s * a.M_occ + j) & (uint64_t)(a.qam.L * a.qam.L - 1));
@@ -210,17 +210,18 @@ void decode_persistent_kernel(DecodeArgs a) {
   auto fetch = [&](uint32_t item) {
     bool ok = false;
     int64_t abs0 = 0;
-    uint32_t f = 0;
+    uint32_t cap = 0;
     if (item < total) {
-      uint32_t s;
+      uint32_t f, s;
       locate(item, f, s);
       const FrameInfo &I = a.info[f];
       abs0 = I.base + (int64_t)I.i0 + (int64_t)s * a.SL + a.cp;
       ok = abs0 >= 0 && abs0 + M <= (int64_t)a.frame_len;
+      cap = I.cap;
     }
 #pragma unroll
     for (int r = 0; r < NA; r++) {
-      const float2 *__restrict__ x = a.iq + ((uint64_t)f * NA + r) * a.stride + abs0;
+      const float2 *__restrict__ x = a.iq + ((uint64_t)cap * NA + r) * a.stride + abs0;
 #pragma unroll
       for (int u = 0; u < NIN; u++) {
         const int i2 = tid + u * T;
@@ -264,7 +265,8 @@ void decode_persistent_kernel(DecodeArgs a) {
     float e_num[NA], e_den[NA], e_err[NA];
 #pragma unroll
     for (int t = 0; t < NA; t++) e_num[t] = e_den[t] = e_err[t] = 0.0f;
-    const uint64_t frame_id = a.frame_id0 + f;
+    const uint32_t fref = a.info[f].ref;
+    const uint64_t frame_id = a.frame_id0 + fref;
     const float2 *__restrict__ Wf = a.W + (uint64_t)f * NA * NA * M;
     const float *__restrict__ gf = a.gain + (uint64_t)f * M;
     const v2f *vl = reinterpret_cast<const v2f *>(lds);
@@ -337,7 +339,7 @@ void decode_persistent_kernel(DecodeArgs a) {
         uint32_t refs = 0;
         if constexpr (REF == 1)
           refs = *reinterpret_cast<const uint32_t *>(
-              a.ref_idx + (((uint64_t)f * NA + t) * a.max_out + s) * a.M_occ + k0);
+              a.ref_idx + (((uint64_t)fref * NA + t) * a.max_out + s) * a.M_occ + k0);
 #pragma unroll
         for (int e = 0; e < 4; e++) {
           const int k = k0 + e;
@@ -547,7 +549,7 @@ void decode_reg_kernel(DecodeArgs a) {
     v2f v[8];
     {                                      // pass 0 straight from HBM
       const int g = tid / (M / 8), j = tid % (M / 8);
-      const v2f *x = reinterpret_cast<const v2f *>(a.iq + ((uint64_t)f * NA + g0 + g) * a.stride);
+      const v2f *x = reinterpret_cast<const v2f *>(a.iq + ((uint64_t)I.cap * NA + g0 + g) * a.stride);
 #pragma unroll
       for (int r = 0; r < 8; r++) {
         const int64_t n = abs0 + j + r * (M / 8);
@@ -580,7 +582,7 @@ void decode_reg_kernel(DecodeArgs a) {
       gn[q] = gf[k];
     }
   }
-  const uint64_t frame_id = a.frame_id0 + f;
+  const uint64_t frame_id = a.frame_id0 + I.ref;
   float e_num[NA], e_den[NA], e_err[NA];
 #pragma unroll
   for (int t = 0; t < NA; t++) e_num[t] = e_den[t] = e_err[t] = 0.0f;
@@ -595,7 +597,7 @@ void decode_reg_kernel(DecodeArgs a) {
     uint32_t refq[NA];
 #pragma unroll
     for (int t = 0; t < NA; t++) {
-      const uint64_t ob = (((uint64_t)f * NA + t) * a.max_out + s) * a.M_occ;
+      const uint64_t ob = (((uint64_t)I.ref * NA + t) * a.max_out + s) * a.M_occ;
       refq[t] = 0xFFFFFFFFu;
       if (a.ref_mode == 1 && jq[q] >= 0) refq[t] = a.ref_idx[ob + jq[q]];
     }

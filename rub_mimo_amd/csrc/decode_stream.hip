@@ -39,7 +39,7 @@
 
 namespace mimo {
 
-constexpr uint32_t kStreamMaxFrames = 256;
+constexpr uint32_t kStreamMaxFrames = 192;   // per-frame tables in LDS beside a 157 KB working set
 constexpr uint32_t kStreamMaxQam = 256;          // constellation points (256-QAM)
 
 template <int LOG2M, int NA>
@@ -198,6 +198,7 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
   v2f *twl = reinterpret_cast<v2f *>(rstg + ((REF == 1) ? NA * M : 0));   // twiddle table
   __shared__ uint32_t pfx[kStreamMaxFrames + 1];
   __shared__ int64_t fbody[kStreamMaxFrames];
+  __shared__ uint32_t fcr[kStreamMaxFrames];     // capture | reference row << 16
   __shared__ v2f ptab[kStreamMaxQam];                              // constellation by index
   const int tid = threadIdx.x;
   const uint32_t wv = __builtin_amdgcn_readfirstlane((uint32_t)tid >> 6);
@@ -229,6 +230,7 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
       const FrameInfo &I = a.info[f];
       v = (I.status == 0) ? min(I.n_sym, a.max_out) : 0u;
       fbody[f] = I.base + (int64_t)I.i0 + (int64_t)a.cp;
+      fcr[f] = I.cap | (I.ref << 16);
     }
     if (f <= a.n_frames) pfx[f] = v;
   }
@@ -275,7 +277,7 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
                                     ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)((uint64_t)b0 >> 32)) << 32))) +
                          (int64_t)ss * a.SL;
     const int64_t a0 = abs0 & ~(int64_t)1;
-    const float2 *xf = a.iq + (uint64_t)ff * NA * a.stride;
+    const float2 *xf = a.iq + (uint64_t)(__builtin_amdgcn_readfirstlane(fcr[ff]) & 0xFFFFu) * NA * a.stride;
     const int t0 = opq(tid);
     if (a0 >= 0 && a0 + RS <= (int64_t)a.frame_len && ((uintptr_t)a.iq & 15u) == 0 &&
         (a.stride & 1u) == 0) {
@@ -301,7 +303,7 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
       if (t0 < NREF) {
         const uint32_t dst = __builtin_amdgcn_readfirstlane(rstg_base + (uint32_t)(wv * 64) * 16u);
         const uint32_t t = (uint32_t)t0 / (M / 16), q = (uint32_t)t0 % (M / 16);
-        const auto rb = sgpr_ptr(a.ref_idx + ((uint64_t)ff * NA * a.max_out + ss) * a.M_occ);
+        const auto rb = sgpr_ptr(a.ref_idx + ((uint64_t)(__builtin_amdgcn_readfirstlane(fcr[ff]) >> 16) * NA * a.max_out + ss) * a.M_occ);
         dma16(t * (uint32_t)(a.max_out * a.M_occ) + 16 * q, rb, dst);
       }
     }
@@ -422,7 +424,7 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
     }
 
     // apply, demap, EVM, stores: subcarrier k = tid + q T of every stream
-    const uint64_t frame_id = a.frame_id0 + f;
+    const uint64_t frame_id = a.frame_id0 + (fcr[f] >> 16);
 #pragma unroll
     for (int q = 0; q < S; q++) {
       const uint32_t k = (uint32_t)opq(tid) + q * T;
@@ -514,7 +516,9 @@ static uint32_t stream_launch(const DecodeArgs &a, hipStream_t s) {
 
 uint32_t launch_decode_stream(const DecodeArgs &a, int log2M, uint32_t n_frames, hipStream_t s) {
   static const bool off = [] { const char *e = getenv("RMIMO_DECODE_STREAM"); return e && e[0] == '0'; }();
+  // (capture and reference row of a frame are packed in 16 bits each in LDS)
   if (off || a.detector == 3 || !a.all_occ || !a.nrec || n_frames > kStreamMaxFrames ||
+      a.n_caps > 0xFFFFu || a.n_refs > 0xFFFFu ||
       a.qam.L * a.qam.L > kStreamMaxQam)
     return 0;
   if (a.ref_mode == 1 && ((uintptr_t)a.ref_idx & 3u)) return 0;

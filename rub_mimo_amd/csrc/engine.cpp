@@ -228,6 +228,8 @@ struct mimo_rx {
   DevBuf<ScHot> hot;                    // S&C items awaiting exact resolution
   DevBuf<uint32_t> scr_flag;            // S&C screen: chunk listed [F][nchunks]
   DevBuf<unsigned long long> scr_min, scr_max;   // first / last unproven position per chunk
+  DevBuf<unsigned long long> cand;      // streams: first S&C candidate per chunk [cap][chunks]
+  DevBuf<unsigned long long> certfail;  // streams: re-arm certificate failures [cap] (bit = slot)
   uint32_t cap_hot = 0;
   DevBuf<unsigned long long> sc_prof;   // RMIMO_SC_PROF=1 cycle counters
   uint32_t last_frames = 0, last_max_out = 0;
@@ -248,7 +250,7 @@ struct mimo_rx {
   hipStream_t g_stream = nullptr;
   bool g_valid = false;
   hipGraphExec_t g_exec = nullptr;
-  std::array<const void *, 20> g_sig{};
+  std::array<const void *, 22> g_sig{};
 };
 
 struct mimo_tx {
@@ -290,7 +292,9 @@ int ensure_workspace(mimo_rx *h, uint32_t F, uint64_t chunks, uint64_t evm_entri
     const uint64_t nc = std::max<uint64_t>(chunks, h->cap_chunks * 2);
     ScRecord *np = nullptr;
     HIPCHK(hipMalloc(&np, sizeof(ScRecord) * (size_t)h->cap_frames * nc));
-    if (h->rec.p && h->cap_chunks && h->cap_frames == 1)
+    // frame 0's records survive: the streaming execute path (one frame) never recomputes a
+    // final chunk, whatever batch sizes the handle ran before
+    if (h->rec.p && h->cap_chunks)
       HIPCHK(hipMemcpy(np, h->rec.p, sizeof(ScRecord) * h->cap_chunks, hipMemcpyDeviceToDevice));
     h->rec.release();
     h->rec.p = np;
@@ -314,12 +318,15 @@ static double sc_band(uint32_t M) {
   return 1.25 * u * (std::sqrt(2.0) * (M + 4.0) + 2.0 * M + 6.0);
 }
 
-// S&C + plateau over chunks [chunk_lo, end) of every frame
+// S&C + plateau over chunks [chunk_lo, end) of every capture; with fpc > 1 frames per capture
+// the stream walk assigns F * fpc frame slots
 int run_sync(mimo_rx *h, const float2 *iq, uint64_t stride, uint32_t F, uint64_t frame_len,
-             uint64_t chunk_lo, bool reset_trig, hipStream_t s) {
+             uint64_t chunk_lo, bool reset_trig, hipStream_t s, uint32_t fpc = 1,
+             const uint64_t *ref_starts = nullptr, uint32_t ref_stride = 0) {
   const uint64_t K = sc_chunk_len(h->cp);
   const uint64_t nchunks = (frame_len + K - 1) / K;
-  int rc = ensure_workspace(h, F, nchunks, 0);
+  const bool stream = fpc > 1;
+  int rc = ensure_workspace(h, F * fpc, nchunks, 0);
   if (rc) return rc;
   FillArgs fa{};
   auto add_fill = [&fa](void *p, uint64_t bytes, uint32_t v) {
@@ -329,6 +336,12 @@ int run_sync(mimo_rx *h, const float2 *iq, uint64_t stride, uint32_t F, uint64_t
     fa.count++;
   };
   if (reset_trig) add_fill(h->trig.p, sizeof(unsigned long long) * F, 0xFFFFFFFFu);
+  if (stream) {
+    HIPCHK(h->cand.ensure((size_t)F * nchunks));
+    HIPCHK(h->certfail.ensure(F));
+    add_fill(h->cand.p, sizeof(unsigned long long) * F * nchunks, 0xFFFFFFFFu);
+    add_fill(h->certfail.p, sizeof(unsigned long long) * F, 0u);
+  }
   if (chunk_lo >= nchunks) launch_fill(fa, s);
   if (chunk_lo < nchunks) {
     ScArgs a{};
@@ -341,6 +354,8 @@ int run_sync(mimo_rx *h, const float2 *iq, uint64_t stride, uint32_t F, uint64_t
     a.band = band_env >= 0.0 ? band_env : sc_band(h->M);
     a.chunk_len = K; a.chunk_lo = chunk_lo; a.chunk_hi = nchunks;
     a.trig = h->trig.p; a.rec = h->rec.p; a.rec_stride = h->cap_chunks;
+    a.cand = stream ? h->cand.p : nullptr;
+    a.no_skip = stream ? 1 : 0;
     if (!h->n_exact.p) {
       HIPCHK(h->n_exact.ensure(1));
       HIPCHK(hipMemsetAsync(h->n_exact.p, 0, sizeof(unsigned long long), s));
@@ -418,9 +433,16 @@ int run_sync(mimo_rx *h, const float2 *iq, uint64_t stride, uint32_t F, uint64_t
   pa.trig = h->trig.p; pa.rec = h->rec.p; pa.rec_stride = h->cap_chunks; pa.chunk_len = K;
   pa.iq = iq; pa.stride = stride; pa.frame_len = frame_len;
   pa.N = h->N; pa.M = h->M; pa.SL = h->SL; pa.thr = h->thr; pa.win_len = h->win_len;
+  pa.band = sc_band(h->M);
   pa.info = h->info.p;
+  pa.fpc = fpc; pa.nchunks = nchunks;
+  pa.cand = stream ? h->cand.p : nullptr;
+  pa.certfail = stream ? h->certfail.p : nullptr;
+  pa.ref_starts = ref_starts;
+  pa.ref_stride = ref_stride ? ref_stride : fpc;
   hipEvent_t e = h->timer.begin(s);
-  launch_plateau(pa, F, s);
+  if (stream) launch_stream_walk(pa, F, s);
+  else launch_plateau(pa, F, s);
   h->timer.end(1, e, s);
   HIPCHK(hipGetLastError());
   return MIMO_OK;
@@ -472,7 +494,8 @@ int run_estimate(mimo_rx *h, const float2 *iq, uint64_t stride, uint32_t F, uint
 
 int run_decode(mimo_rx *h, const float2 *iq, uint64_t stride, uint32_t F, uint64_t frame_len,
                uint32_t max_out, float2 *out_sym, uint8_t *out_idx, int ref_mode,
-               const uint8_t *ref_idx, uint64_t ref_seed, uint64_t frame_id0, hipStream_t s) {
+               const uint8_t *ref_idx, uint64_t ref_seed, uint64_t frame_id0, hipStream_t s,
+               uint32_t n_caps = 0) {
   int rc = ensure_workspace(h, F, 0, (uint64_t)F * max_out * h->N * 3 * kMaxEvmParts);
   if (rc) return rc;
   if (max_out == 0) return MIMO_OK;
@@ -485,6 +508,7 @@ int run_decode(mimo_rx *h, const float2 *iq, uint64_t stride, uint32_t F, uint64
   d.ref_mode = ref_mode; d.ref_idx = ref_idx; d.ref_seed = ref_seed; d.frame_id0 = frame_id0;
   d.qam = h->qam; d.evm_part = h->evm_part.p; d.tw = h->tw;
   d.n_frames = F; d.n_cu = h->n_cu;
+  d.n_caps = n_caps ? n_caps : F; d.n_refs = F;
   // RMIMO_DECODE_GRID=1 forces the one-workgroup-per-symbol grid (A/B against the persistent form)
   static const bool grid_only = [] { const char *e = getenv("RMIMO_DECODE_GRID"); return e && e[0] == '1'; }();
   d.all_occ = (h->M_occ == h->M && !grid_only) ? 1 : 0;
@@ -652,8 +676,21 @@ int mimo_rx_set_callback(mimo_rx *h, mimo_rx_symbol_cb cb, void *user) {
   return MIMO_OK;
 }
 
+// A captured batch graph bakes every host scalar of the launch arguments (siso indices,
+// detector, noise variance, threshold) into its kernel nodes: any setter of such a scalar
+// drops the graph so the next batch is launched (and later re-captured) with the new value.
+static void invalidate_graph(mimo_rx *h) {
+  if (h->g_exec) {
+    (void)hipStreamSynchronize(h->g_stream ? h->g_stream : h->stream);
+    (void)hipGraphExecDestroy(h->g_exec);
+    h->g_exec = nullptr;
+  }
+  h->g_valid = false;
+}
+
 int mimo_rx_set_siso(mimo_rx *h, uint32_t tx, uint32_t rx) {
   if (!h || tx >= h->N || rx >= h->N) return fail(MIMO_ERR_ARG, "siso index out of range");
+  if (tx != h->siso_tx || rx != h->siso_rx) invalidate_graph(h);
   h->siso_tx = tx;
   h->siso_rx = rx;
   return MIMO_OK;
@@ -902,16 +939,22 @@ int mimo_rx_get_corr(mimo_rx *h, uint32_t *corr, uint32_t *s0) {
 }
 
 // ---------------- batched device frames ----------------
+static uint32_t batch_fpc(const mimo_batch *b) {
+  return b->frames_per_capture > 1 ? b->frames_per_capture : 1u;
+}
+
 static int run_batch(mimo_rx *h, const mimo_batch *b, hipStream_t s) {
   const float2 *iq = reinterpret_cast<const float2 *>(b->d_iq);
-  int rc = run_sync(h, iq, b->stride, b->n_frames, b->frame_len, 0, true, s);
-  if (!rc) rc = run_estimate(h, iq, b->stride, b->n_frames, b->frame_len, s);
+  const uint32_t fpc = batch_fpc(b), slots = b->n_frames * fpc;
+  int rc = run_sync(h, iq, b->stride, b->n_frames, b->frame_len, 0, true, s, fpc,
+                    fpc > 1 ? b->d_ref_starts : nullptr, b->ref_stride);
+  if (!rc) rc = run_estimate(h, iq, b->stride, slots, b->frame_len, s);
   if (!rc)
-    rc = run_decode(h, iq, b->stride, b->n_frames, b->frame_len, b->max_out_syms,
+    rc = run_decode(h, iq, b->stride, slots, b->frame_len, b->max_out_syms,
                     reinterpret_cast<float2 *>(b->d_out_sym),
                     reinterpret_cast<uint8_t *>(b->d_out_idx), b->ref_mode,
                     reinterpret_cast<const uint8_t *>(b->d_ref_idx), b->ref_seed, b->frame_id0,
-                    s);
+                    s, b->n_frames);
   return rc;
 }
 
@@ -920,17 +963,20 @@ static int run_batch(mimo_rx *h, const mimo_batch *b, hipStream_t s) {
 // the configuration and F (S&C items and hot items are pulled from device-side queues), so
 // the graph stays valid. Not used while stage timing or a diagnostic counter is on.
 // every device pointer a captured batch bakes into its kernels' arguments
-static std::array<const void *, 20> ws_signature(const mimo_rx *h) {
+static std::array<const void *, 22> ws_signature(const mimo_rx *h) {
   return {h->trig.p, h->keys.p, h->rec.p, h->info.p, h->G.p, h->W.p, h->gain.p, h->nvp.p,
           h->evm_part.p, h->evm_out.p, h->n_exact.p, h->queue.p, h->hot.p, h->lspart.p,
-          h->tw, h->codes.codespec.p, h->scr_flag.p, h->scr_min.p, h->scr_max.p, h->nrec.p};
+          h->tw, h->codes.codespec.p, h->scr_flag.p, h->scr_min.p, h->scr_max.p, h->nrec.p,
+          h->cand.p, h->certfail.p};
 }
 
 static bool same_batch(const mimo_batch &x, const mimo_batch &y) {
   return x.d_iq == y.d_iq && x.stride == y.stride && x.frame_len == y.frame_len &&
          x.n_frames == y.n_frames && x.max_out_syms == y.max_out_syms &&
          x.d_out_sym == y.d_out_sym && x.d_out_idx == y.d_out_idx && x.ref_mode == y.ref_mode &&
-         x.d_ref_idx == y.d_ref_idx && x.ref_seed == y.ref_seed && x.frame_id0 == y.frame_id0;
+         x.d_ref_idx == y.d_ref_idx && x.ref_seed == y.ref_seed && x.frame_id0 == y.frame_id0 &&
+         batch_fpc(&x) == batch_fpc(&y) && x.d_ref_starts == y.d_ref_starts &&
+         x.ref_stride == y.ref_stride;
 }
 
 int mimo_rx_process_batch(mimo_rx *h, const mimo_batch *b, void *hip_stream) {
@@ -938,6 +984,8 @@ int mimo_rx_process_batch(mimo_rx *h, const mimo_batch *b, void *hip_stream) {
   if (b->n_frames == 0) return MIMO_OK;
   if (b->stride < b->frame_len) return fail(MIMO_ERR_ARG, "stride < frame_len");
   if (b->ref_mode == 1 && !b->d_ref_idx) return fail(MIMO_ERR_ARG, "ref_mode 1 needs d_ref_idx");
+  if (batch_fpc(b) > 64)
+    return fail(MIMO_ERR_ARG, "frames_per_capture must be at most 64");
   hipStream_t s = hip_stream ? (hipStream_t)hip_stream : h->stream;
   static const bool no_graph = [] {
     const char *e = getenv("RMIMO_NO_GRAPH");
@@ -984,7 +1032,7 @@ int mimo_rx_process_batch(mimo_rx *h, const mimo_batch *b, void *hip_stream) {
     h->g_valid = (rc == MIMO_OK);
   }
   if (rc) return rc;
-  h->last_frames = b->n_frames;
+  h->last_frames = b->n_frames * batch_fpc(b);
   h->last_max_out = b->max_out_syms;
   return MIMO_OK;
 }
@@ -1001,15 +1049,21 @@ int mimo_rx_batch_results(mimo_rx *h, mimo_frame_result *out, uint32_t F) {
   for (uint32_t f = 0; f < F; f++) {
     mimo_frame_result &r = out[f];
     std::memset(&r, 0, sizeof(r));
-    r.status = inf[f].status;
-    r.n_sym = (inf[f].status == 0) ? inf[f].n_sym : 0;
-    r.trigger = inf[f].trigger;
-    r.sync_index = inf[f].sync_index;
-    r.num_samples_processed = inf[f].nsp;
-    r.noise_var = inf[f].noise_var;
+    const FrameInfo &I = inf[f];
+    const bool synced = I.status == MIMO_FRAME_OK || I.status == MIMO_FRAME_INCOMPLETE;
+    const uint64_t o = I.origin;   // positions as the framesync started at origin reports them
+    r.status = I.status;
+    r.n_sym = (I.status == 0) ? I.n_sym : 0;
+    r.trigger = synced ? I.trigger - o : I.trigger;
+    r.sync_index = synced ? I.sync_index - o : 0;
+    r.num_samples_processed = I.nsp;
+    r.noise_var = I.noise_var;
+    r.origin = o;
+    r.capture = I.cap;
+    r.ref_frame = I.ref;
     for (uint32_t s = 0; s < h->N; s++) {
-      r.plateau_start[s] = inf[f].plateau_start[s];
-      r.plateau_end[s] = inf[f].plateau_end[s];
+      r.plateau_start[s] = synced ? I.plateau_start[s] - o : 0;
+      r.plateau_end[s] = synced ? I.plateau_end[s] - o : 0;
       if (inf[f].status == 0) {
         r.evm_num[s] = ev[((size_t)f * h->N + s) * 3 + 0];
         r.evm_den[s] = ev[((size_t)f * h->N + s) * 3 + 1];
@@ -1350,6 +1404,11 @@ int mimo_memcpy_h2d(void *dst, const void *src, size_t bytes, void *s) {
 }
 int mimo_memcpy_d2h(void *dst, const void *src, size_t bytes, void *s) {
   HIPCHK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, (hipStream_t)s));
+  HIPCHK(hipStreamSynchronize((hipStream_t)s));
+  return MIMO_OK;
+}
+int mimo_memcpy_d2d(void *dst, const void *src, size_t bytes, void *s) {
+  HIPCHK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, (hipStream_t)s));
   HIPCHK(hipStreamSynchronize((hipStream_t)s));
   return MIMO_OK;
 }

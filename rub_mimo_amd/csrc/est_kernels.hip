@@ -75,7 +75,7 @@ __global__ __launch_bounds__(kEstT) void search_kernel(SearchArgs a) {
   const int64_t nl = min((int64_t)a.lagc, (int64_t)a.SL - lag0);
   const int64_t ws = (int64_t)a.SL * slot + lag0;   // window index of lag 0 of this segment
   const int64_t abs0 = I.base + ws;
-  const float2 *__restrict__ x = a.iq + ((uint64_t)f * a.N + r) * a.stride;
+  const float2 *__restrict__ x = a.iq + ((uint64_t)I.cap * a.N + r) * a.stride;
   const int64_t L = (int64_t)a.frame_len;
   for (int i = tid; i < F; i += kEstT) {
     const int64_t n = abs0 + i;
@@ -137,7 +137,7 @@ void search_reg_kernel(SearchArgs a) {
   const int64_t ws = (int64_t)a.SL * slot + lag0;   // window index of lag 0 of this segment
   const int64_t abs0 = I.base + ws;
   const int64_t L = (int64_t)a.frame_len;
-  const v2f *__restrict__ x = reinterpret_cast<const v2f *>(a.iq + ((uint64_t)f * a.N + r) * a.stride);
+  const v2f *__restrict__ x = reinterpret_cast<const v2f *>(a.iq + ((uint64_t)I.cap * a.N + r) * a.stride);
   const bool inb = abs0 >= 0 && abs0 + F <= L;
   v2f v[PTS], cs[PTS];
   // unconditional loads from clamped indices, masked afterwards: a per-element "load or zero"
@@ -211,7 +211,7 @@ __global__ __launch_bounds__(T) void ls_kernel(LsArgs a) {
   const uint32_t rt = blockIdx.x / P, grp = blockIdx.x % P;
   const uint32_t r = rt / a.N, t = rt % a.N;
   const int tid = threadIdx.x;
-  const float2 *__restrict__ x = a.iq + ((uint64_t)f * a.N + r) * a.stride;
+  const float2 *__restrict__ x = a.iq + ((uint64_t)I.cap * a.N + r) * a.stride;
   const int64_t L = (int64_t)a.frame_len;
   const uint32_t c0 = grp * CB;
   const uint32_t nb = min((uint32_t)CB, a.nac - c0);

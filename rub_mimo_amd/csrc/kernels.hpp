@@ -60,6 +60,10 @@ struct ScArgs {
   // screened path: chunk geometry and the screen's first/last unproven position per chunk
   uint64_t nchunks;
   const unsigned long long *fmin, *fmax;   // [F][nchunks]
+  // back-to-back streams: every chunk's first candidate ([F][nchunks], ~0 = none) for the
+  // stream walk, and no skipping of chunks past a capture's earliest trigger
+  unsigned long long *cand;
+  int no_skip;
 };
 
 // S&C screen over antenna 0 (sc_screen_kernel): blocks of kScrB positions, kScrSpan positions
@@ -106,11 +110,22 @@ struct PlateauArgs {
   const float2 *iq;
   uint64_t stride, frame_len;
   uint32_t N, M, SL;
-  double thr;
+  double thr, band;
   uint64_t win_len;         // ACB + TX (framing.cc:284-285, 387-388)
   FrameInfo *info;
+  // back-to-back streams (frames_per_capture > 1): info is [capture][fpc] slots
+  uint32_t fpc;
+  uint64_t nchunks;
+  const unsigned long long *cand;          // [capture][nchunks] first candidate per chunk
+  unsigned long long *certfail;            // [capture] bit k: slot k's re-arm certificate failed
+  const uint64_t *ref_starts;              // [capture][ref_stride] transmitted frame starts
+  uint32_t ref_stride;                     // or null
 };
+// one frame per capture: trigger -> run starts, sync index, window
 void launch_plateau(const PlateauArgs &a, uint32_t n_frames, hipStream_t s);
+// back-to-back frames per capture: the re-arm walk over the chunk candidates, the re-arm
+// certificates of frames k >= 1 and the chain fix-up (see sync_kernels.hip)
+void launch_stream_walk(const PlateauArgs &a, uint32_t n_caps, hipStream_t s);
 
 // access-code search, framing.cc:702-744 (est_kernels.hip)
 struct SearchArgs {
@@ -188,6 +203,7 @@ struct DecodeArgs {
   double *evm_part;                // [F][max_out][parts][N][3]
   const float2 *tw;
   uint32_t n_frames;
+  uint32_t n_caps, n_refs;         // captures and reference rows the frames point into
   int all_occ;                     // every subcarrier occupied (j == k): vector stores
   uint32_t n_cu;                   // compute units (persistent grid size)
   unsigned long long *prof;        // diagnostics: [items, load, fft, apply, reduce] cycles

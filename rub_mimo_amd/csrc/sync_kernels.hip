@@ -517,6 +517,7 @@ MIMO_DEV void item_record(const ScArgs &a, uint32_t f, uint64_t chunk, int64_t w
       rec->n_cand = cand;
       rec->pos0 = w0;
       atomicMin(&a.trig[f], cand);
+      if (a.cand) a.cand[(uint64_t)f * a.nchunks + chunk] = cand;
     }
   }
 }
@@ -567,7 +568,7 @@ __global__ __launch_bounds__(kScT) __attribute__((amdgpu_waves_per_eu(2))) void 
 #pragma unroll
     for (int it = 0; it < kScIters; it++) acond[it][tid] = 0xFFFFu;
     __syncthreads();
-    if (c0 >= L || s_trig < (unsigned long long)c0) {  // an earlier trigger exists
+    if (c0 >= L || (!a.no_skip && s_trig < (unsigned long long)c0)) {  // an earlier trigger exists
     SC_PROF(if (a.prof && tid == 0) atomicAdd(&a.prof[6], 1ull);)
       continue;
     }
@@ -917,72 +918,336 @@ __global__ __launch_bounds__(kScT) void sc_finalize_kernel(ScArgs a) {
   }
 }
 
-// run starts (from the trigger chunk's record, exact backward scan where the run began
-// before that chunk's halo), sync index, completeness
-__global__ __launch_bounds__(64) void plateau_kernel(PlateauArgs a) {
-  const uint32_t f = blockIdx.x;
-  const int lane = threadIdx.x;
-  FrameInfo &I = a.info[f];
-  const unsigned long long n = a.trig[f];
-  const int64_t L = (int64_t)a.frame_len;
-  if (n == ~0ull) {
-    if (lane == 0) {
-      I.status = 1;  // MIMO_FRAME_NO_SYNC
-      I.trigger = n;
-      I.nsp = (uint64_t)L;
-      I.n_sym = 0;
-      I.sync_index = 0;
-      I.base = 0;
-    }
-    return;
-  }
-  const ScRecord &rec = a.rec[(uint64_t)f * a.rec_stride + n / a.chunk_len];
-  uint64_t sum = 0;
+// run starts of trigger n on capture cap (its chunk's record rec), none earlier than `floor`:
+// the record's run starts where the chunk saw the run begin, otherwise an exact backward scan
+// (64 positions per step, the oracle's fp32 metric). Returns true when a run reaches below
+// floor > 0, i.e. began before the re-arm point of a stream frame.
+MIMO_DEV bool trigger_run_starts(const PlateauArgs &a, uint32_t cap, const ScRecord &rec,
+                                 int64_t floor, int64_t (&st)[kMaxStreams]) {
+  const int lane = threadIdx.x & 63;
+  bool spans = false;
   for (uint32_t s = 0; s < a.N; s++) {
-    int64_t start = 0;
+    int64_t start = floor;
     if (rec.found & (1u << s)) {
       start = (int64_t)rec.start[s];
     } else {
       // every computed sample of the chunk's range is in the run: walk back exactly
-      const float2 *__restrict__ x = a.iq + ((uint64_t)f * a.N + s) * a.stride;
-      start = 0;
-      for (int64_t q0 = (int64_t)rec.start[s] - 1; q0 >= 0; q0 -= 64) {
+      const float2 *__restrict__ x = a.iq + ((uint64_t)cap * a.N + s) * a.stride;
+      bool hit = false;
+      for (int64_t q0 = (int64_t)rec.start[s] - 1; q0 >= floor; q0 -= 64) {
         const int64_t q = q0 - lane;
-        bool zero = true;
-        if (q >= 0) {
-          const float y = sc_exact(x, q, a.M);
-          zero = !((double)y > a.thr);
-        } else {
-          zero = false;
-        }
+        bool zero = false;
+        if (q >= floor) zero = !((double)sc_exact(x, q, a.M) > a.thr);
         const unsigned long long bal = __ballot(zero);
         if (bal) {
           const int l = __ffsll((long long)bal) - 1;   // lowest lane = highest position
           start = q0 - l + 1;
+          hit = true;
           break;
         }
       }
+      if (!hit && floor > 0) spans = true;
     }
-    if (lane == 0) {
-      I.plateau_start[s] = (uint64_t)start;
-      I.plateau_end[s] = n;
+    if (start < floor) {
+      start = floor;
+      spans = true;
     }
-    sum += (uint64_t)start;
+    st[s] = start;
+  }
+  return spans;
+}
+
+// A framesync started at capture sample `origin` that triggers at n with run starts st
+// (framing.cc:612-623): sync index, window base, completeness and num_samples_processed, all
+// relative to origin as that framesync counts them; FrameInfo keeps absolute positions.
+// Uniform on every lane; lane 0 writes. Returns the status.
+MIMO_DEV int frame_from_trigger(const PlateauArgs &a, FrameInfo &I, uint32_t cap, uint32_t ref,
+                                int64_t origin, int64_t n, const int64_t (&st)[kMaxStreams],
+                                bool need_base_in_view, uint64_t &nsp_rel) {
+  const int lane = threadIdx.x & 63;
+  const int64_t L_rel = (int64_t)a.frame_len - origin;
+  uint64_t sum = 0;
+  for (uint32_t s = 0; s < a.N; s++) sum += (uint64_t)(st[s] - origin);
+  const int64_t sync_rel = (int64_t)(sum / a.N);           // framing.cc:618-620
+  const int64_t base_rel = sync_rel - (int64_t)a.SL;       // window start
+  const int64_t n_e = base_rel + (int64_t)a.win_len;       // estimate_channel runs at this sample
+  int status;
+  if (need_base_in_view && base_rel < 0) {
+    // the fresh framesync's window would hold zeros before the re-arm point, the capture
+    // holds real samples there: resume this frame as a fresh capture instead
+    status = 3;   // MIMO_FRAME_RESCAN
+    nsp_rel = 0;
+  } else if (n_e < L_rel) {
+    status = 0;
+    nsp_rel = (uint64_t)((n_e + 1 < L_rel) ? n_e + 2 : n_e + 1);
+  } else {
+    status = 2;   // MIMO_FRAME_INCOMPLETE: still saving access codes
+    nsp_rel = (uint64_t)L_rel;
   }
   if (lane == 0) {
-    const uint64_t sync = sum / a.N;                 // framing.cc:618-620
-    const int64_t base = (int64_t)sync - a.SL;       // window start
-    const int64_t n_e = base + (int64_t)a.win_len;   // estimate_channel runs at this sample
-    I.trigger = n;
-    I.sync_index = sync;
-    I.base = base;
-    if (n_e < L) {
-      I.status = 0;
-      I.nsp = (uint64_t)((n_e + 1 < L) ? n_e + 2 : n_e + 1);
-    } else {
-      I.status = 2;  // MIMO_FRAME_INCOMPLETE: still saving access codes
-      I.nsp = (uint64_t)L;
+    I.status = status;
+    I.trigger = (uint64_t)n;
+    I.sync_index = (uint64_t)(origin + sync_rel);
+    I.base = origin + base_rel;
+    I.nsp = nsp_rel;
+    I.origin = (uint64_t)origin;
+    I.cap = cap;
+    I.ref = ref;
+    if (status != 0) I.n_sym = 0;
+    for (uint32_t s = 0; s < a.N; s++) {
+      I.plateau_start[s] = (uint64_t)st[s];
+      I.plateau_end[s] = (uint64_t)n;
+    }
+  }
+  return status;
+}
+
+// The plateau rule run exactly from a re-arm point: positions [r, end) of every antenna, 64
+// at a time (the oracle's fp32 metric per lane), then the per-sample state machine of
+// framing.cc:601-623 over the ballots with in_plateau false at r. For chunks whose recorded
+// (first) candidate precedes r -- frames shorter than a chunk -- so its cost is bounded by a
+// chunk of small-M work. Returns the trigger (-1: none before end) and the run starts.
+MIMO_DEV int64_t forward_trigger(const PlateauArgs &a, uint32_t cap, int64_t r, int64_t end,
+                                 int64_t (&st)[kMaxStreams]) {
+  const int lane = threadIdx.x & 63;
+  int64_t ps[kMaxStreams], pe[kMaxStreams];
+  bool in[kMaxStreams];
+  for (uint32_t s = 0; s < a.N; s++) { ps[s] = pe[s] = r; in[s] = false; }
+  for (int64_t q0 = r; q0 < end; q0 += 64) {
+    unsigned long long bal[kMaxStreams];
+    for (uint32_t s = 0; s < a.N; s++) {
+      const float2 *__restrict__ x = a.iq + ((uint64_t)cap * a.N + s) * a.stride;
+      const int64_t q = q0 + lane;
+      const bool b = q < end && (double)sc_exact(x, q, a.M) > a.thr;
+      bal[s] = __ballot(b);
+    }
+    const int cnt = (int)((end - q0) < 64 ? (end - q0) : 64);
+    for (int i = 0; i < cnt; i++) {
+      const int64_t n = q0 + i;
+      bool proceed = true;
+      for (uint32_t s = 0; s < a.N; s++) {
+        if ((bal[s] >> i) & 1ull) {
+          if (in[s]) pe[s] = n;
+          else { in[s] = true; ps[s] = n; pe[s] = n; }
+        } else {
+          in[s] = false;
+        }
+        proceed = proceed && in[s] && (pe[s] - ps[s] > (int64_t)(a.SL - a.M));   // > cp_len
+      }
+      if (proceed) {
+        for (uint32_t s = 0; s < a.N; s++) st[s] = ps[s];
+        return n;
+      }
+    }
+  }
+  return -1;
+}
+
+MIMO_DEV void frame_empty(FrameInfo &I, int status, uint32_t cap, uint32_t ref, int64_t origin,
+                          uint64_t nsp_rel) {
+  I.status = status;
+  I.trigger = ~0ull;
+  I.nsp = nsp_rel;
+  I.n_sym = 0;
+  I.sync_index = 0;
+  I.base = 0;
+  I.origin = (uint64_t)origin;
+  I.cap = cap;
+  I.ref = ref;
+}
+
+// one frame per capture: run starts (from the trigger chunk's record, exact backward scan
+// where the run began before that chunk's halo), sync index, completeness
+__global__ __launch_bounds__(64) void plateau_kernel(PlateauArgs a) {
+  const uint32_t f = blockIdx.x;
+  FrameInfo &I = a.info[f];
+  const unsigned long long n = a.trig[f];
+  if (n == ~0ull) {
+    if (threadIdx.x == 0) frame_empty(I, 1, f, f, 0, a.frame_len);   // MIMO_FRAME_NO_SYNC
+    return;
+  }
+  const ScRecord &rec = a.rec[(uint64_t)f * a.rec_stride + n / a.chunk_len];
+  int64_t st[kMaxStreams];
+  (void)trigger_run_starts(a, f, rec, 0, st);
+  uint64_t nsp;
+  (void)frame_from_trigger(a, I, f, f, 0, (int64_t)n, st, false, nsp);
+}
+
+// ---- back-to-back frames in one capture (stream re-arm) ------------------------------------
+// The reference's framesync stops at STATE_MIMO (framing.cc:494-496) and reset() only rewinds
+// the state (:461-464). A stream of frames is received here as a caller of that API would:
+// after a frame, a fresh framesync takes the remaining samples, starting at origin
+// r_{k+1} = r_k + get_num_samples_processed(). Frame k's S&C therefore runs with zero filter
+// history before r_k. The S&C kernels compute the metric with the capture's real history; the
+// two agree at every n >= r_k + M - 1, and the walk takes frame k's trigger as the first chunk
+// candidate at or after r_k. That is exact when, over Z_k = [r_k, r_k + M - 1), neither metric
+// has a sample above the threshold on any antenna -- then every run counted after r_k starts
+// past Z_k in both. stream_cert_kernel proves that per (frame, antenna) in fp64 with a margin
+// over the fp32 error band; a frame it cannot prove, or one whose run or window reaches
+// before r_k, is reported MIMO_FRAME_RESCAN (the caller resumes that capture at r_k as a
+// fresh capture) and the slots after it MIMO_FRAME_NONE.
+__global__ __launch_bounds__(64) void stream_walk_kernel(PlateauArgs a) {
+  const uint32_t cap = blockIdx.x;
+  const int lane = threadIdx.x;
+  const int64_t K = (int64_t)a.chunk_len;
+  const unsigned long long *cand = a.cand + (uint64_t)cap * a.nchunks;
+  FrameInfo *slot = a.info + (uint64_t)cap * a.fpc;
+  const uint64_t *rs = a.ref_starts ? a.ref_starts + (uint64_t)cap * a.ref_stride : nullptr;
+  int64_t r = 0;
+  uint32_t k = 0;
+  while (k < a.fpc) {
+    FrameInfo &I = slot[k];
+    const uint32_t ref_slot = cap * a.fpc + k;
+    int64_t st[kMaxStreams];
+    int64_t n = -1;
+    uint64_t c_from = (uint64_t)(r / K);
+    if (c_from < a.nchunks && cand[c_from] != ~0ull && (int64_t)cand[c_from] < r) {
+      // chunk(r) recorded an earlier trigger (several frames per chunk): exact scan of the
+      // rest of that chunk, then the recorded candidates of the chunks after it
+      n = forward_trigger(a, cap, r, std::min<int64_t>((int64_t)(c_from + 1) * K,
+                                                       (int64_t)a.frame_len), st);
+      c_from++;
+    }
+    uint64_t cf = ~0ull;                   // first chunk at or after c_from with a candidate
+    for (uint64_t c0 = n >= 0 ? a.nchunks : c_from; c0 < a.nchunks; c0 += 64) {
+      const uint64_t c = c0 + lane;
+      const unsigned long long b = __ballot(c < a.nchunks && cand[c] != ~0ull);
+      if (b) {
+        cf = c0 + __ffsll((long long)b) - 1;
+        break;
+      }
+    }
+    if (n < 0 && cf == ~0ull) {            // no trigger in the rest of the capture
+      if (lane == 0) frame_empty(I, 1, cap, ref_slot, r, a.frame_len - r);
+      k++;
+      break;
+    }
+    bool spans = false;
+    if (n < 0) {
+      n = (int64_t)cand[cf];
+      spans = trigger_run_starts(a, cap, a.rec[(uint64_t)cap * a.rec_stride + cf], r, st);
+    }
+    if (spans) {
+      if (lane == 0) frame_empty(I, 3, cap, ref_slot, r, 0);
+      k++;
+      break;
+    }
+    // transmitted frame holding this sync index (reference rows for the EVM)
+    uint32_t ref = ref_slot;
+    if (rs) {
+      uint64_t sum = 0;
+      for (uint32_t s = 0; s < a.N; s++) sum += (uint64_t)(st[s] - r);
+      const uint64_t sync_abs = (uint64_t)r + sum / a.N;
+      uint32_t j = 0;
+      while (j + 1 < a.ref_stride && rs[j + 1] != ~0ull && rs[j + 1] <= sync_abs) j++;
+      ref = cap * a.ref_stride + j;
+    }
+    uint64_t nsp_rel = 0;
+    const int status = frame_from_trigger(a, I, cap, ref, r, n, st, k > 0, nsp_rel);
+    k++;
+    if (status != 0) break;
+    r += (int64_t)nsp_rel;
+  }
+  for (uint32_t kk = k + lane; kk < a.fpc; kk += 64)
+    frame_empty(slot[kk], 4, cap, cap * a.fpc + kk, r, 0);   // MIMO_FRAME_NONE
+}
+
+// Re-arm certificate of slot k >= 1 on antenna s: over n in Z = [r, r + M - 1) both the
+// capture-history metric (P over the M/2 products ending at n, R over the last M samples)
+// and the fresh framesync's metric (samples before r read as zero: P sums products m >=
+// r + M/2, R samples m >= r) stay clearly below the threshold. Running fp64 sums per thread
+// segment, seeded by one block scan of the segments' differences (as sc_exact_kernel).
+__global__ __launch_bounds__(kScT) void stream_cert_kernel(PlateauArgs a) {
+  __shared__ double ws[2][6][kScT / 64];
+  __shared__ int s_fail;
+  const uint32_t k = blockIdx.x + 1, s = blockIdx.y, cap = blockIdx.z;
+  const FrameInfo &I = a.info[(uint64_t)cap * a.fpc + k];
+  if (I.status != 0 && I.status != 2) return;
+  const int tid = threadIdx.x;
+  const int64_t M = a.M, M2 = M / 2, r = (int64_t)I.origin;
+  const int64_t L = (int64_t)a.frame_len;
+  const float2 *__restrict__ x = a.iq + ((uint64_t)cap * a.N + s) * a.stride;
+  auto ld = [&](int64_t q) { return (q >= 0 && q < L) ? x[q] : make_float2(0.0f, 0.0f); };
+  if (tid == 0) s_fail = 0;
+  // capture-history sums ending at r - 1 and the region's energy (the cancellation guard)
+  double c[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0}, tot[6];
+  for (int64_t i = tid; i < M; i += kScT) {
+    const int64_t m = r - M + i;
+    const float2 v = ld(m);
+    const float z = v.x * v.x + v.y * v.y;
+    c[2] += (double)z;
+    if (i >= M2) {
+      const float2 pp = cj_mul(ld(m - M2), v);
+      c[0] += (double)pp.x;
+      c[1] += (double)pp.y;
+    }
+    const float2 w = ld(r + i);
+    c[3] += (double)(w.x * w.x + w.y * w.y);
+  }
+  block_scan<6>(c, tot, ws[0]);
+  const double Pc0r = tot[0], Pc0i = tot[1], Zc0 = tot[2];
+  const double E = tot[2] + tot[3];
+  // this thread's positions n = r + j, j in [j0, j1)
+  const int64_t G = (M - 1 + kScT - 1) / kScT;
+  const int64_t j0 = std::min<int64_t>(M - 1, tid * G), j1 = std::min<int64_t>(M - 1, j0 + G);
+  double d[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+  for (int64_t j = j0; j < j1; j++) {
+    const int64_t n = r + j;
+    const float2 vn = ld(n), vh = ld(n - M2), vm = ld(n - M);
+    const float2 pn = cj_mul(vh, vn), pl = cj_mul(ld(n - M), vh);
+    const float zn = vn.x * vn.x + vn.y * vn.y, zl = vm.x * vm.x + vm.y * vm.y;
+    d[0] += (double)pn.x - (double)pl.x;
+    d[1] += (double)pn.y - (double)pl.y;
+    d[2] += (double)zn - (double)zl;
+    if (j >= M2) { d[3] += (double)pn.x; d[4] += (double)pn.y; }
+    d[5] += (double)zn;
+  }
+  block_scan<6>(d, tot, ws[1]);
+  double Pcr = Pc0r + d[0], Pci = Pc0i + d[1], Zc = Zc0 + d[2];
+  double Pfr = d[3], Pfi = d[4], Zf = d[5];
+  const double lim = a.thr - 2.0 * a.band - 1e-3;
+  auto fails = [&](double pr, double pi, double z) {
+    const double R = 0.5 * z;
+    if (E == 0.0) return false;                 // all-zero region: y is 0/0 (false) throughout
+    if (R < 1e-9 * E) return true;              // too close to cancellation to certify
+    return pr * pr + pi * pi > lim * R * R;
+  };
+  bool bad = false;
+  for (int64_t j = j0; j < j1; j++) {
+    const int64_t n = r + j;
+    const float2 vn = ld(n), vh = ld(n - M2), vm = ld(n - M);
+    const float2 pn = cj_mul(vh, vn), pl = cj_mul(vm, vh);
+    const float zn = vn.x * vn.x + vn.y * vn.y, zl = vm.x * vm.x + vm.y * vm.y;
+    Pcr += (double)pn.x - (double)pl.x;
+    Pci += (double)pn.y - (double)pl.y;
+    Zc += (double)zn - (double)zl;
+    if (j >= M2) { Pfr += (double)pn.x; Pfi += (double)pn.y; }
+    Zf += (double)zn;
+    bad = bad || fails(Pcr, Pci, Zc) || fails(Pfr, Pfi, Zf);
+  }
+  if (bad) s_fail = 1;
+  __syncthreads();
+  if (tid == 0 && s_fail) atomicOr(&a.certfail[cap], 1ull << k);
+}
+
+// the first uncertified slot of each capture becomes RESCAN (resume at its origin), the
+// slots after it NONE
+__global__ __launch_bounds__(64) void stream_fixup_kernel(PlateauArgs a) {
+  const uint32_t cap = blockIdx.x;
+  const unsigned long long m = a.certfail[cap];
+  if (!m) return;
+  const uint32_t k0 = (uint32_t)(__ffsll((long long)m) - 1);
+  FrameInfo *slot = a.info + (uint64_t)cap * a.fpc;
+  for (uint32_t k = k0 + threadIdx.x; k < a.fpc; k += 64) {
+    FrameInfo &I = slot[k];
+    if (k == k0) {
+      I.status = 3;
       I.n_sym = 0;
+      I.nsp = 0;
+    } else {
+      I.status = 4;
+      I.n_sym = 0;
+      I.nsp = 0;
     }
   }
 }
@@ -1415,6 +1680,14 @@ void launch_sc_exact(const ScArgs &a, hipStream_t s) {
 
 void launch_plateau(const PlateauArgs &a, uint32_t n_frames, hipStream_t s) {
   hipLaunchKernelGGL(plateau_kernel, dim3(n_frames), dim3(64), 0, s, a);
+}
+
+void launch_stream_walk(const PlateauArgs &a, uint32_t n_caps, hipStream_t s) {
+  hipLaunchKernelGGL(stream_walk_kernel, dim3(n_caps), dim3(64), 0, s, a);
+  if (a.fpc > 1) {
+    hipLaunchKernelGGL(stream_cert_kernel, dim3(a.fpc - 1, a.N, n_caps), dim3(kScT), 0, s, a);
+    hipLaunchKernelGGL(stream_fixup_kernel, dim3(n_caps), dim3(64), 0, s, a);
+  }
 }
 
 }  // namespace mimo

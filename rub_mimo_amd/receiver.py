@@ -68,7 +68,10 @@ def _ptr(x):
     raise TypeError("expected a device pointer")
 
 
-SC16_SCALE = 1.0 / 32768.0     # int16 full scale -> [-1, 1); the caller may pass UHD's own
+# UHD's sc16 -> fc32 host conversion scales by 1/32767 (so +32767 maps to 1.0): the reference's
+# rx worker receives fc32 produced that way from the sc16 wire (mimo/config.h:51-52,
+# mimo/main.cc:837-848), so that is the default here. Callers may pass another scale.
+SC16_SCALE = 1.0 / 32767.0
 
 
 def ingest_sc16(src, src_stride, dst, dst_stride, n_arrays, n, scale=SC16_SCALE, stream=None):
@@ -117,13 +120,97 @@ class Receiver:
             self._h = None
 
     def process(self, iq, stride, frame_len, n_frames, max_out=None, out_sym=None, out_idx=None,
-                ref_mode=0, ref_idx=None, ref_seed=0, frame_id0=0, stream=None):
+                ref_mode=0, ref_idx=None, ref_seed=0, frame_id0=0, stream=None,
+                frames_per_capture=1, ref_starts=None, ref_stride=0):
+        """One batch (mimo_rx_process_batch). frames_per_capture > 1: every capture is a
+        stream of back-to-back frames, received as fresh framesyncs re-armed after each frame
+        (frame slots [capture][frames_per_capture]; see include/mimo_rx.h)."""
         P = self.params
         b = _lib.Batch(_ptr(iq), stride, frame_len, n_frames,
                        P.pid_max if max_out is None else max_out, _ptr(out_sym), _ptr(out_idx),
-                       ref_mode, _ptr(ref_idx), ref_seed, frame_id0)
+                       ref_mode, _ptr(ref_idx), ref_seed, frame_id0, frames_per_capture,
+                       ref_stride, _ptr(ref_starts))
         check(lib().mimo_rx_process_batch(self._h, C.byref(b), stream), "process_batch")
-        self._last = n_frames
+        self._last = n_frames * max(1, frames_per_capture)
+
+    def receive_streams(self, iq, stride, frame_len, n_caps, frames_per_capture, max_out=None,
+                        out_sym=None, out_idx=None, ref_mode=0, ref_idx=None, ref_seed=0,
+                        frame_id0=0, ref_starts=None, stream=None):
+        """Back-to-back frames in n_caps captures (process with frames_per_capture), then
+        every capture whose chain stopped at a MIMO_FRAME_RESCAN frame is resumed at that
+        frame's origin as a fresh capture, into the same frame slots, until none is left.
+        ref_starts: host uint64 array [n_caps][frames_per_capture] (see mimo_batch), uploaded
+        here. Returns the per-slot result dicts ([capture][k] order, origins absolute)."""
+        import torch
+        P = self.params
+        K = frames_per_capture
+        mo = P.pid_max if max_out is None else max_out
+        N, mocc = P.num_streams, self.M_occ
+        dev_rs = None
+        rs_host = None
+        if ref_starts is not None:
+            rs_host = np.ascontiguousarray(ref_starts, np.uint64).reshape(n_caps, K)
+            dev_rs = torch.from_numpy(rs_host.view(np.int64).copy()).cuda()
+        self.process(iq, stride, frame_len, n_caps, max_out=mo, out_sym=out_sym, out_idx=out_idx,
+                     ref_mode=ref_mode, ref_idx=ref_idx, ref_seed=ref_seed, frame_id0=frame_id0,
+                     stream=stream, frames_per_capture=K, ref_starts=dev_rs)
+        res = self.results(n_caps * K)
+        base = _ptr(iq)
+        slot_sym = N * mo * mocc * 8
+        slot_idx = N * mo * mocc
+        for c in range(n_caps):
+            while True:
+                ks = [k for k in range(K) if res[c * K + k]["status"] == _lib.FRAME_RESCAN]
+                if not ks:
+                    break
+                k0 = ks[0]
+                org = res[c * K + k0]["origin"]
+                rem = K - k0
+                rs = None
+                if rs_host is not None:
+                    sh = rs_host[c].astype(np.int64) - org
+                    sh = np.where(rs_host[c] == np.uint64(2 ** 64 - 1), -1, np.maximum(sh, 0))
+                    rs = torch.from_numpy(sh.astype(np.int64)).cuda()
+                    fid0 = frame_id0 + c * K
+                    refp = None if ref_idx is None else _ptr(ref_idx) + c * K * slot_idx
+                else:
+                    fid0 = frame_id0 + c * K + k0
+                    refp = None if ref_idx is None else _ptr(ref_idx) + (c * K + k0) * slot_idx
+                sl = c * K + k0
+                # the resumed call runs in stream mode with at least two slots; a lone last
+                # slot decodes into scratch and is copied into place
+                osym = None if out_sym is None else _ptr(out_sym) + sl * slot_sym
+                oidx = None if out_idx is None else _ptr(out_idx) + sl * slot_idx
+                scratch = None
+                if rem == 1 and (osym or oidx):
+                    scratch = torch.empty(2 * (slot_sym + slot_idx), dtype=torch.uint8,
+                                          device="cuda")
+                    dsym = scratch.data_ptr() if osym else None
+                    didx = scratch.data_ptr() + 2 * slot_sym if oidx else None
+                else:
+                    dsym, didx = osym, oidx
+                self.process(base + ((c * N) * stride + org) * 8, stride, frame_len - org, 1,
+                             max_out=mo, out_sym=dsym, out_idx=didx, ref_mode=ref_mode,
+                             ref_idx=refp, ref_seed=ref_seed, frame_id0=fid0, stream=stream,
+                             frames_per_capture=max(rem, 2), ref_starts=rs,
+                             ref_stride=K if rs is not None else 0)
+                if scratch is not None:
+                    torch.cuda.synchronize()
+                    if osym:
+                        _lib.memcpy_d2d(osym, dsym, slot_sym)
+                    if oidx:
+                        _lib.memcpy_d2d(oidx, didx, slot_idx)
+                sub_res = self.results(max(rem, 2))
+                for k, r in enumerate(sub_res[:rem]):
+                    r = dict(r)
+                    r["origin"] += org
+                    r["capture"] = c
+                    if rs_host is not None or r["status"] == _lib.FRAME_OK:
+                        r["ref_frame"] = (c * K + r["ref_frame"]) if rs_host is not None \
+                            else (c * K + k0 + k)
+                    res[sl + k] = r
+        self._last = n_caps * K
+        return res
 
     def results(self, n_frames=None):
         n = self._last if n_frames is None else n_frames
@@ -137,7 +224,8 @@ class Receiver:
                 num_samples_processed=r.num_samples_processed,
                 plateau_start=list(r.plateau_start)[:N], plateau_end=list(r.plateau_end)[:N],
                 noise_var=r.noise_var, evm_num=np.array(r.evm_num[:N]),
-                evm_den=np.array(r.evm_den[:N]), errors=np.array(r.errors[:N], np.int64)))
+                evm_den=np.array(r.evm_den[:N]), errors=np.array(r.errors[:N], np.int64),
+                origin=r.origin, capture=r.capture, ref_frame=r.ref_frame))
         return out
 
     def corr(self, n_frames=None):

@@ -68,7 +68,72 @@ def make_case(name, M, cp, N, nac, pid, qam, det, seed, sct, snr, bias):
     return rec
 
 
+STREAM_CASES = [
+    # name, M, cp, N, nac, pid, qam, detector, seed, frames, snr, lead_cut (frame -> samples
+    # removed from its lead: a frame whose S0 follows the previous window end too closely)
+    ("m64_2x2_stream", 64, 16, 2, 4, 8, 16, "zf2", 11, 4, 30.0, {}),
+    ("m64_2x2_stream_rescan", 64, 16, 2, 4, 8, 16, "zf2", 11, 3, 30.0, {2: 735}),
+]
+
+
+def make_stream_case(name, M, cp, N, nac, pid, qam, det, seed, frames, snr, lead_cut):
+    """Back-to-back frames in one capture (frames 0..frames-1 of the synthesiser, optionally
+    with part of a frame's lead removed), received by the oracle's fresh-framesync-per-frame
+    stream driver (oracle/ref.py stream_ref) and accepted after the numpy model's own
+    stream driver agrees frame by frame."""
+    p = ref.default_sctype(M)
+    parts, txs, starts = [], [], []
+    pos = 0
+    for f in range(frames):
+        rx, tx_idx, _ = ref.synth_frame(M, cp, N, nac, pid, qam, seed=seed, frame=f, offset=-1,
+                                        snr_db=snr, p=p)
+        cut = lead_cut.get(f, 0)
+        rx = rx[:, cut:]
+        starts.append(pos)
+        pos += rx.shape[1]
+        parts.append(rx)
+        txs.append(tx_idx)
+    rx = np.concatenate(parts, axis=1)
+    recs = ref.stream_ref(rx, M, cp, N, nac, pid_max=pid, detector=DETS[det], p=p)
+    ok = [r for r in recs if r["state"] == ref.STATE_MIMO]
+    assert len(ok) >= 2, (name, len(ok))
+    s0b, s1b = ref.code_bits(M, N, nac, codes.s1_polynomials(N))
+    nmo = nm.receive_stream(rx, M, cp, N, nac, pid, s0b, s1b, p=p, detector=det)
+    assert len(nmo) == len(ok), name
+    for r, (org, d) in zip(ok, nmo):
+        assert r["origin"] == org and r["sync_index"] == d["sync_index"], name
+        assert list(r["plateau_start"]) == list(d["plateau_start"]), name
+        assert r["num_samples_processed"] == d["num_samples_processed"], name
+        assert (r["corr_idx"] == d["corr_idx"]).all(), name
+        scale = np.abs(d["symbols"]).max()
+        assert np.abs(d["symbols"] - r["symbols"]).max() / scale < 1e-5, name
+    K = len(ok)
+    # transmitted frame of each decoded frame (sync index inside that frame's span)
+    fidx = np.array([int(np.searchsorted(starts, r["origin"] + r["sync_index"], "right")) - 1
+                     for r in ok], np.int64)
+    return dict(
+        M=M, cp=cp, N=N, nac=nac, pid=pid, qam=qam, detector=DETS[det], seed=seed, p=p, rx=rx,
+        frame_starts=np.array(starts, np.uint64), tx_idx=np.stack(txs),
+        n_ok=K, origin=np.array([r["origin"] for r in ok], np.int64),
+        sync_index=np.array([r["sync_index"] for r in ok], np.int64),
+        plateau_start=np.array([r["plateau_start"] for r in ok], np.int64),
+        plateau_end=np.array([r["plateau_end"] for r in ok], np.int64),
+        num_samples_processed=np.array([r["num_samples_processed"] for r in ok], np.int64),
+        corr_idx=np.stack([r["corr_idx"] for r in ok]), symbols=np.stack([r["symbols"] for r in ok]),
+        tx_frame=fidx, tail_state=recs[-1]["state"], tail_origin=recs[-1]["origin"],
+        tail_nsp=recs[-1]["num_samples_processed"])
+
+
 def main():
+    for case in STREAM_CASES:
+        rec = make_stream_case(*case)
+        path = os.path.join(HERE, case[0] + ".npz")
+        np.savez_compressed(path, **rec)
+        print("wrote", path, os.path.getsize(path), "bytes; frames", rec["n_ok"], "origins",
+              list(rec["origin"]), "syncs", list(rec["sync_index"]), "tx frames",
+              list(rec["tx_frame"]))
+    if len(sys.argv) > 1 and sys.argv[1] == "streams":
+        return
     for case in CASES:
         rec = make_case(*case)
         path = os.path.join(HERE, case[0] + ".npz")

@@ -97,10 +97,26 @@ def test_invert2_matches_oracle():
         assert np.array_equal(W, Wr) and g == gr
 
 
-def test_struct_layouts():
-    assert C.sizeof(_lib.FrameResult) == 4 + 4 + 8 * 3 + 8 * 8 * 2 + 4 + 4 + 8 * 8 * 3
-    assert C.sizeof(_lib.Batch) == 8 * 3 + 4 * 2 + 8 * 2 + 8 + 8 * 3
-    assert _lib.RxConfig.plateau_threshold.offset % 8 == 0
+def test_struct_layouts(tmp_path):
+    """Every ctypes mirror matches the C header field for field (offsets and sizes from a
+    compiled probe of include/mimo_rx.h)."""
+    structs = {"mimo_frame_result": _lib.FrameResult, "mimo_batch": _lib.Batch,
+               "mimo_rx_config": _lib.RxConfig, "mimo_synth_config": _lib.SynthConfig}
+    lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "mimo_rx.h"', 'int main(void) {']
+    for cname, py in structs.items():
+        lines.append('printf("%s %%zu\\n", sizeof(%s));' % (cname, cname))
+        for fname, _ in py._fields_:
+            lines.append('printf("%s.%s %%zu\\n", offsetof(%s, %s));' % (cname, fname, cname, fname))
+    lines.append("return 0; }")
+    src = tmp_path / "probe.c"
+    src.write_text("\n".join(lines))
+    exe = tmp_path / "probe"
+    subprocess.check_call(["gcc", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)])
+    got = dict(l.split() for l in subprocess.check_output([str(exe)]).decode().splitlines())
+    for cname, py in structs.items():
+        assert int(got[cname]) == C.sizeof(py), cname
+        for fname, _ in py._fields_:
+            assert int(got["%s.%s" % (cname, fname)]) == getattr(py, fname).offset, (cname, fname)
 
 
 def test_error_path_without_gpu_is_loud():

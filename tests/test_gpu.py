@@ -16,6 +16,8 @@ from rub_mimo_amd.receiver import Receiver, RxParams, Synthesizer, SynthParams
 pytestmark = pytest.mark.gpu
 
 GOLDEN = sorted(glob.glob(os.path.join(os.path.dirname(__file__), "golden", "m[0-9]*.npz")))
+GOLDEN = [g for g in GOLDEN if "_stream" not in os.path.basename(g)]
+STREAMS = sorted(glob.glob(os.path.join(os.path.dirname(__file__), "golden", "m*_stream*.npz")))
 SYM_TOL = 1e-4        # sqrt(sum|y_gpu - y_cpu|^2 / sum|y_cpu|^2)
 EVM_DB_TOL = 1e-3
 

@@ -9,6 +9,8 @@ import pytest
 from oracle import codes, numpy_model as nm, ref
 
 GOLDEN = sorted(glob.glob(os.path.join(os.path.dirname(__file__), "golden", "m[0-9]*.npz")))
+GOLDEN = [g for g in GOLDEN if "_stream" not in os.path.basename(g)]
+STREAMS = sorted(glob.glob(os.path.join(os.path.dirname(__file__), "golden", "m*_stream*.npz")))
 
 
 def load(path):
@@ -257,3 +259,39 @@ def test_faded_link_search_is_junk_in_reference_too(golden_dir):
         ac = k + 1 if abs(d[r, k]) > SL else k
         t = ac % int(g["N"])
         assert H2[r, t] < 0.05
+
+
+@pytest.mark.parametrize("path", STREAMS, ids=[os.path.basename(p) for p in STREAMS])
+def test_stream_oracle_matches_golden(path):
+    """Back-to-back frames: the oracle's fresh-framesync-per-frame driver reproduces the
+    fixture (origins, sync indices, plateau starts, samples processed, corr indices, symbols),
+    and the origins chain through num_samples_processed (framing.cc:471-506)."""
+    g = load(path)
+    N, K = int(g["N"]), int(g["n_ok"])
+    recs = ref.stream_ref(g["rx"], int(g["M"]), int(g["cp"]), N, int(g["nac"]),
+                          pid_max=int(g["pid"]), detector=int(g["detector"]), p=g["p"])
+    ok = [r for r in recs if r["state"] == ref.STATE_MIMO]
+    assert len(ok) == K
+    for k, r in enumerate(ok):
+        assert r["origin"] == g["origin"][k]
+        assert r["sync_index"] == g["sync_index"][k]
+        assert list(r["plateau_start"]) == list(g["plateau_start"][k])
+        assert r["num_samples_processed"] == g["num_samples_processed"][k]
+        assert (r["corr_idx"] == g["corr_idx"][k]).all()
+        assert np.array_equal(r["symbols"], g["symbols"][k])
+        if k + 1 < K:
+            assert g["origin"][k + 1] == g["origin"][k] + g["num_samples_processed"][k]
+    assert recs[-1]["state"] == int(g["tail_state"])
+    # every decoded frame is a distinct transmitted frame, in order
+    assert list(g["tx_frame"]) == sorted(set(int(v) for v in g["tx_frame"]))
+
+
+def test_stream_numpy_model_agrees():
+    """The independent numpy model's stream driver finds the same frames at the same origins."""
+    g = load(STREAMS[0])
+    M, N, nac = int(g["M"]), int(g["N"]), int(g["nac"])
+    s0b, s1b = ref.code_bits(M, N, nac, codes.s1_polynomials(N))
+    out = nm.receive_stream(g["rx"], M, int(g["cp"]), N, nac, int(g["pid"]), s0b, s1b, p=g["p"],
+                            detector="zf2")
+    assert [o for o, _ in out] == list(g["origin"])
+    assert [d["sync_index"] for _, d in out] == list(g["sync_index"])
