@@ -10,6 +10,7 @@
 #include <math.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 
 /* ====================================================================================
  * liquid msequence (used at mimo/main.cc:1268-1270, framing.cc:1075, 1240)
@@ -112,7 +113,7 @@ typedef struct {
 } fft_plan;
 
 #define FFT_PLAN_CACHE 16
-static fft_plan *g_plans[FFT_PLAN_CACHE];
+static __thread fft_plan *g_plans[FFT_PLAN_CACHE]; /* per thread: plans own work buffers */
 
 static fft_plan *fft_get_plan(uint32_t n) {
   for (int i = 0; i < FFT_PLAN_CACHE; i++)
@@ -572,7 +573,15 @@ struct ref_framesync {
   /* trace */
   float *trace; uint64_t trace_len, trace_cap;
   float *ctrace, *s0trace;
+  /* CPU-baseline phase clocks (wall seconds), see ref_framesync_get_phase_times */
+  double t_phase[4];
 };
+
+static double wall_now(void) {
+  struct timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  return (double)ts.tv_sec + 1e-9 * (double)ts.tv_nsec;
+}
 
 static int is_occ(const ref_framesync *fs, uint32_t sc) { return fs->p[sc] != REF_SC_NULL; }
 
@@ -833,6 +842,62 @@ static void solve_weights(uint32_t N, const ref_cf32 *G, ref_cf32 *W, int mmse, 
   for (uint32_t i = 0; i < N * N; i++) { W[i].re = (float)B[i].re; W[i].im = (float)B[i].im; }
 }
 
+/* Parseval variant of the access-code search (CPU-baseline mode, not the reference's loop).
+ * The brute-force metric at lag i is |sum_k FFT(x[i..i+M))[k] conj(C[k])|^2 / M^2 with C the
+ * code spectrum; by Parseval (unnormalised DFT) that sum is M sum_n x[i+n] conj(c[n]) with
+ * c = IDFT(C)/M, the time-domain code. One overlap-save FFT of P >= SL+M-1 per (rx, code)
+ * yields all SL lags: r = IDFT_P(FFT_P(x seg) conj(FFT_P(c))) / P, metric |r[i]|^2. First
+ * maximum wins over ascending i, as framing.cc:720-741. */
+static void search_parseval(ref_framesync *fs, const ref_cf32 *buf) {
+  uint32_t M = fs->M, N = fs->N, SL = fs->SL, nac = fs->nac, nacN = nac * N;
+  uint32_t P = 1;
+  while (P < SL + M - 1) P <<= 1;
+  uint32_t ncode = nacN + 1; /* code 0: S0; code 1 + ac: S1 of (tx, code) */
+  ref_cf32 *Z = (ref_cf32 *)malloc(sizeof(ref_cf32) * (size_t)ncode * P);
+  ref_cf32 *Y = (ref_cf32 *)malloc(sizeof(ref_cf32) * P);
+  for (uint32_t q = 0; q < ncode; q++) {
+    const ref_cf32 *S = q == 0 ? fs->S0
+                               : fs->S1 + (size_t)((q - 1) % N) * nac * M +
+                                     (size_t)((q - 1) / N) * M;
+    ref_cf32 *z = Z + (size_t)q * P;
+    memset(z, 0, sizeof(ref_cf32) * P);
+    memcpy(z, S, sizeof(ref_cf32) * M);
+    ref_fft(z, M, 1);                     /* M * c[n] */
+    for (uint32_t n = 0; n < M; n++) { z[n].re /= (float)M; z[n].im /= (float)M; }
+    ref_fft(z, P, 0);
+  }
+  for (uint32_t r = 0; r < N; r++) {
+    const ref_cf32 *b = buf + (size_t)r * fs->win_len;
+    for (uint32_t q = 0; q < ncode; q++) {
+      uint64_t base = (uint64_t)SL * q;
+      memset(Y, 0, sizeof(ref_cf32) * P);
+      for (uint32_t n = 0; n < SL + M - 1 && base + n < fs->win_len; n++) Y[n] = b[base + n];
+      ref_fft(Y, P, 0);
+      const ref_cf32 *z = Z + (size_t)q * P;
+      for (uint32_t k = 0; k < P; k++) Y[k] = cmul(Y[k], cconj(z[k]));
+      ref_fft(Y, P, 1);
+      float inv = 1.0f / (float)P;
+      for (uint32_t i = 0; i < SL; i++) {
+        float re = Y[i].re * inv, im = Y[i].im * inv;
+        float v = re * re + im * im;
+        if (q == 0) {
+          if (fs->s0trace) fs->s0trace[(size_t)r * SL + i] = v;
+          if (v > fs->s0_max[r]) { fs->s0_max[r] = v; fs->s0_idx[r] = i; }
+        } else {
+          uint32_t ac = q - 1; /* ac = code * N + tx */
+          if (fs->ctrace) fs->ctrace[((size_t)r * nacN + ac) * SL + i] = v;
+          if (v > fs->corr_max[r * nacN + ac]) {
+            fs->corr_idx[r * nacN + ac] = (uint32_t)(i + base);
+            fs->corr_max[r * nacN + ac] = v;
+          }
+        }
+      }
+    }
+  }
+  free(Y);
+  free(Z);
+}
+
 static void estimate_channel(ref_framesync *fs) { /* framing.cc:653-886 */
   uint32_t M = fs->M, N = fs->N, SL = fs->SL, nac = fs->nac, nacN = nac * N;
   /* windowcf_read: linear oldest -> newest */
@@ -844,13 +909,15 @@ static void estimate_channel(ref_framesync *fs) { /* framing.cc:653-886 */
   ref_cf32 *X = (ref_cf32 *)malloc(sizeof(ref_cf32) * (size_t)N * M);
   for (uint32_t i = 0; i < (size_t)N * nacN; i++) { fs->corr_max[i] = 0.0f; fs->corr_idx[i] = 0; }
   for (uint32_t s = 0; s < N; s++) { fs->s0_max[s] = 0.0f; fs->s0_idx[s] = 0; }
+  double t0 = wall_now();
   /* brute-force access-code search, framing.cc:702-744 (USE_NEW_CHANNEL_EST) */
   float MM = (float)(M * M);
   if (fs->cfg.trace_corr) {
     fs->ctrace = (float *)realloc(fs->ctrace, sizeof(float) * (size_t)N * nacN * SL);
     fs->s0trace = (float *)realloc(fs->s0trace, sizeof(float) * (size_t)N * SL);
   }
-  for (uint32_t i = 0; i < SL; i++) {
+  if (fs->cfg.search_mode == 1) search_parseval(fs, buf);
+  for (uint32_t i = 0; fs->cfg.search_mode != 1 && i < SL; i++) {
     for (uint32_t r = 0; r < N; r++) {
       const ref_cf32 *b = buf + (size_t)r * fs->win_len;
       memcpy(X, b + i, sizeof(ref_cf32) * M);
@@ -878,6 +945,7 @@ static void estimate_channel(ref_framesync *fs) { /* framing.cc:653-886 */
         }
     }
   }
+  double t1 = wall_now();
   /* LS estimate, framing.cc:801-824 (+ training-residual noise variance, build extension) */
   if (!fs->cfg.keep_identity_bias)
     for (size_t i = 0; i < (size_t)M * N * N; i++) { fs->G[i].re = 0.0f; fs->G[i].im = 0.0f; }
@@ -936,6 +1004,7 @@ static void estimate_channel(ref_framesync *fs) { /* framing.cc:653-886 */
     }
     j++;
   }
+  double t2 = wall_now();
   /* replay decode of the window, framing.cc:853-868 */
   ref_cf32 *out = (ref_cf32 *)malloc(sizeof(ref_cf32) * (size_t)N * (fs->M_occ ? fs->M_occ : 1));
   fs->sym_count = 0;
@@ -951,6 +1020,10 @@ static void estimate_channel(ref_framesync *fs) { /* framing.cc:653-886 */
   free(out);
   free(X);
   free(buf);
+  double t3 = wall_now();
+  fs->t_phase[1] += t1 - t0;
+  fs->t_phase[2] += t2 - t1;
+  fs->t_phase[3] += t3 - t2;
 }
 
 static void execute_save_access_codes(ref_framesync *fs, const ref_cf32 *x) { /* :639-651 */
@@ -965,6 +1038,7 @@ static void execute_save_access_codes(ref_framesync *fs, const ref_cf32 *x) { /*
 int ref_framesync_execute(ref_framesync *fs, const ref_cf32 *const *in, uint32_t n) {
   ref_cf32 x[64];
   int brk = 0;
+  double te0 = wall_now(), sub0 = fs->t_phase[1] + fs->t_phase[2] + fs->t_phase[3];
   for (uint32_t i = 0; i < n; i++) { /* framing.cc:481-504 */
     for (uint32_t s = 0; s < fs->N; s++) x[s] = in[s][i];
     switch (fs->state) {
@@ -976,10 +1050,37 @@ int ref_framesync_execute(ref_framesync *fs, const ref_cf32 *const *in, uint32_t
     fs->nsp++;
     if (brk) break;
   }
+  fs->t_phase[0] += (wall_now() - te0) -
+                    (fs->t_phase[1] + fs->t_phase[2] + fs->t_phase[3] - sub0);
   return fs->state;
 }
 
+void ref_framesync_get_phase_times(const ref_framesync *fs, double *t4) {
+  for (int i = 0; i < 4; i++) t4[i] = fs->t_phase[i];
+}
+
 void ref_framesync_reset(ref_framesync *fs) { fs->state = REF_STATE_SEEK_PLATEAU; }
+
+/* CPU-baseline helper (not a reference entry point): put a fresh framesync in the state the
+ * plateau rule leaves it in when it fires at sample `trigger` with `sync_index`
+ * (framing.cc:617-623): the window ring holds samples up to `trigger` (zeros before 0), the
+ * sample count is trigger + 1, the state SAVE_ACCESS_CODES. Executing the samples from
+ * trigger + 1 on then runs search, LS, weights and decode exactly as the full run does. */
+int ref_framesync_skip_to_sync(ref_framesync *fs, const ref_cf32 *const *in, uint64_t trigger,
+                               uint64_t sync_index) {
+  if (fs->state != REF_STATE_SEEK_PLATEAU || fs->nsp != 0) return -1;
+  uint64_t start = trigger + 1 > fs->win_len ? trigger + 1 - fs->win_len : 0;
+  fs->win_head = start % fs->win_len;
+  ref_cf32 x[64];
+  for (uint64_t i = start; i <= trigger; i++) {
+    for (uint32_t s = 0; s < fs->N; s++) x[s] = in[s][i];
+    win_push(fs, x);
+  }
+  fs->nsp = trigger + 1;
+  fs->sync_index = sync_index;
+  fs->state = REF_STATE_SAVE_ACCESS_CODES;
+  return 0;
+}
 uint64_t ref_framesync_get_sync_index(const ref_framesync *fs) { return fs->sync_index; }
 uint64_t ref_framesync_get_num_samples_processed(const ref_framesync *fs) { return fs->nsp; }
 uint64_t ref_framesync_get_plateau_start(const ref_framesync *fs, uint32_t s) {

@@ -115,6 +115,10 @@ typedef struct {
   double   threshold;         /* PLATEAU_THREASHOLD 0.95, config.h:87 */
   int      trace_sc;          /* keep per-sample y (DEBUG_LOG f_sc files) */
   int      trace_corr;        /* keep search metrics (DEBUG_LOG corr_* files) */
+  int      search_mode;       /* 0: brute-force FFT per lag, framing.cc:702-744 (faithful);
+                                 1: Parseval variant (CPU-baseline mode 3 of BASELINE.md, labelled):
+                                 one overlap-save FFT correlation per (rx, code); same metric up
+                                 to fp32 rounding */
 } ref_rx_cfg;
 
 typedef struct ref_framesync ref_framesync;
@@ -123,6 +127,9 @@ ref_framesync *ref_framesync_create(const ref_rx_cfg *cfg, const uint8_t *p,
 void     ref_framesync_destroy(ref_framesync *fs);
 int      ref_framesync_execute(ref_framesync *fs, const ref_cf32 *const *in, uint32_t n);
 void     ref_framesync_reset(ref_framesync *fs);
+/* CPU-baseline helper: state after the plateau rule fired at `trigger` (see mimo_ref.c) */
+int      ref_framesync_skip_to_sync(ref_framesync *fs, const ref_cf32 *const *in,
+                                    uint64_t trigger, uint64_t sync_index);
 uint64_t ref_framesync_get_sync_index(const ref_framesync *fs);
 uint64_t ref_framesync_get_num_samples_processed(const ref_framesync *fs);
 uint64_t ref_framesync_get_plateau_start(const ref_framesync *fs, uint32_t s);
@@ -141,6 +148,9 @@ void     ref_framesync_get_symbols(const ref_framesync *fs, ref_cf32 *out, uint3
 uint64_t ref_framesync_sc_trace_len(const ref_framesync *fs);
 void     ref_framesync_get_sc_trace(const ref_framesync *fs, uint32_t s, float *out);
 uint32_t ref_framesync_M_occ(const ref_framesync *fs);
+/* wall seconds spent per phase since create: [0] S&C + plateau, [1] access-code search,
+ * [2] LS + weights, [3] replay decode (FFT, detect, gain) */
+void     ref_framesync_get_phase_times(const ref_framesync *fs, double *t4);
 /* search metric traces by lag i in [0,SL): corr [N][N*nac][SL], s0 [N][SL] */
 int      ref_framesync_get_corr_trace(const ref_framesync *fs, float *corr, float *s0);
 

@@ -70,6 +70,8 @@ def lib():
             "ref_framesync_get_sc_trace": (None, [vp, C.c_uint32, f32p]),
             "ref_framesync_M_occ": (C.c_uint32, [vp]),
             "ref_framesync_get_corr_trace": (C.c_int, [vp, f32p, f32p]),
+            "ref_framesync_get_phase_times": (None, [vp, f64p]),
+            "ref_framesync_skip_to_sync": (C.c_int, [vp, vp, C.c_uint64, C.c_uint64]),
             "ref_sc_metric_at": (C.c_float, [vp, C.c_uint64, C.c_uint32]),
             "ref_demap_evm": (None, [vp, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32,
                                      u8p, u8p, f64p, f64p, u64p]),
@@ -98,7 +100,7 @@ class _RxCfg(C.Structure):
                 ("pid_max", C.c_uint32), ("detector", C.c_int), ("noise_var", C.c_float),
                 ("keep_identity_bias", C.c_int), ("siso_tx", C.c_uint32),
                 ("siso_rx", C.c_uint32), ("threshold", C.c_double), ("trace_sc", C.c_int),
-                ("trace_corr", C.c_int)]
+                ("trace_corr", C.c_int), ("search_mode", C.c_int)]
 
 
 def _u8(a):
@@ -233,7 +235,9 @@ class FrameSyncRef:
 
     def __init__(self, M, cp, N, nac, pid_max=1000, detector=DET_ZF2, noise_var=-1.0,
                  keep_identity_bias=True, siso_tx=0, siso_rx=0, threshold=0.95,
-                 trace_sc=False, trace_corr=False, p=None, s1_polys=None):
+                 trace_sc=False, trace_corr=False, p=None, s1_polys=None, search_mode=0):
+        """search_mode 0: the reference's brute-force search (framing.cc:702-744); 1: the
+        Parseval overlap-save variant (a CPU-baseline mode, labelled as such where used)."""
         from oracle.codes import s1_polynomials
         self.M, self.cp, self.N, self.nac, self.pid_max = M, cp, N, nac, pid_max
         self.p = default_sctype(M) if p is None else np.ascontiguousarray(p, np.uint8)
@@ -242,7 +246,7 @@ class FrameSyncRef:
         s0b, s1b = code_bits(M, N, nac, s1_polys)
         cfg = _RxCfg(M, cp, N, nac, pid_max, detector, noise_var,
                      1 if keep_identity_bias else 0, siso_tx, siso_rx, threshold,
-                     1 if trace_sc else 0, 1 if trace_corr else 0)
+                     1 if trace_sc else 0, 1 if trace_corr else 0, int(search_mode))
         self._h = lib().ref_framesync_create(C.byref(cfg), _u8(self.p), _u8(s0b), _u8(s1b))
         if not self._h:
             raise ValueError("ref_framesync_create failed")
@@ -262,6 +266,22 @@ class FrameSyncRef:
 
     def reset(self):
         lib().ref_framesync_reset(self._h)
+
+    def execute_from_sync(self, rx, trigger, sync_index):
+        """CPU-baseline mode: skip the S&C scan (the plateau rule fired at `trigger`, e.g. as
+        the GPU reported) and run search, LS, weights and decode on the rest of the capture.
+        Same symbols as execute(rx) when trigger/sync_index are the real ones."""
+        rx = [np.ascontiguousarray(r, np.complex64) for r in rx]
+        ptrs = (C.c_void_p * self.N)(*[r.ctypes.data for r in rx])
+        if lib().ref_framesync_skip_to_sync(self._h, ptrs, int(trigger), int(sync_index)) != 0:
+            raise RuntimeError("skip_to_sync needs a fresh framesync")
+        return self.execute([r[int(trigger) + 1:] for r in rx])
+
+    def phase_times(self):
+        """Wall seconds per phase: S&C+plateau, search, LS+weights, replay decode."""
+        t = np.zeros(4)
+        lib().ref_framesync_get_phase_times(self._h, t.ctypes.data_as(C.POINTER(C.c_double)))
+        return dict(zip(("sc", "search", "ls_weights", "decode"), t.tolist()))
 
     @property
     def state(self):

@@ -314,3 +314,36 @@ class Synthesizer:
                  stream=None):
         check(lib().mimo_synth_frames(C.byref(self._cfg), frame_id0, n_frames, _ptr(out), stride,
                                       frame_len, _ptr(tx_idx), _ptr(H), stream), "synth_frames")
+
+    def stream_layout(self, n_streams, frames_per_stream, stream0=0):
+        """Frame lengths [S][J] of streams that carry the synthesiser's frames
+        (stream0+s)*J .. (stream0+s)*J+J-1 back to back, and the common capture length."""
+        J = frames_per_stream
+        lens = [[self.frame_len((stream0 + s) * J + j) for j in range(J)]
+                for s in range(n_streams)]
+        return lens, max(sum(l) for l in lens)
+
+    def generate_streams(self, iq, L, n_streams, frames_per_stream, slots, stream0=0,
+                         tx_idx=None, stream=None):
+        """Back-to-back frames (BASELINE config C5's per-stream workload) into iq [S][N][L]
+        (complex64, zeroed by the caller past each stream's last frame). tx_idx, if given:
+        [S*slots][N][pid][M_occ] reference rows, row s*slots+j for frame j of stream s.
+        Returns the host uint64 array [S][slots] of frame starts (UINT64_MAX after the last),
+        the d_ref_starts of mimo_batch, and the lengths [S][J]."""
+        P = self.params
+        J = frames_per_stream
+        lens, _ = self.stream_layout(n_streams, J, stream0)
+        N = P.num_streams
+        row = N * P.pid * (len(self.p) if P.p is None else
+                           int(np.count_nonzero(self.p)))
+        starts = np.full((n_streams, slots), np.uint64(2 ** 64 - 1), np.uint64)
+        base = _ptr(iq)
+        for s in range(n_streams):
+            pos = 0
+            for j in range(J):
+                txp = None if tx_idx is None else _ptr(tx_idx) + (s * slots + j) * row
+                self.generate(base + ((s * N) * L + pos) * 8, L, lens[s][j], 1,
+                              frame_id0=(stream0 + s) * J + j, tx_idx=txp, stream=stream)
+                starts[s, j] = pos
+                pos += lens[s][j]
+        return starts, lens

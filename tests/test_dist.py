@@ -63,6 +63,95 @@ def _worker(rank, world, port, frames_per_rank, q):
         dist.destroy_process_group()
 
 
+def _pack(names):
+    """Frames of `names` as one float32 row each (rx viewed as float32, zero-padded)."""
+    rows = [np.ascontiguousarray(np.load(os.path.join(GOLD, n + ".npz"))["rx"]).view(np.float32)
+            .ravel() for n in names]
+    return rows
+
+
+def _scatter_worker(rank, world, port, frames_per_rank, width, steps, q):
+    """Rank 0 holds every rank's captures ([world][F][width] float32, the fixtures' rx rows);
+    ScatterPipeline delivers each rank its slice for `steps` double-buffered steps; each rank
+    checks the bytes, runs the oracle on the frames it received and reduces the counters."""
+    from rub_mimo_amd.shard import ScatterPipeline
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        names = [FIXTURES[i % len(FIXTURES)] for i in range(world * frames_per_rank)]
+        rows = _pack(names)
+        src = None
+        if rank == 0:
+            src = torch.zeros((world, frames_per_rank, width), dtype=torch.float32)
+            for i, r in enumerate(rows):
+                src[i // frames_per_rank, i % frames_per_rank, :len(r)] = torch.from_numpy(r)
+        pipe = ScatterPipeline(dist, src, (frames_per_rank, width), torch.float32, "cpu",
+                               rank, world)
+        pipe.start()
+        f0, nf = frame_ids(rank, frames_per_rank)
+        exact = True
+        acc = {k: 0.0 for k in STAT_KEYS}
+        for s in range(steps):
+            got = pipe.next()
+            for j in range(nf):
+                want = rows[f0 + j]
+                exact &= bool(np.array_equal(got[j, :len(want)].numpy(), want))
+                exact &= bool(torch.all(got[j, len(want):] == 0))
+            if s == 0:      # receive what arrived (the oracle stands in for the rank's GPU)
+                for j in range(nf):
+                    name = names[f0 + j]
+                    g = np.load(os.path.join(GOLD, name + ".npz"))
+                    rx = got[j, :len(rows[f0 + j])].numpy().view(np.complex64).reshape(
+                        g["rx"].shape)
+                    assert np.array_equal(rx, g["rx"])
+                    for k, v in _frame_stats(name).items():
+                        acc[k] += v
+        pipe.drain()
+        tot, emax = reduce_stats(acc, 0.1 * (rank + 1), dist)
+        q.put((rank, exact, tot, emax))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_rank0_scatter_delivers_bytes_and_counters(world):
+    """bench.py --ingest scatter's data movement on CPU (gloo): byte-exact delivery of every
+    rank's slice over double-buffered steps, and the reduced counters equal one process."""
+    per, steps = 2, 3
+    width = max(len(r) for r in _pack(FIXTURES)) + 5
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_scatter_worker, args=(r, world, port, per, width, steps, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    out = sorted(q.get(timeout=180) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    single = {k: 0.0 for k in STAT_KEYS}
+    for i in range(world * per):
+        for k, v in _frame_stats(FIXTURES[i % len(FIXTURES)]).items():
+            single[k] += v
+    for rank, exact, tot, emax in out:
+        assert exact, rank
+        assert emax == pytest.approx(0.1 * world)
+        for k in STAT_KEYS:
+            assert tot[k] == pytest.approx(single[k], rel=1e-12)
+
+
+def test_split_streams_partition():
+    from rub_mimo_amd.shard import split_streams
+    for world in (1, 2, 3, 4, 8):
+        spans = [split_streams(8, world, r) for r in range(world)]
+        assert spans[0][0] == 0 and spans[-1][1] == 8
+        assert all(a[1] == b[0] for a, b in zip(spans, spans[1:]))
+        assert max(b - a for a, b in spans) - min(b - a for a, b in spans) <= 1
+    with pytest.raises(ValueError):
+        split_streams(8, 2, 2)
+
+
 def test_frame_ids_partition():
     seen = []
     for r in range(4):

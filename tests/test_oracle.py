@@ -139,6 +139,70 @@ def test_oracle_matches_golden(path):
     assert np.abs(syms - g["symbols"]).max() / scale < 1e-6
 
 
+@pytest.mark.parametrize("path", GOLDEN, ids=[os.path.basename(p) for p in GOLDEN])
+def test_parseval_search_variant_matches_brute_force(path):
+    """The oracle's Parseval search (search_mode 1, a labelled CPU-baseline mode for C4) finds
+    the brute-force search's corr indices wherever the brute-force peak has a margin, with
+    metrics equal to fp32 rounding, and the phase clocks account for the run."""
+    g = load(path)
+    N, M = int(g["N"]), int(g["M"])
+    kw = dict(pid_max=int(g["pid"]), detector=int(g["detector"]),
+              keep_identity_bias=bool(g["keep_identity_bias"]), p=g["p"],
+              siso_tx=int(g["siso_tx"]), siso_rx=int(g["siso_rx"]), trace_corr=True)
+    a = ref.FrameSyncRef(M, int(g["cp"]), N, int(g["nac"]), **kw)
+    b = ref.FrameSyncRef(M, int(g["cp"]), N, int(g["nac"]), search_mode=1, **kw)
+    a.execute(g["rx"])
+    b.execute(g["rx"])
+    ca, _ = a.corr_trace()
+    cb, _ = b.corr_trace()
+    scale = ca.max()
+    assert np.abs(ca - cb).max() <= 1e-4 * scale
+    cia, _, sia, _ = a.get_corr()
+    cib, _, sib, _ = b.get_corr()
+    for r in range(N):
+        for ac in range(cia.shape[1]):
+            tr = np.sort(ca[r, ac])
+            if tr[-1] > (1 + 1e-3) * tr[-2]:
+                assert cia[r, ac] == cib[r, ac], (r, ac)
+    t = b.phase_times()
+    assert all(v >= 0 for v in t.values()) and t["sc"] > 0
+
+
+@pytest.mark.parametrize("path", GOLDEN, ids=[os.path.basename(p) for p in GOLDEN])
+def test_execute_from_sync_equals_full_run(path):
+    """CPU-baseline helper: starting at the trigger (S&C skipped) gives the full run's
+    samples-processed, corr indices, G and symbols exactly."""
+    g = load(path)
+    full = run_oracle(g)
+    N = int(g["N"])
+    fs = ref.FrameSyncRef(int(g["M"]), int(g["cp"]), N, int(g["nac"]), pid_max=int(g["pid"]),
+                          detector=int(g["detector"]),
+                          keep_identity_bias=bool(g["keep_identity_bias"]), p=g["p"],
+                          siso_tx=int(g["siso_tx"]), siso_rx=int(g["siso_rx"]))
+    trig = _trigger_of(g)
+    st = fs.execute_from_sync(g["rx"], trig, full.get_sync_index())
+    assert st == ref.STATE_MIMO
+    assert fs.get_num_samples_processed() == full.get_num_samples_processed()
+    assert (fs.get_corr()[0] == full.get_corr()[0]).all()
+    assert np.array_equal(fs.get_G(), full.get_G())
+    assert np.array_equal(fs.symbols(), full.symbols())
+
+
+def _trigger_of(g):
+    """First sample where every antenna's plateau is longer than cp (framing.cc:617-623),
+    from the oracle's S&C trace."""
+    fs = run_oracle(g)
+    N, cp = int(g["N"]), int(g["cp"])
+    y = np.stack([fs.sc_trace(s) for s in range(N)], 1)      # [samples][N]
+    above = y > 0.95
+    run = np.zeros(N, np.int64)
+    for n in range(len(y)):
+        run = np.where(above[n], run + 1, 0)
+        if np.all(run - 1 > cp):
+            return n
+    raise AssertionError("no trigger")
+
+
 @pytest.mark.parametrize("path", [p for p in GOLDEN if "siso" not in p],
                          ids=[os.path.basename(p) for p in GOLDEN if "siso" not in p])
 def test_numpy_model_matches_golden(path):
