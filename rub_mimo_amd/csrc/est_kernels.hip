@@ -466,6 +466,150 @@ __global__ __launch_bounds__(256) void weights_kernel(WeightArgs a) {
 }
 
 // ------------------------------------------------------------------------------------
+// N = 8: the per-thread form above needs 2 N^2 complex doubles in registers (512 VGPRs at
+// 8x8) and spills to scratch. Here one subcarrier is solved by a group of 8 lanes, lane j
+// holding row j of [A | B] (4 N doubles). The same Gauss-Jordan with partial pivoting as
+// cd_solve / the oracle: a lane's `pos` is its row's current index in the oracle's row
+// array, so the pivot search (largest |a|^2 among rows >= c, the smallest index winning
+// ties = the oracle's strict '>' scan from c) and the row swap (two lanes exchange pos) follow
+// the oracle exactly. The normalised pivot row is broadcast through LDS.
+constexpr int kWRowT = 256;
+constexpr int kWRowG = kWRowT / 8;   // subcarriers per workgroup
+
+template <int N>
+__global__ __launch_bounds__(kWRowT) void weights_row_kernel(WeightArgs a) {
+  static_assert(N >= 2 && N <= 8, "row solve handles 2..8 streams");
+  const uint32_t f = blockIdx.y;
+  FrameInfo &I = a.info[f];
+  if (I.status != 0) return;
+  __shared__ float2 s_g[kWRowG][N * N];
+  __shared__ cd s_piv[kWRowG][2 * N];
+  __shared__ int s_sing[kWRowG];
+  __shared__ double s_acc;
+  const int tid = threadIdx.x, grp = tid >> 3, j = tid & 7;
+  const uint32_t k = blockIdx.x * kWRowG + grp;
+  double s2 = (double)a.noise_var;
+  if (a.noise_var < 0.0f) {   // fixed-order partial sum, as weights_kernel
+    if (tid < 64) {
+      double acc = 0.0;
+      for (uint32_t e = tid; e < a.n_nvp; e += 64) acc += a.nv_part[(uint64_t)f * a.n_nvp + e];
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off);
+      if (tid == 0) s_acc = acc;
+    }
+    __syncthreads();
+    s2 = (double)(float)(s_acc * a.nv_norm);
+  }
+  if (blockIdx.x == 0 && tid == 0) {
+    I.noise_var = (float)s2;
+    const unsigned long long key =
+        a.keys[((uint64_t)f * N + (N - 1)) * a.n_slots + a.n_slots - 1];
+    const uint32_t ci = key ? (0xFFFFFFFFu - (uint32_t)(key & 0xFFFFFFFFull)) : 0u;
+    const uint64_t i0 = (uint64_t)ci + a.M;
+    I.i0 = (uint32_t)i0;
+    I.n_sym = (i0 < a.win_len) ? (uint32_t)((a.win_len - i0) / a.SL) : 0u;
+  }
+  const bool live = k < a.M;
+  const bool occ = live && a.occ_index[k] >= 0;
+  if (live)
+    for (int e = j; e < N * N; e += 8) s_g[grp][e] = a.G[((uint64_t)f * a.M + k) * N * N + e];
+  __syncthreads();
+  const bool row = j < N;
+  cd A[N], B[N];
+  const float2 *g = s_g[grp];
+#pragma unroll
+  for (int c = 0; c < N; c++) {
+    A[c] = {0.0, 0.0};
+    B[c] = {0.0, 0.0};
+  }
+  if (row) {
+    if (a.detector == 1) {   // ZF: A = G, B = I
+#pragma unroll
+      for (int c = 0; c < N; c++) {
+        A[c] = {(double)g[j * N + c].x, (double)g[j * N + c].y};
+        B[c] = {c == j ? 1.0 : 0.0, 0.0};
+      }
+    } else {                 // MMSE: A = G^H G + s2 I, B = G^H
+#pragma unroll
+      for (int c = 0; c < N; c++) {
+        double sr = 0.0, si = 0.0;
+#pragma unroll
+        for (int rr = 0; rr < N; rr++) {
+          const double gar = g[rr * N + j].x, gai = g[rr * N + j].y;
+          const double gbr = g[rr * N + c].x, gbi = g[rr * N + c].y;
+          sr += gar * gbr + gai * gbi;
+          si += gar * gbi - gai * gbr;
+        }
+        A[c] = {sr + ((c == j) ? s2 : 0.0), si};
+        B[c] = {(double)g[c * N + j].x, -(double)g[c * N + j].y};
+      }
+    }
+  }
+  int pos = row ? j : 64;
+  bool ok = true;
+#pragma unroll
+  for (int c = 0; c < N; c++) {
+    // pivot: max |A[.][c]|^2 over rows with pos >= c, smallest pos on ties
+    double m = (row && pos >= c) ? A[c].re * A[c].re + A[c].im * A[c].im : -1.0;
+    int mp = (row && pos >= c) ? pos : 64;
+#pragma unroll
+    for (int off = 1; off < 8; off <<= 1) {
+      const double om = __shfl_xor(m, off);
+      const int op = __shfl_xor(mp, off);
+      if (om > m || (om == m && op < mp)) { m = om; mp = op; }
+    }
+    // swap: the row at pos c takes the pivot's place
+    if (pos == c) pos = mp;
+    else if (pos == mp) pos = c;
+    if (pos == c && row) {              // the pivot lane normalises and publishes its row
+      const cd d = A[c];
+      const double dd = d.re * d.re + d.im * d.im;
+      s_sing[grp] = dd == 0.0 ? 1 : 0;
+      if (dd != 0.0) {
+        const cd inv = {d.re / dd, -d.im / dd};
+#pragma unroll
+        for (int q = 0; q < N; q++) {
+          const cd x = A[q], y = B[q];
+          A[q] = {x.re * inv.re - x.im * inv.im, x.re * inv.im + x.im * inv.re};
+          B[q] = {y.re * inv.re - y.im * inv.im, y.re * inv.im + y.im * inv.re};
+          s_piv[grp][q] = A[q];
+          s_piv[grp][N + q] = B[q];
+        }
+      }
+    }
+    __syncthreads();
+    const bool sing = s_sing[grp] != 0;
+    ok = ok && !sing;
+    if (!sing && row && pos != c) {
+      const cd fct = A[c];
+      if (!(fct.re == 0.0 && fct.im == 0.0)) {
+#pragma unroll
+        for (int q = 0; q < N; q++) {
+          const cd x = s_piv[grp][q], y = s_piv[grp][N + q];
+          A[q].re -= fct.re * x.re - fct.im * x.im;
+          A[q].im -= fct.re * x.im + fct.im * x.re;
+          B[q].re -= fct.re * y.re - fct.im * y.im;
+          B[q].im -= fct.re * y.im + fct.im * y.re;
+        }
+      }
+    }
+    __syncthreads();
+  }
+  if (!live || !row) return;
+  // row `pos` of B is row `pos` of W (output stream pos); zero on a null carrier or a singular
+  // system (as weights_kernel); detectors other than ZF/MMSE keep the identity (weights_kernel)
+  const bool solve = a.detector == 1 || a.detector == 2;
+#pragma unroll
+  for (int rr = 0; rr < N; rr++) {
+    float2 w = make_float2(0.0f, 0.0f);
+    if (occ && solve && ok) w = make_float2((float)B[rr].re, (float)B[rr].im);
+    else if (occ && !solve && rr == pos) w = make_float2(1.0f, 0.0f);
+    a.W[(((uint64_t)f * N + pos) * N + rr) * a.M + k] = w;
+  }
+  if (j == 0) a.gain[(uint64_t)f * a.M + k] = 1.0f;
+}
+
+// ------------------------------------------------------------------------------------
 template <int LOG2M, int LOG2F>
 static void codes_dispatch_f(const CodesArgs &a, int log2F, hipStream_t s) {
   if constexpr (LOG2F <= 13) {
@@ -549,10 +693,11 @@ void launch_weights(const WeightArgs &a, uint32_t n_frames, hipStream_t s) {
     case 2: hipLaunchKernelGGL(weights_kernel<2>, grid, dim3(256), 0, s, a); break;
     case 3: hipLaunchKernelGGL(weights_kernel<3>, grid, dim3(256), 0, s, a); break;
     case 4: hipLaunchKernelGGL(weights_kernel<4>, grid, dim3(256), 0, s, a); break;
-    case 5: hipLaunchKernelGGL(weights_kernel<5>, grid, dim3(256), 0, s, a); break;
-    case 6: hipLaunchKernelGGL(weights_kernel<6>, grid, dim3(256), 0, s, a); break;
-    case 7: hipLaunchKernelGGL(weights_kernel<7>, grid, dim3(256), 0, s, a); break;
-    default: hipLaunchKernelGGL(weights_kernel<8>, grid, dim3(256), 0, s, a); break;
+    default: {   // 8 streams (mimo_rx_create admits 1, 2, 4, 8): the 8-lane row solve
+      dim3 rgrid((a.M + kWRowG - 1) / kWRowG, n_frames);
+      hipLaunchKernelGGL(weights_row_kernel<8>, rgrid, dim3(kWRowT), 0, s, a);
+      break;
+    }
   }
 }
 

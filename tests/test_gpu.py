@@ -83,6 +83,9 @@ def test_streaming_framesync_matches_golden(path):
         assert np.allclose(gn, g["gain"], rtol=1e-3)
     if int(g["detector"]) == ref.DET_MMSE:
         assert abs(fs.get_noise_var() - float(g["noise_var"])) <= 1e-4 * float(g["noise_var"])
+    if int(g["detector"]) in (ref.DET_ZF2, ref.DET_ZF, ref.DET_MMSE):
+        W = fs.get_W()
+        assert np.abs(W - g["W"]).max() <= 1e-4 * np.abs(g["W"]).max()
 
 
 @pytest.mark.parametrize("path", GOLDEN[:3], ids=[os.path.basename(p) for p in GOLDEN[:3]])
@@ -352,6 +355,13 @@ def test_c3_4x4_mmse_2048_64qam_full_frame():
 def test_c4_8x8_mmse_4096_256qam_reduced_codes():
     """C4 geometry with 2 access codes so the brute-force oracle stays within ~30 s."""
     _c_frame_parity(4096, 304, 8, 2, 12, 256, _lib.DET_MMSE, 35.0, seed=41, bias=False)
+
+
+@pytest.mark.parametrize("det", [_lib.DET_ZF, _lib.DET_MMSE])
+def test_row_solve_8x8_matches_oracle(det):
+    """8 streams take the 8-lane row solve (weights_row_kernel): reduced 8x8 frames checked
+    against the oracle's Gauss-Jordan, symbols within the EVM tolerance."""
+    _c_frame_parity(256, 32, 8, 2, 12, 16, det, 35.0, seed=68 + det)
 
 
 def test_c4_batched_full_size_properties():
