@@ -190,6 +190,7 @@ struct mimo_rx {
   uint32_t M_null = 0, M_pilot = 0, M_data = 0, M_occ = 0;
   int log2M = 0, log2F = 0;
   uint32_t F = 0, lagc = 0, n_lagc = 0, n_slots = 0;
+  bool search_ls = false;               // fused search + LS (search_ls_kernel) for this geometry
   uint32_t n_cu = 256;
   int det = 0;
   float noise_var = -1.0f;
@@ -220,6 +221,7 @@ struct mimo_rx {
   DevBuf<float2> G, W;
   DevBuf<float> gain;
   DevBuf<double> nvp, evm_part, evm_out, lspart, evm_chunk;
+  DevBuf<float2> lsq;                   // fused search + LS: X/S1 per access code
   DevBuf<uint32_t> evm_cnt;             // per-frame chunk counters of evm_kernel (self-resetting)
   DevBuf<uint32_t> nrec;                // per-frame EVM records of the streaming decode
   size_t cap_lspart = 0;
@@ -250,7 +252,7 @@ struct mimo_rx {
   hipStream_t g_stream = nullptr;
   bool g_valid = false;
   hipGraphExec_t g_exec = nullptr;
-  std::array<const void *, 22> g_sig{};
+  std::array<const void *, 23> g_sig{};
 };
 
 struct mimo_tx {
@@ -322,7 +324,8 @@ static double sc_band(uint32_t M) {
 // the stream walk assigns F * fpc frame slots
 int run_sync(mimo_rx *h, const float2 *iq, uint64_t stride, uint32_t F, uint64_t frame_len,
              uint64_t chunk_lo, bool reset_trig, hipStream_t s, uint32_t fpc = 1,
-             const uint64_t *ref_starts = nullptr, uint32_t ref_stride = 0) {
+             const uint64_t *ref_starts = nullptr, uint32_t ref_stride = 0,
+             bool zero_keys = false) {
   const uint64_t K = sc_chunk_len(h->cp);
   const uint64_t nchunks = (frame_len + K - 1) / K;
   const bool stream = fpc > 1;
@@ -336,6 +339,8 @@ int run_sync(mimo_rx *h, const float2 *iq, uint64_t stride, uint32_t F, uint64_t
     fa.count++;
   };
   if (reset_trig) add_fill(h->trig.p, sizeof(unsigned long long) * F, 0xFFFFFFFFu);
+  // the search's argmax keys, zeroed here instead of by a memset ahead of the search
+  if (zero_keys) add_fill(h->keys.p, sizeof(unsigned long long) * F * fpc * h->N * h->n_slots, 0u);
   if (stream) {
     HIPCHK(h->cand.ensure((size_t)F * nchunks));
     HIPCHK(h->certfail.ensure(F));
@@ -449,17 +454,15 @@ int run_sync(mimo_rx *h, const float2 *iq, uint64_t stride, uint32_t F, uint64_t
 }
 
 int run_estimate(mimo_rx *h, const float2 *iq, uint64_t stride, uint32_t F, uint64_t frame_len,
-                 hipStream_t s) {
-  HIPCHK(hipMemsetAsync(h->keys.p, 0, sizeof(unsigned long long) * F * h->N * h->n_slots, s));
+                 hipStream_t s, bool keys_zeroed = false) {
+  if (!keys_zeroed)
+    HIPCHK(hipMemsetAsync(h->keys.p, 0, sizeof(unsigned long long) * F * h->N * h->n_slots, s));
   SearchArgs sa{};
   sa.iq = iq; sa.stride = stride; sa.frame_len = frame_len;
   sa.N = h->N; sa.M = h->M; sa.SL = h->SL; sa.n_slots = h->n_slots;
   sa.lagc = h->lagc; sa.n_lagc = h->n_lagc;
   sa.codespec = h->codes.codespec.p; sa.vscale = h->vscale.p;
   sa.info = h->info.p; sa.keys = h->keys.p; sa.tw = h->tw;
-  hipEvent_t e = h->timer.begin(s);
-  launch_search(sa, h->log2F, F, s);
-  h->timer.end(2, e, s);
   LsArgs la{};
   la.iq = iq; la.stride = stride; la.frame_len = frame_len;
   la.N = h->N; la.M = h->M; la.nac = h->nac; la.n_slots = h->n_slots;
@@ -467,17 +470,34 @@ int run_estimate(mimo_rx *h, const float2 *iq, uint64_t stride, uint32_t F, uint
   la.keep_bias = h->keep_bias; la.scale = h->ls_scale; la.info = h->info.p;
   la.n_groups = (h->nac + kLsCodesPerGroup - 1) / kLsCodesPerGroup;
   la.n_nvp = h->N * h->N * ((h->M + 255) / 256);
-  {
-    const size_t need = (size_t)F * h->N * h->N * la.n_groups * 3 * h->M;
-    if (need > h->cap_lspart) {
-      HIPCHK(h->lspart.ensure(need));
-      h->cap_lspart = need;
+  la.G = h->G.p; la.nv_part = h->nvp.p; la.tw = h->tw;
+  if (h->search_ls) {
+    // search of slot pairs with the LS terms fused in, then the fixed-order LS combine
+    HIPCHK(h->lsq.ensure((size_t)F * h->N * h->N * h->nac * h->M));
+    sa.s1sign = h->s1sign.p; sa.lsq = h->lsq.p; sa.nac = h->nac;
+    la.lsq = h->lsq.p;
+    hipEvent_t e = h->timer.begin(s);
+    launch_search_ls(sa, h->log2F, h->log2M, F, s);
+    h->timer.end(2, e, s);
+    e = h->timer.begin(s);
+    launch_ls_combine_q(la, F, s);
+    h->timer.end(3, e, s);
+  } else {
+    hipEvent_t e = h->timer.begin(s);
+    launch_search(sa, h->log2F, F, s);
+    h->timer.end(2, e, s);
+    {
+      const size_t need = (size_t)F * h->N * h->N * la.n_groups * 3 * h->M;
+      if (need > h->cap_lspart) {
+        HIPCHK(h->lspart.ensure(need));
+        h->cap_lspart = need;
+      }
     }
+    la.part = h->lspart.p;
+    e = h->timer.begin(s);
+    launch_ls(la, h->log2M, F, s);
+    h->timer.end(3, e, s);
   }
-  la.G = h->G.p; la.part = h->lspart.p; la.nv_part = h->nvp.p; la.tw = h->tw;
-  e = h->timer.begin(s);
-  launch_ls(la, h->log2M, F, s);
-  h->timer.end(3, e, s);
   WeightArgs wa{};
   wa.N = h->N; wa.M = h->M; wa.M_occ = h->M_occ; wa.nac = h->nac; wa.SL = h->SL;
   wa.n_slots = h->n_slots; wa.detector = h->det; wa.noise_var = h->noise_var;
@@ -485,7 +505,7 @@ int run_estimate(mimo_rx *h, const float2 *iq, uint64_t stride, uint32_t F, uint
   wa.gain = h->gain.p; wa.nv_part = h->nvp.p; wa.n_nvp = la.n_nvp; wa.keys = h->keys.p;
   wa.win_len = h->win_len;
   wa.info = h->info.p;
-  e = h->timer.begin(s);
+  hipEvent_t e = h->timer.begin(s);
   launch_weights(wa, F, s);
   h->timer.end(4, e, s);
   HIPCHK(hipGetLastError());
@@ -607,11 +627,19 @@ int mimo_rx_create(const mimo_rx_config *cfg, void *hip_stream, mimo_rx **out) {
   h->nv_norm = (h->nac >= 2) ? ((double)h->dn * (double)h->dn /
                                 ((double)h->M_occ * N * N * (h->nac - 1)))
                              : 0.0;
-  // search transform: F >= SL + M - 1 lags+taps, capped at 8192 (then several lag chunks)
+  // search transform. Fused search + LS (search_ls_kernel): two slots per transform,
+  // F >= 2 SL + M - 1, up to 16384. Otherwise F >= SL + M - 1 lags+taps, capped at 8192 (then
+  // several lag chunks per slot) and a separate LS pass.
   uint32_t F = 1;
-  while (F < h->SL + h->M - 1) F <<= 1;
-  if (F > 8192) F = 8192;
-  if (F < 2 * h->M) F = 2 * h->M;
+  while (F < 2 * h->SL + h->M - 1 || F < 2 * h->M) F <<= 1;
+  static const bool no_fuse = [] { const char *e = getenv("RMIMO_SEARCH_LS"); return e && e[0] == '0'; }();
+  h->search_ls = !no_fuse && F <= 16384 && search_ls_supported(ilog2(F), ilog2(h->M));
+  if (!h->search_ls) {
+    F = 1;
+    while (F < h->SL + h->M - 1) F <<= 1;
+    if (F > 8192) F = 8192;
+    if (F < 2 * h->M) F = 2 * h->M;
+  }
   h->F = F; h->log2F = ilog2(F);
   h->lagc = F - h->M + 1;
   h->n_lagc = (h->SL + h->lagc - 1) / h->lagc;
@@ -947,8 +975,8 @@ static int run_batch(mimo_rx *h, const mimo_batch *b, hipStream_t s) {
   const float2 *iq = reinterpret_cast<const float2 *>(b->d_iq);
   const uint32_t fpc = batch_fpc(b), slots = b->n_frames * fpc;
   int rc = run_sync(h, iq, b->stride, b->n_frames, b->frame_len, 0, true, s, fpc,
-                    fpc > 1 ? b->d_ref_starts : nullptr, b->ref_stride);
-  if (!rc) rc = run_estimate(h, iq, b->stride, slots, b->frame_len, s);
+                    fpc > 1 ? b->d_ref_starts : nullptr, b->ref_stride, true);
+  if (!rc) rc = run_estimate(h, iq, b->stride, slots, b->frame_len, s, true);
   if (!rc)
     rc = run_decode(h, iq, b->stride, slots, b->frame_len, b->max_out_syms,
                     reinterpret_cast<float2 *>(b->d_out_sym),
@@ -963,11 +991,11 @@ static int run_batch(mimo_rx *h, const mimo_batch *b, hipStream_t s) {
 // the configuration and F (S&C items and hot items are pulled from device-side queues), so
 // the graph stays valid. Not used while stage timing or a diagnostic counter is on.
 // every device pointer a captured batch bakes into its kernels' arguments
-static std::array<const void *, 22> ws_signature(const mimo_rx *h) {
+static std::array<const void *, 23> ws_signature(const mimo_rx *h) {
   return {h->trig.p, h->keys.p, h->rec.p, h->info.p, h->G.p, h->W.p, h->gain.p, h->nvp.p,
           h->evm_part.p, h->evm_out.p, h->n_exact.p, h->queue.p, h->hot.p, h->lspart.p,
           h->tw, h->codes.codespec.p, h->scr_flag.p, h->scr_min.p, h->scr_max.p, h->nrec.p,
-          h->cand.p, h->certfail.p};
+          h->cand.p, h->certfail.p, h->lsq.p};
 }
 
 static bool same_batch(const mimo_batch &x, const mimo_batch &y) {

@@ -193,6 +193,144 @@ MIMO_DEV uint32_t key_index(unsigned long long k) {
   return k ? (0xFFFFFFFFu - (uint32_t)(k & 0xFFFFFFFFull)) : 0u;
 }
 
+// Search of two consecutive slots with the LS term of each fused in (one lag chunk per slot,
+// 2 SL + M - 1 <= F). Slot s0 + u's window at lag i is segment offset u SL + i of the F-point
+// segment starting at window index SL s0, so one forward FFT_F serves both slots: per slot a
+// product with conj(its code spectrum), the inverse and the first-maximum score over its SL
+// lags (3 FFT_F per two slots instead of 4). The workgroup is then the only writer of the
+// slot's key, so the argmax is final and the LS term of access code ac = slot - 1 follows at
+// once: the M-point FFT of the window at the argmax (framing.cc:801-806), times the S1 sign
+// (X / S1, S1 = +-1, framing.cc:811), stored per code in lsq[f][rx][tx][code][M] for
+// ls_combine_q_kernel's fixed-order sum. The separate LS pass re-read and re-transformed the
+// same windows; here the window is still in L2 from the segment load.
+template <int LOG2F, int LOG2M>
+__global__ __launch_bounds__((1 << LOG2F) / 16) __attribute__((amdgpu_waves_per_eu(4)))
+void search_ls_kernel(SearchArgs a) {
+  constexpr int PTS = 16;
+  using PL = RegPlan<LOG2F, PTS>;
+  constexpr int F = PL::N, T = PL::T, M = 1 << LOG2M;
+  extern __shared__ __attribute__((aligned(16))) float2 lds_raw[];
+  v2f *buf = reinterpret_cast<v2f *>(lds_raw);
+  __shared__ unsigned long long s_key[2];
+  const uint32_t f = blockIdx.y;
+  const FrameInfo &I = a.info[f];
+  if (I.status != 0) return;
+  const int tid = threadIdx.x;
+  const uint32_t r = blockIdx.x % a.N;
+  const uint32_t s0 = 2 * (blockIdx.x / a.N);
+  const uint32_t ns = min(2u, a.n_slots - s0);
+  const int64_t abs0 = I.base + (int64_t)a.SL * s0;
+  const int64_t L = (int64_t)a.frame_len;
+  const float2 *__restrict__ xf = a.iq + ((uint64_t)I.cap * a.N + r) * a.stride;
+  const v2f *__restrict__ x = reinterpret_cast<const v2f *>(xf);
+  const bool inb = abs0 >= 0 && abs0 + F <= L;
+  v2f v[PTS], X[PTS];
+#pragma unroll
+  for (int e = 0; e < PTS; e++) {
+    const int64_t n = abs0 + reg_index<LOG2F, PTS>(tid, e);
+    v[e] = x[inb ? n : (n < 0 ? 0 : (n >= L ? L - 1 : n))];
+  }
+  if (!inb) {
+#pragma unroll
+    for (int e = 0; e < PTS; e++) {
+      const int64_t n = abs0 + reg_index<LOG2F, PTS>(tid, e);
+      if (n < 0 || n >= L) v[e] = v2f{0.0f, 0.0f};
+    }
+  }
+  v2f w1[PL::NTW > 0 ? PL::NTW : 1];
+  reg_twiddles<LOG2F, PTS>(w1, a.tw, tid);
+  if (tid == 0) { s_key[0] = 0ull; s_key[1] = 0ull; }
+  reg_compute<LOG2F, PTS, 0, false>(v, w1);
+  reg_rest<LOG2F, PTS, 1, false>(buf, v, w1, tid);
+#pragma unroll
+  for (int e = 0; e < PTS; e++) X[e] = v[e];
+  for (uint32_t u = 0; u < ns; u++) {                 // uniform
+    const uint32_t slot = s0 + u;
+    const v2f *__restrict__ csp = reinterpret_cast<const v2f *>(a.codespec + (size_t)slot * F);
+#pragma unroll
+    for (int e = 0; e < PTS; e++) v[e] = vmulc(X[e], csp[reg_index<LOG2F, PTS>(tid, e)]);
+    reg_compute<LOG2F, PTS, 0, true>(v, w1);
+    reg_rest<LOG2F, PTS, 1, true>(buf, v, w1, tid);
+    const float vs = a.vscale[slot];
+    const int off = (int)(u * a.SL);
+    const uint32_t ws = a.SL * slot;                  // window index of lag 0
+    unsigned long long best = 0ull;
+#pragma unroll
+    for (int e = 0; e < PTS; e++) {
+      const int i = reg_index<LOG2F, PTS>(tid, e) - off;
+      const float val = (v[e].x * v[e].x + v[e].y * v[e].y) * vs;
+      if (i >= 0 && i < (int)a.SL && val > 0.0f) {
+        const unsigned long long key = ((unsigned long long)__float_as_uint(val) << 32) |
+                                       (unsigned long long)(0xFFFFFFFFu - (ws + (uint32_t)i));
+        best = key > best ? key : best;
+      }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const unsigned long long q = __shfl_xor(best, o);
+      best = q > best ? q : best;
+    }
+    if ((tid & 63) == 0 && best) atomicMax(&s_key[u], best);
+    __syncthreads();                                  // key final; every reader of buf is done
+    const unsigned long long key = s_key[u];
+    if (tid == 0) a.keys[((uint64_t)f * a.N + r) * a.n_slots + slot] = key;
+    if (slot == 0) continue;                          // S0: timing only
+    const uint32_t ac = slot - 1, code = ac / a.N, t = ac % a.N;
+    const int64_t w = I.base + (int64_t)key_index(key);
+    float2 *lb = reinterpret_cast<float2 *>(buf);
+    for (int i = tid; i < M; i += T) {
+      const int64_t n = w + i;
+      lb[lds_pad(i)] = (n >= 0 && n < L) ? xf[n] : make_float2(0.0f, 0.0f);
+    }
+    __syncthreads();
+    fft_lds<LOG2M, T, 1, false>(lb, a.tw);
+    const int8_t *sg = a.s1sign + ((size_t)t * a.nac + code) * M;
+    float2 *q = a.lsq + ((((uint64_t)f * a.N + r) * a.N + t) * a.nac + code) * M;
+    for (int k = tid; k < M; k += T) {
+      const float2 Xk = lb[lds_pad(k)];
+      const int s = sg[k];
+      q[k] = s > 0 ? Xk : (s < 0 ? cneg(Xk) : make_float2(0.0f, 0.0f));
+    }
+    __syncthreads();                                  // lb readers done before the next slot
+  }
+}
+
+// one thread per (frame, subcarrier, rx-tx pair): the codes' X/S1 of lsq in code order, G and
+// this block's share of the residual variance (as ls_combine_kernel)
+__global__ __launch_bounds__(256) void ls_combine_q_kernel(LsArgs a) {
+  __shared__ double red[4];
+  const uint32_t rt = blockIdx.y, f = blockIdx.z;
+  const FrameInfo &I = a.info[f];
+  if (I.status != 0) return;
+  const uint32_t M = a.M, N = a.N;
+  const uint32_t k = blockIdx.x * 256 + threadIdx.x;
+  double nv = 0.0;
+  if (k < M) {
+    const bool occ = a.occ_index[k] >= 0;
+    const float2 *q = a.lsq + ((uint64_t)f * N * N + rt) * a.nac * M + k;
+    double sr = 0.0, si = 0.0, s2 = 0.0;
+    for (uint32_t c = 0; c < a.nac; c++) {
+      const float2 v = q[(uint64_t)c * M];
+      sr += (double)v.x;
+      si += (double)v.y;
+      s2 += (double)v.x * v.x + (double)v.y * v.y;
+    }
+    const uint32_t r = rt / N, t = rt % N;
+    const double bias = (a.keep_bias && r == t) ? 1.0 : 0.0;
+    a.G[(((uint64_t)f * M + k) * N + r) * N + t] =
+        occ ? make_float2((float)((bias + sr) * a.scale), (float)(si * a.scale))
+            : make_float2(0.0f, 0.0f);
+    if (occ) nv = s2 - (sr * sr + si * si) / (double)a.nac;
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) nv += __shfl_xor(nv, off);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = nv;
+  __syncthreads();
+  if (threadIdx.x == 0)
+    a.nv_part[(uint64_t)f * a.n_nvp + (uint64_t)rt * gridDim.x + blockIdx.x] =
+        red[0] + red[1] + red[2] + red[3];
+}
+
 // ------------------------------------------------------------------------------------
 // LS estimate, two stages. ls_kernel: one workgroup per (frame, rx, tx, code group) FFTs the
 // group's CB access codes as received on rx (the window at the search's corr index) and
@@ -612,7 +750,7 @@ __global__ __launch_bounds__(kWRowT) void weights_row_kernel(WeightArgs a) {
 // ------------------------------------------------------------------------------------
 template <int LOG2M, int LOG2F>
 static void codes_dispatch_f(const CodesArgs &a, int log2F, hipStream_t s) {
-  if constexpr (LOG2F <= 13) {
+  if constexpr (LOG2F <= 14) {
     if (log2F == LOG2F) {
       constexpr int F = 1 << LOG2F;
       const size_t shm = sizeof(float2) * lds_padded_len(F);
@@ -660,6 +798,45 @@ static void search_dispatch(const SearchArgs &a, int log2F, uint32_t nf, hipStre
 
 void launch_search(const SearchArgs &a, int log2F, uint32_t n_frames, hipStream_t s) {
   search_dispatch<7>(a, log2F, n_frames, s);
+}
+
+// search_ls_kernel instances: F = 2^10 .. 2^14 with F/M = 2, 4 or 8 (F is the smallest power
+// of two >= max(2 SL + M - 1, 2M), so F/M <= 8 for cp <= M)
+template <int LOG2F, int D>
+static bool search_ls_try(const SearchArgs &a, int log2F, int log2M, uint32_t nf, hipStream_t s) {
+  if constexpr (LOG2F <= 14) {
+    if constexpr (D <= 3) {
+      constexpr int LOG2M = LOG2F - D;
+      if (log2F == LOG2F && log2M == LOG2M) {
+        if (nf) {
+          const size_t shm = sizeof(float2) * lds_padded_len(1 << LOG2F);
+          (void)hipFuncSetAttribute((const void *)search_ls_kernel<LOG2F, LOG2M>,
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
+          dim3 grid(((a.n_slots + 1) / 2) * a.N, nf);
+          hipLaunchKernelGGL((search_ls_kernel<LOG2F, LOG2M>), grid, dim3((1 << LOG2F) / 16),
+                             shm, s, a);
+        }
+        return true;
+      }
+      return search_ls_try<LOG2F, D + 1>(a, log2F, log2M, nf, s);
+    } else {
+      return search_ls_try<LOG2F + 1, 1>(a, log2F, log2M, nf, s);
+    }
+  }
+  return false;
+}
+
+bool search_ls_supported(int log2F, int log2M) {
+  return search_ls_try<10, 1>(SearchArgs{}, log2F, log2M, 0, nullptr);
+}
+
+bool launch_search_ls(const SearchArgs &a, int log2F, int log2M, uint32_t n_frames, hipStream_t s) {
+  return search_ls_try<10, 1>(a, log2F, log2M, n_frames, s);
+}
+
+void launch_ls_combine_q(const LsArgs &a, uint32_t n_frames, hipStream_t s) {
+  hipLaunchKernelGGL(ls_combine_q_kernel, dim3((a.M + 255) / 256, a.N * a.N, n_frames), dim3(256),
+                     0, s, a);
 }
 
 template <int LOG2M>

@@ -87,7 +87,7 @@ struct ScreenArgs {
 };
 // several small 32-bit-word fills in one launch (the per-batch resets of the S&C queues,
 // flags and trigger words: one kernel instead of one memset node each)
-constexpr int kMaxFill = 8;
+constexpr int kMaxFill = 10;
 struct FillArgs {
   uint32_t *p[kMaxFill];
   uint64_t n[kMaxFill];       // words
@@ -138,8 +138,15 @@ struct SearchArgs {
   const FrameInfo *info;
   unsigned long long *keys;        // [F][N][n_slots] packed (value, ~index)
   const float2 *tw;
+  // fused search + LS terms (search_ls_kernel): slot pairs, one lag chunk per slot
+  const int8_t *s1sign;            // [N][nac][M]
+  float2 *lsq;                     // [F][N][N][nac][M] X/S1 per access code
+  uint32_t nac;
 };
 void launch_search(const SearchArgs &a, int log2F, uint32_t n_frames, hipStream_t s);
+// true when (log2F, log2M) has a search_ls_kernel instance (it then ran)
+bool launch_search_ls(const SearchArgs &a, int log2F, int log2M, uint32_t n_frames, hipStream_t s);
+bool search_ls_supported(int log2F, int log2M);
 
 // LS estimate, framing.cc:797-824 (+ training residual noise variance)
 struct LsArgs {
@@ -158,9 +165,11 @@ struct LsArgs {
   double *nv_part;                 // [F][n_nvp] residual-variance partials
   uint32_t n_nvp;                  // ceil(M / 256)
   const float2 *tw;
+  const float2 *lsq;               // search_ls_kernel's X/S1 terms (ls_combine_q_kernel)
 };
 constexpr uint32_t kLsCodesPerGroup = 4;   // access codes FFT'd per LS workgroup
 void launch_ls(const LsArgs &a, int log2M, uint32_t n_frames, hipStream_t s);
+void launch_ls_combine_q(const LsArgs &a, uint32_t n_frames, hipStream_t s);
 
 // per-subcarrier weights, framing.cc:826-831 -> 1344-1367 (+ NxN ZF/MMSE)
 struct WeightArgs {
