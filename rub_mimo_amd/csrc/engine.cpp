@@ -357,6 +357,8 @@ int run_sync(mimo_rx *h, const float2 *iq, uint64_t stride, uint32_t F, uint64_t
     static const double band_env = [] { const char *e = getenv("RMIMO_SC_BAND"); return e ? atof(e) : -1.0; }();
     a.thr = h->thr;
     a.band = band_env >= 0.0 ? band_env : sc_band(h->M);
+    static const int diag_env = [] { const char *e = getenv("RMIMO_SC_DIAG"); return e ? atoi(e) : 0; }();
+    a.diag = (uint32_t)diag_env;
     a.chunk_len = K; a.chunk_lo = chunk_lo; a.chunk_hi = nchunks;
     a.trig = h->trig.p; a.rec = h->rec.p; a.rec_stride = h->cap_chunks;
     a.cand = stream ? h->cand.p : nullptr;
@@ -400,6 +402,7 @@ int run_sync(mimo_rx *h, const float2 *iq, uint64_t stride, uint32_t F, uint64_t
       if (!h->sc_prof.p) HIPCHK(h->sc_prof.ensure(20));
       HIPCHK(hipMemsetAsync(h->sc_prof.p, 0, 20 * sizeof(unsigned long long), s));
       HIPCHK(hipMemsetAsync(h->sc_prof.p + 8, 0xFF, sizeof(unsigned long long), s));
+      if (screen) HIPCHK(hipMemsetAsync(h->sc_prof.p, 0xFF, sizeof(unsigned long long), s));
       a.prof = h->sc_prof.p;
     }
     hipEvent_t e = h->timer.begin(s);
@@ -412,13 +415,36 @@ int run_sync(mimo_rx *h, const float2 *iq, uint64_t stride, uint32_t F, uint64_t
       sa.flag = h->scr_flag.p; sa.fmin = h->scr_min.p; sa.fmax = h->scr_max.p;
       sa.count = a.hot_count; sa.hot = a.hot; sa.cap = a.hot_cap;
       launch_sc_screen(sa, F, s);
-      launch_sc_exact(a, s);
+      if (a.diag & 32) a.diag |= 16;   // diagnostics: finalize as a separate kernel
+      launch_sc_exact(a, s);   // resolves and finalises its items itself
+      if (a.diag & 32) launch_sc_finalize(a, s);
     } else {
       launch_sc(a, F, h->n_cu, s);
+      launch_sc_hot(a, s);
     }
-    launch_sc_hot(a, s);
+    static const bool cnt_env = [] { const char *e = getenv("RMIMO_SC_COUNT"); return e && e[0] == '1'; }();
+    hipStreamCaptureStatus cst = hipStreamCaptureStatusNone;
+    (void)hipStreamIsCapturing(s, &cst);
+    if (cnt_env && cst == hipStreamCaptureStatusNone) {   // diagnostics: S&C work-list size
+      uint32_t q[2] = {0, 0};
+      HIPCHK(hipMemcpyAsync(q, h->queue.p, sizeof(q), hipMemcpyDeviceToHost, s));
+      HIPCHK(hipStreamSynchronize(s));
+      fprintf(stderr, "sc_count hot_items %u (screen %d, frames %u, chunks %llu)\n", q[1],
+              screen ? 1 : 0, F, (unsigned long long)nchunks);
+    }
     h->timer.end(0, e, s);
-    if (prof_env) {   // diagnostics: per-item cycle split of the S&C kernel
+    if (prof_env && screen) {   // diagnostics: exact-kernel timeline (wall clock, 100 MHz)
+      unsigned long long v[20];
+      HIPCHK(hipMemcpyAsync(v, h->sc_prof.p, sizeof(v), hipMemcpyDeviceToHost, s));
+      HIPCHK(hipStreamSynchronize(s));
+      fprintf(stderr, "exact_prof passes %llu last_pass_end %.2f us finalize_end %.2f us "
+              "avg_pass %.2f us avg_resolve %.2f us finalizes %llu cond %.2f us record %.2f us "
+              "(%llu with candidates)\n", v[4],
+              (double)(v[1] - v[0]) / 100.0, (double)(v[2] - v[0]) / 100.0,
+              v[4] ? (double)v[3] / v[4] / 100.0 : 0.0, v[4] ? (double)v[7] / v[4] / 100.0 : 0.0,
+              v[6], v[6] ? (double)v[10] / v[6] / 100.0 : 0.0,
+              v[12] ? (double)v[11] / v[12] / 100.0 : 0.0, v[12]);
+    } else if (prof_env) {   // diagnostics: per-item cycle split of the S&C kernel
       unsigned long long v[20];
       HIPCHK(hipMemcpyAsync(v, h->sc_prof.p, sizeof(v), hipMemcpyDeviceToHost, s));
       HIPCHK(hipStreamSynchronize(s));

@@ -30,7 +30,7 @@ size_t sc_table_bytes(uint32_t M);
 // an item whose plateau candidates hinge on near-threshold samples, handed from the item
 // kernel to the resolve and finalize kernels
 struct ScHot {
-  uint32_t f, n_done, namb, pad;
+  uint32_t f, n_done, namb, arrived;   // arrived: antenna passes done (sc_exact_kernel)
   uint64_t chunk;
   int64_t c0, w0, cend;
   int64_t lo[kMaxStreams];                          // first evaluated position per antenna
@@ -64,6 +64,7 @@ struct ScArgs {
   // stream walk, and no skipping of chunks past a capture's earliest trigger
   unsigned long long *cand;
   int no_skip;
+  uint32_t diag;            // diagnostics (RMIMO_SC_DIAG bits 8/16: skip in-place resolve/finalize)
 };
 
 // S&C screen over antenna 0 (sc_screen_kernel): blocks of kScrB positions, kScrSpan positions
@@ -101,7 +102,8 @@ void launch_sc_screen(const ScreenArgs &a, uint32_t n_frames, hipStream_t s);
 void launch_sc_exact(const ScArgs &a, hipStream_t s);
 // persistent grid of n_cu x (resident blocks per CU) over the F x chunks items
 void launch_sc(const ScArgs &a, uint32_t n_frames, uint32_t n_cu, hipStream_t s);
-void launch_sc_hot(const ScArgs &a, hipStream_t s);   // resolve + finalize the hot items
+void launch_sc_hot(const ScArgs &a, hipStream_t s);
+void launch_sc_finalize(const ScArgs &a, hipStream_t s);   // plateau rule per hot item   // resolve + finalize the hot items
 
 struct PlateauArgs {
   const unsigned long long *trig;

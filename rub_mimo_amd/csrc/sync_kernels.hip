@@ -476,6 +476,55 @@ MIMO_DEV int item_conditions(const uint16_t *wbits, uint16_t (*acond)[kScT], uin
   return __syncthreads_or(surv);
 }
 
+// item_conditions for cp + 2 > kScS without block scans: only a thread whose 16 positions are
+// ones on every antenna can hold a candidate, and for it the last zero before its segment is
+// found by walking the antenna's words backwards -- at most ~(cp + 2) / 16 words: a longer run
+// of ones qualifies whatever lies further back. The walk stops at the item start, which counts
+// as a zero (item_conditions' carry = w0 - 1), so the result equals run_cond's leading-run
+// branch bit for bit.
+MIMO_DEV int item_conditions_walk(const uint16_t *wbits, uint16_t (*acond)[kScT], uint32_t n_done,
+                                  int64_t w0, int64_t c0, int64_t cend, int64_t cp) {
+  const int tid = threadIdx.x;
+  int surv = 0;
+#pragma unroll 1
+  for (int it = 0; it < kScIters; it++) {
+    const int64_t sb = w0 + (int64_t)it * kScIt + kScS * tid;
+    const int64_t lo = c0 - sb, hi = cend - sb;
+    uint32_t mask = 0;
+    if (hi > 0 && lo < kScS) {
+      const int l = lo < 0 ? 0 : (int)lo, u = hi > kScS ? kScS : (int)hi;
+      mask = ((1u << u) - 1u) & ~((1u << l) - 1u);
+    }
+    uint32_t all = mask;
+    for (uint32_t s = 0; s < n_done; s++) all &= wbits[((int)s * kScIters + it) * kScT + tid];
+    uint32_t cond = 0;
+    if (all) {
+      cond = all;
+      for (uint32_t s = 0; s < n_done && cond; s++) {
+        const uint32_t bits = wbits[((int)s * kScIters + it) * kScT + tid];
+        const uint32_t lead = bits & ~(bits + 1u) & 0xFFFFu;
+        int64_t before = w0 - 1;
+        int wt = tid, wi = it;
+        for (;;) {
+          if (--wt < 0) {
+            wt = kScT - 1;
+            if (--wi < 0) break;
+          }
+          const int64_t wsb = w0 + (int64_t)wi * kScIt + kScS * wt;
+          const uint32_t z = ~(uint32_t)wbits[((int)s * kScIters + wi) * kScT + wt] & 0xFFFFu;
+          if (z) { before = wsb + 31 - __clz(z); break; }
+          if (sb - wsb > cp + 2) { before = wsb - 1; break; }
+        }
+        const int64_t i0 = before + cp + 2 - sb;
+        cond &= i0 <= 0 ? lead : (i0 >= kScS ? 0u : lead & ~((1u << i0) - 1u));
+      }
+    }
+    acond[it][tid] = (uint16_t)cond;
+    surv |= (cond != 0);
+  }
+  return __syncthreads_or(surv);
+}
+
 // first qualifying position -> the chunk's record (run starts from the words) and trig[f].
 // s_min must be ~0 on entry.
 MIMO_DEV void item_record(const ScArgs &a, uint32_t f, uint64_t chunk, int64_t w0,
@@ -1387,6 +1436,7 @@ __global__ __launch_bounds__(kScrT) __attribute__((amdgpu_waves_per_eu(6))) void
           hp->f = f;
           hp->n_done = a.N;
           hp->namb = 0;
+          hp->arrived = 0;
           hp->chunk = (uint64_t)c;
           hp->c0 = c * K;
           hp->w0 = c * K - ((int64_t)kScSpan - K);
@@ -1397,19 +1447,47 @@ __global__ __launch_bounds__(kScrT) __attribute__((amdgpu_waves_per_eu(6))) void
   }
 }
 
+// Ring slot of position p in the exact kernel's LDS ring, which holds positions
+// [ib - M, ib + kScIt) of the current iteration at slots (M + p - w0) mod RING.
+MIMO_DEV int ring_slot(int64_t p, int64_t w0, int M, int RING) {
+  return (int)(((int64_t)M + (p - w0)) % RING);
+}
+
+constexpr int kLocAmb = kScT / 2;   // near-threshold samples resolved per iteration pass
+constexpr int kResSpread = 1024;    // positions spanned by one exact-recompute window
+
 // one (listed chunk, antenna): the item kernel's antenna pass over the iterations covering the
-// chunk's unproven range (and its cp+2 run history); bits and deferred samples -> the hot item
+// chunk's unproven range (and its cp+2 run history). Near-threshold samples are resolved in
+// place with the oracle's exact fp32 chains from the ring (two lanes per sample); the last
+// antenna workgroup of an item to finish then applies the plateau rule to the item's words
+// (item_conditions / item_record, as sc_finalize_kernel) -- no separate resolve/finalize pass.
 __global__ __launch_bounds__(kScT) __attribute__((amdgpu_waves_per_eu(2)))
 void sc_exact_kernel(ScArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char sc_dyn[];
   const int M = (int)a.M, RL = M / 2, RING = M + kScIt;
   float2 *ring = reinterpret_cast<float2 *>(sc_dyn);
   __shared__ double scan_ws[2][5][kScT / 64];
+  __shared__ long long s_amb[kLocAmb], s_sorted[kLocAmb];
+  __shared__ float s_rv[kLocAmb][3];
+  // exact-recompute tables after the ring: rtz[W] (0.5|x|^2), rtp[W] (-conj(x[k-M/2]) x[k])
+  float *rtz = reinterpret_cast<float *>(sc_dyn + sizeof(float2) * ring_pad(RING));
+  float2 *rtp = reinterpret_cast<float2 *>(rtz + ((M + kResSpread + 3) & ~3));
+  __shared__ int s_namb, s_last;
+  __shared__ __attribute__((aligned(16))) uint16_t fwb[kMaxStreams * kScIters * kScT];
+  __shared__ uint16_t acond[kScIters][kScT];
+  __shared__ long long run_ws[2][kScT / 64];
+  __shared__ long long flo[kMaxStreams];
+  __shared__ unsigned long long s_min;
   const uint32_t count = min(*a.hot_count, a.hot_cap);
-  const uint32_t s = blockIdx.y;
-  for (uint32_t slot = blockIdx.x; slot < count; slot += gridDim.x) {
+  const uint32_t s = blockIdx.x;   // antenna fastest: an item's passes are dispatched together,
+                                   // ahead of the grid's empty tail
+  for (uint32_t slot = blockIdx.y; slot < count; slot += gridDim.y) {
   ScHot *hp = a.hot + slot;
   const int tid = threadIdx.x;
+  if (tid == 0) s_namb = 0;
+  const unsigned long long t_item = a.prof ? (unsigned long long)wall_clock64() : 0ull;
+  if (a.prof && tid == 0) atomicMin(&a.prof[0], t_item);
+  unsigned long long t_res = 0;
   const uint32_t f = hp->f;
   const int64_t L = (int64_t)a.frame_len;
   const int64_t w0 = hp->w0;
@@ -1565,11 +1643,10 @@ void sc_exact_kernel(ScArgs a) {
           const double R = 0.5 * Z, R2 = R * R;
           const double q = Pre * Pre + Pim * Pim - a.thr * R2;
           if (fabs(q) <= a.band * R2 || Z <= zfloor) {
-            const uint32_t k = atomicAdd(&hp->namb, 1u);
-            if (k < (uint32_t)kAmbMax) {
-              hp->amb_n[k] = n;
-              hp->amb_s[k] = (uint8_t)s;
-              b = true;
+            const int k = atomicAdd(&s_namb, 1);
+            if (k < kLocAmb) {
+              s_amb[k] = n;
+              b = true;                // provisional: resolved below, from the ring
             } else {
               ovf |= 1u << (i + h);   // list full: this lane recomputes it below
             }
@@ -1586,10 +1663,114 @@ void sc_exact_kernel(ScArgs a) {
       if (!((double)sc_exact(x, sb + i, a.M) > a.thr)) bits &= ~(1u << i);
       if (a.n_exact) atomicAdd(a.n_exact, 1ull);
     }
+    __syncthreads();
+    const int namb = (a.diag & 8) ? 0 : min(s_namb, kLocAmb);          // uniform
+    const unsigned long long t_r0 = a.prof ? (unsigned long long)wall_clock64() : 0ull;
+    if (namb > 0) {
+      // exact fp32 recompute of this iteration's near-threshold samples (the oracle's chains,
+      // as resolve_window): ascending order, then windows of <= kResSpread positions; per
+      // window the per-sample terms are tabled from the ring by every thread, then each
+      // sample's R chain runs on a lane of waves 0-1 and its P chains on a lane of waves 2-3
+      for (int i = tid; i < namb; i += kScT) {
+        int rank = 0;
+        for (int j = 0; j < namb; j++) rank += (s_amb[j] < s_amb[i]) ? 1 : 0;
+        s_sorted[rank] = s_amb[i];
+      }
+      __syncthreads();
+      for (int k = 0; k < namb;) {                    // uniform
+        const int64_t nmin = s_sorted[k];
+        int e = k + 1;
+        while (e < namb && s_sorted[e] - nmin < kResSpread) e++;
+        const int64_t q0 = nmin - M + 1;              // table index i <-> position q0 + i
+        const int W = (int)(s_sorted[e - 1] - nmin) + M;
+        for (int i = tid; i < W; i += kScT) {
+          const float2 vv = ring[ring_pad(ring_slot(q0 + i, w0, M, RING))];
+          const float z = vv.x * vv.x + vv.y * vv.y;
+          rtz[i] = 0.5f * z;
+          if (i >= RL) {
+            const float2 dv = ring[ring_pad(ring_slot(q0 + i - RL, w0, M, RING))];
+            const float2 pp = cj_mul(dv, vv);
+            rtp[i] = make_float2((-1.0f) * pp.x, (-1.0f) * pp.y);
+          }
+        }
+        __syncthreads();
+        {
+          const int g = k + (tid & (kLocAmb - 1));
+          if (g < e) {
+            const int r = (int)(s_sorted[g] - nmin);
+            if (tid < kLocAmb) {
+              s_rv[g][0] = seq_sum(rtz + r, M);
+            } else {
+              const float2 P = seq_sum2(rtp + r + RL, RL);
+              s_rv[g][1] = P.x;
+              s_rv[g][2] = P.y;
+            }
+          }
+        }
+        __syncthreads();
+        k = e;
+      }
+      for (int g = 0; g < namb; g++) {
+        const int64_t o = s_sorted[g] - sb;
+        if (o >= 0 && o < kScS) {
+          const float Pr = s_rv[g][1], Pi = s_rv[g][2], R = s_rv[g][0];
+          const float y32 = (Pr * Pr + Pi * Pi) / (R * R);
+          if (!((double)y32 > a.thr)) bits &= ~(1u << (int)o);
+        }
+      }
+      if (tid == 0 && a.n_exact) atomicAdd(a.n_exact, (unsigned long long)namb);
+      __syncthreads();
+      if (tid == 0) s_namb = 0;
+      if (a.prof) t_res += (unsigned long long)wall_clock64() - t_r0;
+    }
     Pc_re += tot[0]; Pc_im += tot[1]; Zc += tot[2]; Cc += tot[3]; Ac = Aend;
     hp->wbits[((int)s * kScIters + it) * kScT + tid] = (uint16_t)bits;
     __syncthreads();   // every lane's phase B reads of the ring precede the next block's writes
   }
+  // the item's last antenna pass: plateau rule over every antenna's words
+  if (a.prof && tid == 0) {
+    const unsigned long long t = (unsigned long long)wall_clock64();
+    atomicMax(&a.prof[1], t);
+    atomicAdd(&a.prof[3], t - t_item);
+    atomicAdd(&a.prof[4], 1ull);
+    atomicAdd(&a.prof[7], t_res);
+  }
+  __threadfence();
+  __syncthreads();
+  if (tid == 0)
+    s_last = (__hip_atomic_fetch_add(&hp->arrived, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) ==
+              hp->n_done - 1u) ? 1 : 0;
+  __syncthreads();
+  if (s_last && !(a.diag & 16)) {
+    // the acquire of the arrival counter (agent scope) invalidated this CU's L1: plain 16-byte
+    // loads see every antenna pass's words
+    __atomic_thread_fence(__ATOMIC_ACQUIRE);
+    const uint32_t n_done = hp->n_done;
+    const uint4 *src = reinterpret_cast<const uint4 *>(hp->wbits);
+    uint4 *dst = reinterpret_cast<uint4 *>(fwb);
+    for (int i = tid; i < (int)n_done * kScIters * kScT / 8; i += kScT) dst[i] = src[i];
+    if (tid < (int)n_done) flo[tid] = hp->lo[tid];
+    if (tid == 0) s_min = ~0ull;
+    __syncthreads();
+    const unsigned long long tf0 = a.prof ? (unsigned long long)wall_clock64() : 0ull;
+    int par = 0;
+    const int any = (int64_t)a.cp + 2 > kScS
+                        ? item_conditions_walk(fwb, acond, n_done, hp->w0, hp->c0, hp->cend,
+                                               (int64_t)a.cp)
+                        : item_conditions(fwb, acond, n_done, hp->w0, hp->c0, hp->cend,
+                                          (int64_t)a.cp, run_ws, par);
+    const unsigned long long tf1 = a.prof ? (unsigned long long)wall_clock64() : 0ull;
+    if (any) item_record(a, hp->f, hp->chunk, hp->w0, fwb, acond, flo, s_min);
+    if (a.prof && tid == 0) {
+      atomicAdd(&a.prof[10], tf1 - tf0);
+      atomicAdd(&a.prof[11], (unsigned long long)wall_clock64() - tf1);
+      atomicAdd(&a.prof[12], any ? 1ull : 0ull);
+      const unsigned long long t = (unsigned long long)wall_clock64();
+      atomicMax(&a.prof[2], t);
+      atomicAdd(&a.prof[6], 1ull);
+    }
+  }
+  __syncthreads();
   }
 }
 
@@ -1642,6 +1823,12 @@ void launch_sc_hot(const ScArgs &a, hipStream_t s) {
   if (!(diag & 2)) hipLaunchKernelGGL(sc_finalize_kernel, dim3(gx), dim3(kScT), 0, s, a);
 }
 
+void launch_sc_finalize(const ScArgs &a, hipStream_t s) {
+  if (a.hot && a.hot_cap)
+    hipLaunchKernelGGL(sc_finalize_kernel, dim3(std::min<uint32_t>(a.hot_cap, 256)), dim3(kScT), 0,
+                       s, a);
+}
+
 __global__ __launch_bounds__(256) void fill_kernel(FillArgs a) {
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
   for (int k = 0; k < a.count; k++) {
@@ -1667,14 +1854,16 @@ void launch_sc_screen(const ScreenArgs &a, uint32_t n_frames, hipStream_t s) {
 }
 
 void launch_sc_exact(const ScArgs &a, hipStream_t s) {
-  const size_t shm = sc_table_bytes(a.M);
+  const size_t shm = sc_table_bytes(a.M) +
+                     sizeof(float) * (size_t)((a.M + kResSpread + 3) & ~3u) +
+                     sizeof(float2) * (size_t)(a.M + kResSpread);
   static size_t set_shm = 0;
   if (shm != set_shm) {
     (void)hipFuncSetAttribute((const void *)sc_exact_kernel,
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
     set_shm = shm;
   }
-  hipLaunchKernelGGL(sc_exact_kernel, dim3(std::min<uint32_t>(a.hot_cap, 256), a.N), dim3(kScT),
+  hipLaunchKernelGGL(sc_exact_kernel, dim3(a.N, std::min<uint32_t>(a.hot_cap, 256)), dim3(kScT),
                      shm, s, a);
 }
 
