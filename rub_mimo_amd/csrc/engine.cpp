@@ -439,11 +439,14 @@ int run_sync(mimo_rx *h, const float2 *iq, uint64_t stride, uint32_t F, uint64_t
       HIPCHK(hipStreamSynchronize(s));
       fprintf(stderr, "exact_prof passes %llu last_pass_end %.2f us finalize_end %.2f us "
               "avg_pass %.2f us avg_resolve %.2f us finalizes %llu cond %.2f us record %.2f us "
-              "(%llu with candidates)\n", v[4],
+              "(%llu with candidates) slowest pass %.2f us (%llu iterations, resolve %.2f us) "
+              "max windows/pass %llu (samples %llu) total samples %llu\n", v[4],
               (double)(v[1] - v[0]) / 100.0, (double)(v[2] - v[0]) / 100.0,
               v[4] ? (double)v[3] / v[4] / 100.0 : 0.0, v[4] ? (double)v[7] / v[4] / 100.0 : 0.0,
               v[6], v[6] ? (double)v[10] / v[6] / 100.0 : 0.0,
-              v[12] ? (double)v[11] / v[12] / 100.0 : 0.0, v[12]);
+              v[12] ? (double)v[11] / v[12] / 100.0 : 0.0, v[12], (double)(v[13] >> 32) / 100.0,
+              (v[13] >> 24) & 0xFF, (double)(v[13] & 0xFFFFFF) / 100.0, v[14] >> 32,
+              v[14] & 0xFFFFFFFFull, v[15]);
     } else if (prof_env) {   // diagnostics: per-item cycle split of the S&C kernel
       unsigned long long v[20];
       HIPCHK(hipMemcpyAsync(v, h->sc_prof.p, sizeof(v), hipMemcpyDeviceToHost, s));

@@ -209,6 +209,10 @@ MIMO_DEV uint32_t run_cond(uint32_t bits, int64_t sb, long long &carry, int64_t 
 // sequential fp32 sum q[0] + q[1] + ... + q[n-1], in that order. Scalar head up to 16-byte
 // alignment, then 16-byte reads with the next 16 terms in flight while 16 are added (the
 // dependent-add latency, ~7 cycles on gfx950, is the bound: ~9 cycles per term measured).
+// Sequential fp32 sums in the oracle's order, oldest -> newest, from an LDS table. The chain
+// of dependent adds is the critical path, so the table reads run three 16-term blocks ahead
+// (the loop is unrolled by three so the blocks rotate through fixed registers; a read past the
+// last block is clamped onto it and never consumed).
 MIMO_DEV float seq_sum(const float *q, int n) {
   float acc = 0.0f;
   const int h = min(n, (int)((4u - (((uint32_t)(uintptr_t)q >> 2) & 3u)) & 3u));
@@ -216,17 +220,27 @@ MIMO_DEV float seq_sum(const float *q, int n) {
   const float4 *qa = reinterpret_cast<const float4 *>(q + h);
   const int m = n - h, nb = m >> 4;
   if (nb > 0) {
-    float4 n0 = qa[0], n1 = qa[1], n2 = qa[2], n3 = qa[3];
-    for (int b = 0; b < nb; b++) {
-      const float4 c0 = n0, c1 = n1, c2 = n2, c3 = n3;
-      if (b + 1 < nb) {
-        n0 = qa[4 * b + 4]; n1 = qa[4 * b + 5]; n2 = qa[4 * b + 6]; n3 = qa[4 * b + 7];
+    auto ld = [&](float4 (&d)[4], int b) {
+      const int bb = b < nb ? b : nb - 1;
+#pragma unroll
+      for (int i = 0; i < 4; i++) d[i] = qa[4 * bb + i];
+    };
+    auto add = [&](const float4 (&d)[4]) {
+#pragma unroll
+      for (int i = 0; i < 4; i++) {
+        acc = acc + d[i].x; acc = acc + d[i].y; acc = acc + d[i].z; acc = acc + d[i].w;
       }
-      acc = acc + c0.x; acc = acc + c0.y; acc = acc + c0.z; acc = acc + c0.w;
-      acc = acc + c1.x; acc = acc + c1.y; acc = acc + c1.z; acc = acc + c1.w;
-      acc = acc + c2.x; acc = acc + c2.y; acc = acc + c2.z; acc = acc + c2.w;
-      acc = acc + c3.x; acc = acc + c3.y; acc = acc + c3.z; acc = acc + c3.w;
+    };
+    float4 A[4], B[4], C[4];
+    ld(A, 0); ld(B, 1); ld(C, 2);
+    int b = 0;
+    for (; b + 3 <= nb; b += 3) {
+      add(A); ld(A, b + 3);
+      add(B); ld(B, b + 4);
+      add(C); ld(C, b + 5);
     }
+    if (b < nb) add(A);
+    if (b + 1 < nb) add(B);
   }
   for (int k = h + 16 * nb; k < n; k++) acc = acc + q[k];
   return acc;
@@ -240,17 +254,27 @@ MIMO_DEV float2 seq_sum2(const float2 *q, int n) {
   const float4 *qa = reinterpret_cast<const float4 *>(q + h);
   const int m = n - h, nb = m >> 3;
   if (nb > 0) {
-    float4 n0 = qa[0], n1 = qa[1], n2 = qa[2], n3 = qa[3];
-    for (int b = 0; b < nb; b++) {
-      const float4 c0 = n0, c1 = n1, c2 = n2, c3 = n3;
-      if (b + 1 < nb) {
-        n0 = qa[4 * b + 4]; n1 = qa[4 * b + 5]; n2 = qa[4 * b + 6]; n3 = qa[4 * b + 7];
+    auto ld = [&](float4 (&d)[4], int b) {
+      const int bb = b < nb ? b : nb - 1;
+#pragma unroll
+      for (int i = 0; i < 4; i++) d[i] = qa[4 * bb + i];
+    };
+    auto add = [&](const float4 (&d)[4]) {
+#pragma unroll
+      for (int i = 0; i < 4; i++) {
+        ax = ax + d[i].x; ay = ay + d[i].y; ax = ax + d[i].z; ay = ay + d[i].w;
       }
-      ax = ax + c0.x; ay = ay + c0.y; ax = ax + c0.z; ay = ay + c0.w;
-      ax = ax + c1.x; ay = ay + c1.y; ax = ax + c1.z; ay = ay + c1.w;
-      ax = ax + c2.x; ay = ay + c2.y; ax = ax + c2.z; ay = ay + c2.w;
-      ax = ax + c3.x; ay = ay + c3.y; ax = ax + c3.z; ay = ay + c3.w;
+    };
+    float4 A[4], B[4], C[4];
+    ld(A, 0); ld(B, 1); ld(C, 2);
+    int b = 0;
+    for (; b + 3 <= nb; b += 3) {
+      add(A); ld(A, b + 3);
+      add(B); ld(B, b + 4);
+      add(C); ld(C, b + 5);
     }
+    if (b < nb) add(A);
+    if (b + 1 < nb) add(B);
   }
   for (int k = h + 8 * nb; k < n; k++) { ax = ax + q[k].x; ay = ay + q[k].y; }
   return make_float2(ax, ay);
@@ -1488,6 +1512,7 @@ void sc_exact_kernel(ScArgs a) {
   const unsigned long long t_item = a.prof ? (unsigned long long)wall_clock64() : 0ull;
   if (a.prof && tid == 0) atomicMin(&a.prof[0], t_item);
   unsigned long long t_res = 0;
+  uint32_t n_win = 0, n_smp = 0;   // diagnostics: resolve windows and samples of this pass
   const uint32_t f = hp->f;
   const int64_t L = (int64_t)a.frame_len;
   const int64_t w0 = hp->w0;
@@ -1709,7 +1734,9 @@ void sc_exact_kernel(ScArgs a) {
         }
         __syncthreads();
         k = e;
+        n_win++;
       }
+      n_smp += namb;
       for (int g = 0; g < namb; g++) {
         const int64_t o = s_sorted[g] - sb;
         if (o >= 0 && o < kScS) {
@@ -1734,6 +1761,12 @@ void sc_exact_kernel(ScArgs a) {
     atomicAdd(&a.prof[3], t - t_item);
     atomicAdd(&a.prof[4], 1ull);
     atomicAdd(&a.prof[7], t_res);
+    // slowest pass: duration (10 ns), iterations, resolve time (10 ns), packed
+    const unsigned long long dur = t - t_item;
+    atomicMax(&a.prof[13], (dur << 32) | ((unsigned long long)(it_hi - it_lo + 1) << 24) |
+                               (t_res & 0xFFFFFFull));
+    atomicMax(&a.prof[14], ((unsigned long long)n_win << 32) | n_smp);
+    atomicAdd(&a.prof[15], (unsigned long long)n_smp);
   }
   __threadfence();
   __syncthreads();
