@@ -81,6 +81,9 @@ def parse():
                          "scatter: rank 0 scatters sc16 wire captures every step (timed)")
     ap.add_argument("--scatter-steps", type=int, default=5,
                     help="steps of the secondary rank-0 scatter leg when N > 1 (0: skip)")
+    ap.add_argument("--cfo", type=float, default=0.0,
+                    help="apply this carrier-frequency offset (subcarrier spacings) to the "
+                         "synthetic captures and turn on the receiver's opt-in CFO correction")
     ap.add_argument("--cpu-baseline", type=int, default=1, help="0 to skip the oracle timing")
     ap.add_argument("--cpu-threads", type=int, default=0,
                     help="threads of the multi-core CPU baseline (0: the box's core share)")
@@ -272,9 +275,13 @@ def main():
         ref_starts = None
         slot_len = [[syn.frame_len(frame_id0 + f)] for f in range(F)]
     all_len = sum(sum(r) for r in slot_len)          # transmitted samples per antenna
+    if args.cfo:
+        from rub_mimo_amd.receiver import cfo_derotate
+        cfo_derotate(iq, L, F * N, L, 0, -args.cfo, M, stream=sh)   # a CFO of +args.cfo
 
     rx = Receiver(RxParams(M=M, cp_len=cp, num_streams=N, num_access_codes=nac, pid_max=pid,
-                           detector=det, qam_order=args.qam), stream=sh)
+                           detector=det, qam_order=args.qam, cfo_correct=args.cfo != 0.0),
+                  stream=sh)
     m_occ = rx.M_occ
     out_sym = torch.empty((F * K, N, pid, m_occ), dtype=torch.complex64, device=dev)
     out_idx = torch.empty((F * K, N, pid, m_occ), dtype=torch.uint8, device=dev)
@@ -484,6 +491,7 @@ def main():
                    "captures_per_step_per_gpu": F, "frames_per_capture": K if c5 else 1,
                    "ingest": ("rank-0 sc16 scatter over RCCL P2P" if timed_scatter
                               else "resident in HBM"),
+                   "cfo": args.cfo,
                    "parallelism": ("%d streams over %d GPU(s)" % (args.frames, world) if c5 else
                                    "frames sharded across %d GPU(s), no collective" % world)},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,

@@ -71,6 +71,12 @@ typedef struct mimo_rx_config {
   uint32_t siso_tx, siso_rx;  /* set_siso_tx / set_siso_rx (framing.h:211-212) */
   double plateau_threshold;   /* PLATEAU_THREASHOLD (config.h:87), 0.95 */
   uint32_t qam_order;         /* square Gray QAM for the fused demap/EVM stage (4..256) */
+  int32_t cfo_correct;        /* batched path, opt-in (absent from the reference: FIXME at
+                                 framing.cc:486): 1 = estimate each synced frame's CFO from the
+                                 S0 half-period correlation ending at its trigger, summed over
+                                 the antennas, and derotate its window (into a device scratch
+                                 copy; the caller's capture is not modified) before search, LS
+                                 and decode. 0 = off (the reference's behaviour). */
 } mimo_rx_config;
 
 typedef struct mimo_rx mimo_rx;
@@ -153,7 +159,7 @@ typedef struct mimo_frame_result {
   uint64_t plateau_start[MIMO_MAX_STREAMS];
   uint64_t plateau_end[MIMO_MAX_STREAMS];
   float noise_var;
-  float pad_;
+  float cfo_eps;                           /* cfo_correct: estimated CFO, subcarrier spacings */
   double evm_num[MIMO_MAX_STREAMS];        /* sum |y - s|^2 over kept symbols */
   double evm_den[MIMO_MAX_STREAMS];        /* sum |s|^2 */
   uint64_t errors[MIMO_MAX_STREAMS];       /* symbol errors (ref_mode 1/2) */

@@ -30,7 +30,7 @@ class RxConfig(C.Structure):
                 ("detector", C.c_int32), ("noise_var", C.c_float),
                 ("keep_identity_bias", C.c_int32), ("siso_tx", C.c_uint32),
                 ("siso_rx", C.c_uint32), ("plateau_threshold", C.c_double),
-                ("qam_order", C.c_uint32)]
+                ("qam_order", C.c_uint32), ("cfo_correct", C.c_int32)]
 
 
 class Batch(C.Structure):
@@ -47,7 +47,7 @@ class FrameResult(C.Structure):
                 ("sync_index", C.c_uint64), ("num_samples_processed", C.c_uint64),
                 ("plateau_start", C.c_uint64 * MAX_STREAMS),
                 ("plateau_end", C.c_uint64 * MAX_STREAMS), ("noise_var", C.c_float),
-                ("pad_", C.c_float), ("evm_num", C.c_double * MAX_STREAMS),
+                ("cfo_eps", C.c_float), ("evm_num", C.c_double * MAX_STREAMS),
                 ("evm_den", C.c_double * MAX_STREAMS), ("errors", C.c_uint64 * MAX_STREAMS),
                 ("origin", C.c_uint64), ("capture", C.c_uint32), ("ref_frame", C.c_uint32)]
 

@@ -12,6 +12,8 @@
 // their phase accuracy.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+#include <cmath>
 #include <cstdint>
 
 #include "kernels.hpp"
@@ -65,7 +67,143 @@ __global__ __launch_bounds__(kCfoThreads) void cfo_derotate_kernel(float2 *__res
   *p = make_float2((float)(v.x * c - v.y * s), (float)(v.x * s + v.y * c));
 }
 
+// Batched path (mimo_rx_config.cfo_correct), two stages per synced frame, sums over the
+// antennas in fp64:
+//  1. coarse, |eps| < 1, before the search: the S0 half-period correlation over the S&C window
+//     ending at the trigger (x[t-M+1 .. t] lies in the M/2-periodic S0, cyclic prefix included,
+//     since y[t] > thr on every antenna): eps0 = arg(P) / pi; the frame's window is derotated by
+//     eps0 into a scratch capture that search, LS, weights and decode read.
+//  2. fine, after the search: one S0 leaves a residual of ~1e-4 subcarrier spacings at 30 dB,
+//     ~0.3-1 rad of drift over 1000 symbols (and a phase spread across the access codes that
+//     the MMSE noise estimate would read as noise). The cyclic prefixes of the data symbols --
+//     their positions known from the search (base + i0 + s SL, framing.cc:857) -- correlate
+//     conj(x[k]) x[k + M] over each prefix's interior: delta = arg(P) / (2 pi) on the coarse-
+//     corrected samples. The LS terms are rotated by delta at their code windows
+//     (ls_combine_q_kernel) and the data region is derotated by delta, both about base.
+// Blocks sum fixed symbol subsets into partials, combined in fixed order by the rotation
+// kernels (bitwise reproducible).
+constexpr uint32_t kCfoMargin = 4;   // prefix samples skipped at each end
+
+MIMO_DEV bool cfo_live(const FrameInfo &I) { return I.status == 0 || I.status == 2; }
+
+// replay start from the search's last access-code key (framing.cc:857), as weights_kernel
+MIMO_DEV int64_t cfo_i0(const CfoBatchArgs &a, uint32_t f) {
+  const unsigned long long key =
+      a.keys[((uint64_t)f * a.N + (a.N - 1)) * a.n_slots + a.n_slots - 1];
+  const uint32_t ci = key ? (0xFFFFFFFFu - (uint32_t)(key & 0xFFFFFFFFull)) : 0u;
+  return (int64_t)ci + a.M;
+}
+
+template <int STAGE>
+__global__ __launch_bounds__(kCfoThreads) void cfo_batch_est_kernel(CfoBatchArgs a) {
+  const uint32_t f = blockIdx.y, b = blockIdx.x;
+  const FrameInfo &I = a.info[f];
+  __shared__ double sre[kCfoThreads], sim[kCfoThreads];
+  const bool live = STAGE == 1 ? cfo_live(I) : I.status == 0;
+  double re = 0.0, im = 0.0;
+  const int64_t L = (int64_t)a.frame_len;
+  const float2 *src = STAGE == 1 ? a.iq : a.out;
+  if (live) {
+    for (uint32_t r = 0; r < a.N; r++) {
+      const float2 *row = src + ((uint64_t)I.cap * a.N + r) * a.stride;
+      if (STAGE == 1) {
+        const uint32_t half = a.M / 2;
+        const int64_t start = (int64_t)I.trigger - (int64_t)a.M + 1;
+        for (uint32_t n = b * kCfoThreads + threadIdx.x; n < half; n += kCfoBlocks * kCfoThreads) {
+          const int64_t k = start + n;
+          if (k < 0 || k + half >= L) continue;
+          const float2 u = row[k], v = row[k + half];
+          re += (double)u.x * v.x + (double)u.y * v.y;
+          im += (double)u.x * v.y - (double)u.y * v.x;
+        }
+      } else {
+        const uint32_t inner = a.cp > 2 * kCfoMargin ? a.cp - 2 * kCfoMargin : 0;
+        const int64_t d0 = I.base + cfo_i0(a, f);             // data symbol 0's prefix
+        for (uint32_t sym = b; sym < a.n_data; sym += kCfoBlocks) {
+          const int64_t c0 = d0 + (int64_t)sym * a.SL + kCfoMargin;
+          for (uint32_t n = threadIdx.x; n < inner; n += kCfoThreads) {
+            const int64_t k = c0 + n;
+            if (k < 0 || k + a.M >= L) continue;
+            const float2 u = row[k], v = row[k + a.M];
+            re += (double)u.x * v.x + (double)u.y * v.y;
+            im += (double)u.x * v.y - (double)u.y * v.x;
+          }
+        }
+      }
+    }
+  }
+  sre[threadIdx.x] = re;
+  sim[threadIdx.x] = im;
+  __syncthreads();
+  for (int w = kCfoThreads / 2; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w) {
+      sre[threadIdx.x] += sre[threadIdx.x + w];
+      sim[threadIdx.x] += sim[threadIdx.x + w];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    double *p = a.part + (((uint64_t)f * 2 + (STAGE - 1)) * kCfoBlocks + b) * 2;
+    p[0] = sre[0];
+    p[1] = sim[0];
+  }
+}
+
+// x[n] exp(-j 2 pi (eps / M)(n - base)) over [n0, n0 + len) of every antenna: stage 1 from the
+// input into the scratch capture over the frame's window (n0 = base); stage 2 in place, over
+// the data region (n0 = base + i0; the LS terms were corrected to the same reference in
+// ls_combine_q_kernel) or, before a separate LS pass, over the whole window
+template <int STAGE>
+__global__ __launch_bounds__(kCfoThreads) void cfo_batch_rot_kernel(CfoBatchArgs a) {
+  FrameInfo &I = a.info[blockIdx.z];
+  if (STAGE == 1 ? !cfo_live(I) : I.status != 0) return;
+  const double eps = cfo_stage_eps(a.part, blockIdx.z, STAGE);
+  const double eps0 = STAGE == 2 ? cfo_stage_eps(a.part, blockIdx.z, 1) : 0.0;
+  if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) I.cfo_eps = (float)(eps + eps0);
+  const double nu = eps / (double)a.M;
+  const uint64_t off = ((uint64_t)I.cap * a.N + blockIdx.y) * a.stride;
+  const bool whole = STAGE == 1 || a.rot_window;
+  const int64_t n0 = whole ? I.base : I.base + cfo_i0(a, blockIdx.z);
+  const int64_t nref = I.base;
+  const uint64_t len = whole ? a.len : (uint64_t)a.n_data * a.SL + 64;
+  const float2 *src = STAGE == 1 ? a.iq : a.out;
+  for (uint64_t i = (uint64_t)blockIdx.x * kCfoThreads + threadIdx.x; i < len;
+       i += (uint64_t)gridDim.x * kCfoThreads) {
+    const int64_t n = n0 + (int64_t)i;
+    if (n < 0 || n >= (int64_t)a.frame_len) continue;
+    double ph = -2.0 * nu * (double)(n - nref);                // in units of pi, fp64
+    ph -= 2.0 * rint(ph * 0.5);                                // [-1, 1]: fp32 from here on
+    float s, c;
+    sincospif((float)ph, &s, &c);
+    const float2 v = src[off + n];
+    a.out[off + n] = make_float2(v.x * c - v.y * s, v.x * s + v.y * c);
+  }
+}
+
 }  // namespace
+
+size_t cfo_batch_part_doubles(uint32_t n_frames) { return (size_t)n_frames * 2 * kCfoBlocks * 2; }
+
+void launch_cfo_batch(const CfoBatchArgs &a, uint32_t n_frames, int stage, hipStream_t s) {
+  if (n_frames == 0) return;
+  const uint32_t blocks =
+      (uint32_t)std::min<uint64_t>((a.len + kCfoThreads - 1) / kCfoThreads, 2048);
+  if (stage == 1) {
+    cfo_batch_est_kernel<1><<<dim3(kCfoBlocks, n_frames), kCfoThreads, 0, s>>>(a);
+    cfo_batch_rot_kernel<1><<<dim3(blocks, a.N, n_frames), kCfoThreads, 0, s>>>(a);
+  } else {
+    cfo_batch_est_kernel<2><<<dim3(kCfoBlocks, n_frames), kCfoThreads, 0, s>>>(a);
+    if (a.rot_window)
+      cfo_batch_rot_kernel<2><<<dim3(blocks, a.N, n_frames), kCfoThreads, 0, s>>>(a);
+  }
+}
+
+void launch_cfo_batch_rot2(const CfoBatchArgs &a, uint32_t n_frames, hipStream_t s) {
+  if (n_frames == 0) return;
+  const uint64_t span = (uint64_t)a.n_data * a.SL + 64;
+  const uint32_t blocks = (uint32_t)std::min<uint64_t>((span + kCfoThreads - 1) / kCfoThreads, 2048);
+  cfo_batch_rot_kernel<2><<<dim3(blocks, a.N, n_frames), kCfoThreads, 0, s>>>(a);
+}
 
 bool launch_cfo_corr(const void *x, uint64_t stride, uint32_t rows, uint64_t start,
                      uint32_t half, double *d_out, hipStream_t s) {

@@ -91,6 +91,20 @@ MIMO_DEV uint32_t qam_demap(float2 y, const Qam &q) {
 }
 
 // ---------------- per-frame bookkeeping shared by the stages ----------------
+// opt-in CFO partial correlations: [F][2 stages][kCfoBlocks][2] doubles (cfo_kernels.hip);
+// stage 1 -> eps0 = arg / pi, stage 2 -> delta = arg / (2 pi), summed in fixed block order
+constexpr int kCfoBlocks = 32;
+MIMO_DEV double cfo_stage_eps(const double *part, uint32_t f, int stage) {
+  const double *p = part + ((uint64_t)f * 2 + (uint64_t)(stage - 1)) * kCfoBlocks * 2;
+  double re = 0.0, im = 0.0;
+  for (int b = 0; b < kCfoBlocks; b++) {
+    re += p[2 * b];
+    im += p[2 * b + 1];
+  }
+  if (re == 0.0 && im == 0.0) return 0.0;
+  return atan2(im, re) / (stage == 1 ? M_PI : 2.0 * M_PI);
+}
+
 struct FrameInfo {
   int32_t status;          // MIMO_FRAME_*
   uint32_t n_sym;          // decode callbacks available in the window
@@ -106,6 +120,8 @@ struct FrameInfo {
                            // re-arm point of a back-to-back stream); positions are absolute
   uint32_t cap;            // capture holding the frame (f when each capture is one frame)
   uint32_t ref;            // reference frame (ref_mode 1 index row, ref_mode 2 frame id - id0)
+  float cfo_eps;           // opt-in CFO estimate (subcarrier spacings), 0 when off
+  uint32_t pad_;
 };
 
 }  // namespace mimo

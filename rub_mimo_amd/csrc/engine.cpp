@@ -191,6 +191,9 @@ struct mimo_rx {
   int log2M = 0, log2F = 0;
   uint32_t F = 0, lagc = 0, n_lagc = 0, n_slots = 0;
   bool search_ls = false;               // fused search + LS (search_ls_kernel) for this geometry
+  bool cfo = false;                     // opt-in CFO estimate + derotation (batched path)
+  DevBuf<float2> cfo_iq;                // derotated scratch capture
+  DevBuf<double> cfo_eps;
   uint32_t n_cu = 256;
   int det = 0;
   float noise_var = -1.0f;
@@ -252,7 +255,7 @@ struct mimo_rx {
   hipStream_t g_stream = nullptr;
   bool g_valid = false;
   hipGraphExec_t g_exec = nullptr;
-  std::array<const void *, 23> g_sig{};
+  std::array<const void *, 25> g_sig{};
 };
 
 struct mimo_tx {
@@ -483,7 +486,7 @@ int run_sync(mimo_rx *h, const float2 *iq, uint64_t stride, uint32_t F, uint64_t
 }
 
 int run_estimate(mimo_rx *h, const float2 *iq, uint64_t stride, uint32_t F, uint64_t frame_len,
-                 hipStream_t s, bool keys_zeroed = false) {
+                 hipStream_t s, bool keys_zeroed = false, CfoBatchArgs *cfo = nullptr) {
   if (!keys_zeroed)
     HIPCHK(hipMemsetAsync(h->keys.p, 0, sizeof(unsigned long long) * F * h->N * h->n_slots, s));
   SearchArgs sa{};
@@ -508,6 +511,11 @@ int run_estimate(mimo_rx *h, const float2 *iq, uint64_t stride, uint32_t F, uint
     hipEvent_t e = h->timer.begin(s);
     launch_search_ls(sa, h->log2F, h->log2M, F, s);
     h->timer.end(2, e, s);
+    if (cfo) {   // opt-in CFO stage 2: residual from the data prefixes; LS terms rotated below
+      cfo->keys = h->keys.p; cfo->n_slots = h->n_slots; cfo->rot_window = 0;
+      launch_cfo_batch(*cfo, F, 2, s);
+      la.cfo_part = cfo->part;
+    }
     e = h->timer.begin(s);
     launch_ls_combine_q(la, F, s);
     h->timer.end(3, e, s);
@@ -515,6 +523,10 @@ int run_estimate(mimo_rx *h, const float2 *iq, uint64_t stride, uint32_t F, uint
     hipEvent_t e = h->timer.begin(s);
     launch_search(sa, h->log2F, F, s);
     h->timer.end(2, e, s);
+    if (cfo) {   // opt-in CFO stage 2 before a separate LS pass: the whole window in place
+      cfo->keys = h->keys.p; cfo->n_slots = h->n_slots; cfo->rot_window = 1;
+      launch_cfo_batch(*cfo, F, 2, s);
+    }
     {
       const size_t need = (size_t)F * h->N * h->N * la.n_groups * 3 * h->M;
       if (need > h->cap_lspart) {
@@ -647,6 +659,7 @@ int mimo_rx_create(const mimo_rx_config *cfg, void *hip_stream, mimo_rx **out) {
   h->keep_bias = cfg->keep_identity_bias ? 1 : 0;
   h->siso_tx = cfg->siso_tx; h->siso_rx = cfg->siso_rx;
   h->thr = cfg->plateau_threshold;
+  h->cfo = cfg->cfo_correct != 0;
   h->qam = make_qam(q);
   h->acb = (uint64_t)h->SL * (h->nac * N + 4);     // framing.cc:284
   h->txl = (uint64_t)h->pid * h->SL;               // framing.cc:285
@@ -1005,7 +1018,26 @@ static int run_batch(mimo_rx *h, const mimo_batch *b, hipStream_t s) {
   const uint32_t fpc = batch_fpc(b), slots = b->n_frames * fpc;
   int rc = run_sync(h, iq, b->stride, b->n_frames, b->frame_len, 0, true, s, fpc,
                     fpc > 1 ? b->d_ref_starts : nullptr, b->ref_stride, true);
-  if (!rc) rc = run_estimate(h, iq, b->stride, slots, b->frame_len, s, true);
+  CfoBatchArgs ca{};
+  if (!rc && h->cfo) {
+    // opt-in CFO, stage 1: coarse estimate per synced frame at its trigger, window derotated
+    // into a scratch capture that search, LS, weights and decode read (S&C ran on the raw
+    // samples: |P| and R do not depend on a frequency offset)
+    const size_t need = (size_t)b->n_frames * h->N * b->stride;
+    if (h->cfo_iq.ensure(need) != hipSuccess ||
+        h->cfo_eps.ensure(cfo_batch_part_doubles(slots)) != hipSuccess)
+      return fail(MIMO_ERR_NOMEM, "cfo scratch allocation failed");
+    ca.iq = iq; ca.out = h->cfo_iq.p; ca.stride = b->stride; ca.frame_len = b->frame_len;
+    ca.len = h->win_len + 64; ca.N = h->N; ca.M = h->M; ca.cp = h->cp; ca.SL = h->SL;
+    ca.n_codes = h->N * h->nac; ca.n_data = h->pid + 2; ca.info = h->info.p;
+    ca.part = h->cfo_eps.p;
+    launch_cfo_batch(ca, slots, 1, s);
+    iq = h->cfo_iq.p;
+  }
+  if (!rc) rc = run_estimate(h, iq, b->stride, slots, b->frame_len, s, true,
+                             h->cfo ? &ca : nullptr);
+  if (!rc && h->cfo && h->search_ls)   // stage 2's data-region derotation (fused LS path)
+    launch_cfo_batch_rot2(ca, slots, s);
   if (!rc)
     rc = run_decode(h, iq, b->stride, slots, b->frame_len, b->max_out_syms,
                     reinterpret_cast<float2 *>(b->d_out_sym),
@@ -1020,11 +1052,11 @@ static int run_batch(mimo_rx *h, const mimo_batch *b, hipStream_t s) {
 // the configuration and F (S&C items and hot items are pulled from device-side queues), so
 // the graph stays valid. Not used while stage timing or a diagnostic counter is on.
 // every device pointer a captured batch bakes into its kernels' arguments
-static std::array<const void *, 23> ws_signature(const mimo_rx *h) {
+static std::array<const void *, 25> ws_signature(const mimo_rx *h) {
   return {h->trig.p, h->keys.p, h->rec.p, h->info.p, h->G.p, h->W.p, h->gain.p, h->nvp.p,
           h->evm_part.p, h->evm_out.p, h->n_exact.p, h->queue.p, h->hot.p, h->lspart.p,
           h->tw, h->codes.codespec.p, h->scr_flag.p, h->scr_min.p, h->scr_max.p, h->nrec.p,
-          h->cand.p, h->certfail.p, h->lsq.p};
+          h->cand.p, h->certfail.p, h->lsq.p, h->cfo_iq.p, h->cfo_eps.p};
 }
 
 static bool same_batch(const mimo_batch &x, const mimo_batch &y) {
@@ -1115,6 +1147,7 @@ int mimo_rx_batch_results(mimo_rx *h, mimo_frame_result *out, uint32_t F) {
     r.sync_index = synced ? I.sync_index - o : 0;
     r.num_samples_processed = I.nsp;
     r.noise_var = I.noise_var;
+    r.cfo_eps = h->cfo ? I.cfo_eps : 0.0f;
     r.origin = o;
     r.capture = I.cap;
     r.ref_frame = I.ref;

@@ -168,6 +168,8 @@ struct LsArgs {
   uint32_t n_nvp;                  // ceil(M / 256)
   const float2 *tw;
   const float2 *lsq;               // search_ls_kernel's X/S1 terms (ls_combine_q_kernel)
+  const double *cfo_part;          // opt-in CFO: rotate code c's term by the stage-2 residual
+  uint32_t M_cfo;                  // (M, window-relative; null: off)
 };
 constexpr uint32_t kLsCodesPerGroup = 4;   // access codes FFT'd per LS workgroup
 void launch_ls(const LsArgs &a, int log2M, uint32_t n_frames, hipStream_t s);
@@ -190,6 +192,26 @@ struct WeightArgs {
   FrameInfo *info;
 };
 void launch_weights(const WeightArgs &a, uint32_t n_frames, hipStream_t s);
+
+// opt-in CFO of the batched path (cfo_kernels.hip)
+struct CfoBatchArgs {
+  const float2 *iq;
+  float2 *out;                     // scratch capture, same layout as iq
+  uint64_t stride, frame_len, len; // len: window samples derotated from each frame's base
+  uint32_t N, M, cp, SL;
+  uint32_t n_codes;                // access-code symbols (N * nac) after S0
+  uint32_t n_data;                 // data symbols in a window (PID + 2)
+  uint32_t n_slots;
+  int rot_window;                  // stage 2 derotates the whole window (LS not yet run)
+  FrameInfo *info;
+  const unsigned long long *keys;  // search keys (stage 2 timing)
+  double *part;                    // [F][2 stages][blocks][2] partial correlations
+};
+size_t cfo_batch_part_doubles(uint32_t n_frames);
+// stage 1 (after S&C): coarse estimate, window derotated into `out`; stage 2 (after the
+// weights): fine residual from the data symbols' prefixes, data region of `out` in place
+void launch_cfo_batch(const CfoBatchArgs &a, uint32_t n_frames, int stage, hipStream_t s);
+void launch_cfo_batch_rot2(const CfoBatchArgs &a, uint32_t n_frames, hipStream_t s);
 
 // replay decode, framing.cc:535-589 / 508-533 fused with square-QAM demap + EVM
 struct DecodeArgs {

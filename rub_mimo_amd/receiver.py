@@ -33,6 +33,7 @@ class RxParams:
     plateau_threshold: float = 0.95
     qam_order: int = 64
     p: np.ndarray = field(default=None)
+    cfo_correct: bool = False
 
     @property
     def SL(self):
@@ -107,7 +108,7 @@ class Receiver:
         cfg = _lib.RxConfig(P.M, P.cp_len, P.num_streams, P.num_access_codes, P.pid_max,
                             p.ctypes.data, b0.ctypes.data, b1.ctypes.data, P.detector,
                             P.noise_var, 1 if P.keep_identity_bias else 0, P.siso_tx, P.siso_rx,
-                            P.plateau_threshold, P.qam_order)
+                            P.plateau_threshold, P.qam_order, 1 if P.cfo_correct else 0)
         h = C.c_void_p()
         check(lib().mimo_rx_create(C.byref(cfg), stream, C.byref(h)), "mimo_rx_create")
         self._h = h
@@ -223,7 +224,7 @@ class Receiver:
                 status=r.status, n_sym=r.n_sym, trigger=r.trigger, sync_index=r.sync_index,
                 num_samples_processed=r.num_samples_processed,
                 plateau_start=list(r.plateau_start)[:N], plateau_end=list(r.plateau_end)[:N],
-                noise_var=r.noise_var, evm_num=np.array(r.evm_num[:N]),
+                noise_var=r.noise_var, cfo_eps=r.cfo_eps, evm_num=np.array(r.evm_num[:N]),
                 evm_den=np.array(r.evm_den[:N]), errors=np.array(r.errors[:N], np.int64),
                 origin=r.origin, capture=r.capture, ref_frame=r.ref_frame))
         return out
