@@ -84,6 +84,12 @@ def parse():
     ap.add_argument("--cfo", type=float, default=0.0,
                     help="apply this carrier-frequency offset (subcarrier spacings) to the "
                          "synthetic captures and turn on the receiver's opt-in CFO correction")
+    ap.add_argument("--sample-format", default="fc32", choices=["fc32", "sc16"],
+                    help="resident capture format: fc32 (complex64, the reference's framesync "
+                         "input) or sc16 (UHD wire samples read in place, 4 B/sample)")
+    ap.add_argument("--sc16-steps", type=int, default=None,
+                    help="steps of the secondary sc16-resident leg of an fc32 run (0: skip; "
+                         "default: --steps)")
     ap.add_argument("--cpu-baseline", type=int, default=1, help="0 to skip the oracle timing")
     ap.add_argument("--cpu-threads", type=int, default=0,
                     help="threads of the multi-core CPU baseline (0: the box's core share)")
@@ -129,7 +135,7 @@ def decode_kernel_name(M, N, args):
     decode_kernels.hip dispatch rules; all-carrier allocation, 16-byte aligned buffers)."""
     lg = M.bit_length() - 1
     stream_ok = (os.environ.get("RMIMO_DECODE_STREAM", "1") != "0" and args.detector != "siso"
-                 and args.qam <= 256 and (N, lg) in ((4, 11), (4, 10), (2, 12), (2, 11)))
+                 and args.qam <= 256 and (N, lg) in ((4, 11), (4, 10), (2, 12), (2, 11), (2, 10)))
     if stream_ok:
         return "decode_stream_kernel<%d,%d>" % (lg, N)
     if 512 <= M <= 4096 and N in (2, 4):
@@ -278,6 +284,19 @@ def main():
     if args.cfo:
         from rub_mimo_amd.receiver import cfo_derotate
         cfo_derotate(iq, L, F * N, L, 0, -args.cfo, M, stream=sh)   # a CFO of +args.cfo
+    sc16 = args.sample_format == "sc16"
+    # sc16 full scale: the job's peak |I|, |Q| with 1 % headroom, as a receive gain would set it
+    amax = torch.view_as_real(iq).abs().max().reshape(1).float()
+    if world > 1:
+        dist.all_reduce(amax, op=dist.ReduceOp.MAX)
+    wscale = float(amax.item()) * 1.01 / 32767.0
+    src = iq
+    if sc16:
+        # resident wire captures [F][N][L][2] int16; iq becomes their widened copy, which the
+        # CPU baseline reads
+        src = (torch.view_as_real(iq) / wscale).round_().clamp_(-32768, 32767).to(torch.int16)
+        ingest_sc16(src, L, iq, L, F * N, L, wscale, stream=sh)
+    in_bytes = 4 if sc16 else 8             # HBM bytes per input sample
 
     rx = Receiver(RxParams(M=M, cp_len=cp, num_streams=N, num_access_codes=nac, pid_max=pid,
                            detector=det, qam_order=args.qam, cfo_correct=args.cfo != 0.0),
@@ -286,11 +305,12 @@ def main():
     out_sym = torch.empty((F * K, N, pid, m_occ), dtype=torch.complex64, device=dev)
     out_idx = torch.empty((F * K, N, pid, m_occ), dtype=torch.uint8, device=dev)
 
-    def step():
-        rx.process(iq, L, L, F, max_out=pid, out_sym=out_sym, out_idx=out_idx,
-                   ref_mode=args.ref_mode, ref_idx=tx_idx if args.ref_mode == 1 else None,
-                   ref_seed=args.seed, frame_id0=frame_id0, stream=sh, frames_per_capture=K,
-                   ref_starts=ref_starts)
+    def step(x=None, wire_in=sc16):
+        rx.process(src if x is None else x, L, L, F, max_out=pid, out_sym=out_sym,
+                   out_idx=out_idx, ref_mode=args.ref_mode,
+                   ref_idx=tx_idx if args.ref_mode == 1 else None, ref_seed=args.seed,
+                   frame_id0=frame_id0, stream=sh, frames_per_capture=K, ref_starts=ref_starts,
+                   sc16=wire_in, sc16_scale=wscale)
 
     # ---- rank-0 sc16 ingest (used by --ingest scatter and the secondary scatter leg)
     wire = None
@@ -310,15 +330,16 @@ def main():
                                      stream=sh)
             else:
                 syn.generate(tmp, L, L, F, frame_id0=r * F, stream=sh)
-            v = torch.view_as_real(tmp) * 32767.0
+            v = torch.view_as_real(tmp) / wscale
             w[r].copy_(v.round_().clamp_(-32768, 32767).to(torch.int16))
         del tmp
         return w
 
     def scatter_loop(pipe, n):
-        """n steps of: wait for this rank's wire batch, widen it (mimo_ingest_sc16) into the
-        planar complex64 batch, receive it; batch i+1's scatter overlaps batch i's receive."""
-        scale = 1.0 / 32767.0
+        """n steps of: wait for this rank's wire batch, receive it (read in place with
+        --sample-format sc16, else widened by mimo_ingest_sc16 into the complex64 batch first);
+        batch i+1's scatter overlaps batch i's receive."""
+        scale = wscale
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize(dev)
@@ -326,8 +347,11 @@ def main():
         pipe.start()
         for _ in range(n):
             w = pipe.next()
-            ingest_sc16(w.data_ptr(), L, iq.data_ptr(), L, F * N, L, scale, stream=sh)
-            step()
+            if sc16:
+                step(w, True)
+            else:
+                ingest_sc16(w.data_ptr(), L, iq.data_ptr(), L, F * N, L, scale, stream=sh)
+                step(iq, False)
         pipe.drain()
         torch.cuda.synchronize(dev)
         if world > 1:
@@ -378,9 +402,9 @@ def main():
     evm_den = sum(float(np.sum(res[i]["evm_den"])) for i in ok_slots)
     errors = sum(int(np.sum(res[i]["errors"])) for i in ok_slots)
 
-    def ok_len(i):
+    def ok_len(i, rr=None):
         """Transmitted length of the frame decoded in slot i (its reference row)."""
-        r = res[i]
+        r = (res if rr is None else rr)[i]
         if not c5:
             return slot_len[i][0]
         c = i // K
@@ -401,6 +425,42 @@ def main():
                                     dist if world > 1 else None, device=dev)
     scanned_total = scanned_total["samples"]
 
+    # ---- secondary leg (fc32 headline): the same captures resident as sc16 wire samples,
+    # read in place (C3-type geometries) or widened internally; its own EVM (quantised input)
+    sc16_info = None
+    n16 = args.steps if args.sc16_steps is None else args.sc16_steps
+    if not sc16 and not timed_scatter and n16 > 0 and not args.cfo:
+        w16 = (torch.view_as_real(iq) / wscale).round_().clamp_(-32768, 32767).to(torch.int16)
+        for _ in range(2):
+            step(w16, True)
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(n16):
+            step(w16, True)
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        t16 = time.perf_counter() - t0
+        r16 = rx.results(F * K)
+        ok16 = [i for i, r in enumerate(r16) if r["status"] == _lib.FRAME_OK]
+        tot16, t16 = reduce_stats(dict(
+            samples=float(N) * sum(ok_len(i, r16) for i in ok16) * n16, frames_ok=len(ok16),
+            symbols=0, evm_num=sum(float(np.sum(r16[i]["evm_num"])) for i in ok16),
+            evm_den=sum(float(np.sum(r16[i]["evm_den"])) for i in ok16), errors=0), t16,
+            dist if world > 1 else None, device=dev)
+        sc16_info = {
+            "value": tot16["samples"] / t16, "ms_per_step": t16 / n16 * 1e3, "steps": n16,
+            "frames_ok": int(tot16["frames_ok"]),
+            "evm_db": (10 * np.log10(tot16["evm_num"] / tot16["evm_den"])
+                       if tot16["evm_den"] > 0 else None),
+            "sc16_scale": wscale,
+            "note": "the same captures quantised to UHD sc16 wire samples (4 B/sample) at the "
+                    "job's peak, resident in HBM and read in place by the S&C, search + LS and "
+                    "streaming decode kernels (mimo_batch.sample_format = MIMO_SAMPLE_SC16)"}
+        del w16
+
     # ---- secondary leg (N > 1, resident headline): rank-0 sc16 scatter, bounded
     scatter_info = None
     if world > 1 and not timed_scatter and args.scatter_steps > 0:
@@ -414,7 +474,8 @@ def main():
         scatter_info = {
             "value": samples_total / args.steps * args.scatter_steps / t_sc,
             "ms_per_step": t_sc / args.scatter_steps * 1e3, "steps": args.scatter_steps,
-            "wire": "sc16 (4 B/sample), mimo_ingest_sc16 widening on each rank",
+            "wire": "sc16 (4 B/sample), " + ("read in place on each rank" if sc16 else
+                                              "mimo_ingest_sc16 widening on each rank"),
             "rank0_out_gbs": wire_bytes / t_sc / 1e9,
             "note": "rank 0 sends every peer its captures each step over RCCL P2P (xGMI), "
                     "double-buffered against the receive; value counts detected-frame samples"}
@@ -425,17 +486,20 @@ def main():
     dec_avg_s = dec_ms / max(dec_n, 1) / 1e3
     # per decoded symbol: N bodies read, N x M_occ complex64 + uint8 written (+ the uint8
     # transmitted index read when the EVM reference comes from HBM)
-    per_sym = N * M * 8 + N * m_occ * 9 + (N * m_occ if args.ref_mode == 1 else 0)
+    kname = decode_kernel_name(M, N, args)
+    # (sc16 is read in place by the streaming decode; other decode kernels read the widened copy)
+    dec_in = in_bytes if kname.startswith("decode_stream") else 8
+    per_sym = N * M * dec_in + N * m_occ * 9 + (N * m_occ if args.ref_mode == 1 else 0)
     dec_bytes = n_dec * per_sym
     achieved = dec_bytes / dec_avg_s / 1e9 if dec_avg_s > 0 else 0.0
-    kname = decode_kernel_name(M, N, args)
     traffic = None
     if os.path.exists(args.pmc_json):
         try:
             pm = json.load(open(args.pmc_json))
             cfgm = pm.get("config", {})
             if ((cfgm.get("M"), cfgm.get("streams"), cfgm.get("frames"), cfgm.get("pid"),
-                    cfgm.get("ref_mode")) == (M, N, F, pid, args.ref_mode)
+                    cfgm.get("ref_mode"), cfgm.get("sample_format", "fc32"))
+                    == (M, N, F, pid, args.ref_mode, args.sample_format)
                     and pm.get("kernel") == kname.split("<")[0]):
                 traffic = pm.get("decode_hbm_bytes_per_launch")
         except Exception:
@@ -470,7 +534,7 @@ def main():
 
     value = samples_total / elapsed
     ms_step = elapsed / args.steps * 1e3
-    bytes_alg = scanned_total * 8 + args.steps * n_dec_all * N * m_occ * 9
+    bytes_alg = scanned_total * in_bytes + args.steps * n_dec_all * N * m_occ * 9
     wl = WORKLOADS[args.workload]
     line = {
         "metric": "complex IQ samples/s through 4x4 MMSE detect; EVM-dB delta vs CPU ref",
@@ -492,6 +556,8 @@ def main():
                    "ingest": ("rank-0 sc16 scatter over RCCL P2P" if timed_scatter
                               else "resident in HBM"),
                    "cfo": args.cfo,
+                   "sample_format": ("sc16 wire samples read in place (4 B/sample)" if sc16
+                                     else "fc32 complex64 (8 B/sample)"),
                    "parallelism": ("%d streams over %d GPU(s)" % (args.frames, world) if c5 else
                                    "frames sharded across %d GPU(s), no collective" % world)},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
@@ -511,6 +577,7 @@ def main():
         "evm_db": 10 * np.log10(evm_num / evm_den) if evm_den > 0 else None,
         "symbol_errors_last_step": int(errors),
         "rank0_scatter": scatter_info,
+        "sc16_resident": sc16_info,
     }
     if rank == 0:
         print(json.dumps(line), flush=True)

@@ -146,7 +146,16 @@ typedef struct mimo_batch {
    * lies in [start_j, start_{j+1}) takes reference row / frame id capture*ref_stride + j;
    * NULL: its slot. */
   const uint64_t *d_ref_starts;
+  /* MIMO_SAMPLE_FC32 (0): d_iq holds complex64. MIMO_SAMPLE_SC16 (1): d_iq holds the UHD sc16
+   * wire format (interleaved int16 I/Q, mimo/config.h:52; 4 bytes per sample, strides and
+   * lengths still in samples), read as float(i16) * sc16_scale -- bit-identical to widening
+   * with mimo_ingest_sc16 first. The S&C, fused search + LS and streaming decode kernels read
+   * it directly (C3-type geometries); other configurations widen it into an internal buffer. */
+  uint32_t sample_format;
+  float sc16_scale;
 } mimo_batch;
+
+enum { MIMO_SAMPLE_FC32 = 0, MIMO_SAMPLE_SC16 = 1 };
 
 /* Positions are those a framesync started at `origin` reports (origin 0 for one frame per
  * capture): add origin for the capture sample. */
@@ -178,7 +187,8 @@ int mimo_rx_batch_G(mimo_rx *h, float *G, uint32_t n_frames);
 int mimo_rx_batch_W(mimo_rx *h, float *W, uint32_t n_frames);
 
 /* stage timing with HIP events on the handle's launch stream (for the roofline line).
- * stages: 0 S&C, 1 plateau, 2 search, 3 LS, 4 weights, 5 decode, 6 EVM reduce */
+ * stages: 0 S&C, 1 plateau, 2 search, 3 LS, 4 weights, 5 decode, 6 EVM reduce; an sc16 batch
+ * that is widened internally (not read in place) adds its widening launch to stage 0 */
 #define MIMO_NUM_STAGES 7
 int mimo_rx_set_timing(mimo_rx *h, int enable);
 /* sums of stage durations (ms) and launch counts since the last call; synchronises */
@@ -244,6 +254,31 @@ int mimo_memset_d(void *dst, int value, size_t bytes, void *hip_stream);
  * layout of mimo_batch. Rows must not overlap. Asynchronous on hip_stream. */
 int mimo_ingest_sc16(const void *d_sc16, uint64_t src_stride, void *d_fc32, uint64_t dst_stride,
                      uint32_t n_arrays, uint64_t n, float scale, void *hip_stream);
+/* ---------------- pinned-host capture ring ----------------
+ * Replaces the rx worker's malloc'd fc32 rx_buffer and its /tmp round trip
+ * (mimo/main.cc:842-848, 872-898, 906-918): the recv loop writes UHD sc16 wire samples
+ * (CPU format "sc16", mimo/config.h:52) straight into pinned host chunks, and every commit is
+ * uploaded asynchronously (one 2-D copy on the ring's own HIP stream) into a device capture
+ * [n_ant][stride] of sc16 samples -- the layout mimo_batch takes with sample_format =
+ * MIMO_SAMPLE_SC16. A chunk is reused only after its upload has completed, so n_chunks >= 2
+ * overlaps the next recv with the previous upload. One producer thread calls acquire/commit;
+ * the consumer calls bind/publish (both may run concurrently with the producer). */
+typedef struct mimo_ring mimo_ring;
+int mimo_ring_create(uint32_t n_ant, uint32_t chunk_samples, uint32_t n_chunks, mimo_ring **out);
+int mimo_ring_destroy(mimo_ring *r);   /* waits for the uploads in flight */
+/* target of the following commits: d_capture rows of `capacity` samples, `stride` apart
+ * (samples; capacity <= stride); write position 0 */
+int mimo_ring_bind(mimo_ring *r, void *d_capture, uint64_t stride, uint64_t capacity);
+/* the next chunk: rows[a] = host pointer of antenna a's chunk_samples interleaved int16 I/Q
+ * (UHD's per-channel buffer vector, main.cc:874); waits for that chunk's previous upload */
+int mimo_ring_acquire(mimo_ring *r, void **rows, uint32_t *max_samples);
+/* n <= max_samples samples were written to every row of the acquired chunk: upload them at
+ * the write position (MIMO_ERR_ARG past capacity or with no bound capture) */
+int mimo_ring_commit(mimo_ring *r, uint32_t n);
+/* make hip_stream wait, on the device, for every upload committed so far; *n_written = the
+ * bound capture's samples per antenna so far */
+int mimo_ring_publish(mimo_ring *r, void *hip_stream, uint64_t *n_written);
+
 /* Carrier-frequency offset (absent from the reference: FIXME at framing.cc:486). Over the S0
  * body starting at sample `start` of each antenna row (period M/2, framing.cc:1054-1111),
  * P = sum_{n<M/2} conj(x[start+n]) x[start+n+M/2]; eps = arg(P)/pi in subcarrier spacings.

@@ -39,7 +39,8 @@ class Batch(C.Structure):
                 ("d_out_sym", C.c_void_p), ("d_out_idx", C.c_void_p), ("ref_mode", C.c_int32),
                 ("d_ref_idx", C.c_void_p), ("ref_seed", C.c_uint64), ("frame_id0", C.c_uint64),
                 ("frames_per_capture", C.c_uint32), ("ref_stride", C.c_uint32),
-                ("d_ref_starts", C.c_void_p)]
+                ("d_ref_starts", C.c_void_p), ("sample_format", C.c_uint32),
+                ("sc16_scale", C.c_float)]
 
 
 class FrameResult(C.Structure):
@@ -111,6 +112,12 @@ SIGNATURES = {
     "mimo_cfo_estimate": (C.c_int, [_vp, _u64, _u32, _u64, _u32, _P(C.c_double), _vp]),
     "mimo_cfo_derotate": (C.c_int, [_vp, _u64, _u32, _u64, C.c_int64, C.c_double, _u32, _vp]),
     "mimo_ingest_sc16": (C.c_int, [_vp, _u64, _vp, _u64, _u32, _u64, C.c_float, _vp]),
+    "mimo_ring_create": (C.c_int, [_u32, _u32, _u32, _P(_vp)]),
+    "mimo_ring_destroy": (C.c_int, [_vp]),
+    "mimo_ring_bind": (C.c_int, [_vp, _vp, _u64, _u64]),
+    "mimo_ring_acquire": (C.c_int, [_vp, _P(_vp), _P(_u32)]),
+    "mimo_ring_commit": (C.c_int, [_vp, _u32]),
+    "mimo_ring_publish": (C.c_int, [_vp, _vp, _P(_u64)]),
     "mimo_stream_sync": (C.c_int, [_vp]),
     "mimo_device_count": (C.c_int, [_P(C.c_int)]),
     "mimo_last_error": (C.c_char_p, []),

@@ -33,6 +33,59 @@ MIMO_DEV float2 cdiv(float2 a, float2 b) {  // (a conj b)/|b|^2, exact for b = +
   return make_float2((a.x * b.x + a.y * b.y) / d, (a.y * b.x - a.x * b.y) / d);
 }
 
+// ---------------- capture samples: complex64, or UHD sc16 on the wire ----------------
+// A capture row is either interleaved fp32 (re, im) -- the fc32 samples the reference's rx
+// worker hands framesync (mimo/main.cc:837-848) -- or the sc16 wire format (interleaved int16
+// I/Q, mimo/config.h:52), read as float(i16) * scale: the same product as UHD's sc16 -> fc32
+// converter and as mimo_ingest_sc16, so both give bit-identical samples to every kernel.
+template <bool SC16>
+struct Iq;
+
+template <>
+struct Iq<false> {
+  const float2 *p;
+  MIMO_DEV float2 at(int64_t i) const { return p[i]; }
+  // samples i, i + 1 (i even, the row 16-byte aligned)
+  MIMO_DEV float4 pair(int64_t i) const { return *reinterpret_cast<const float4 *>(p + i); }
+  MIMO_DEV bool pair_ok() const { return ((uintptr_t)p & 15u) == 0; }
+  MIMO_DEV Iq row(uint64_t off) const { return Iq{p + off}; }
+};
+
+template <>
+struct Iq<true> {
+  const short2 *p;
+  float scale;
+  MIMO_DEV float2 cvt(short2 s) const { return make_float2(wide16(s.x), wide16(s.y)); }
+  // one rounded product, never contracted into a following add (hipcc's default
+  // -ffp-contract=fast-honor-pragmas would otherwise fuse it into the FFT's first butterfly),
+  // so the sample is the same fp32 value in every kernel and in mimo_ingest_sc16
+  MIMO_DEV float wide16(short v) const {
+#pragma clang fp contract(off)
+    return (float)v * scale;
+  }
+  MIMO_DEV float2 at(int64_t i) const { return cvt(p[i]); }
+  MIMO_DEV float4 pair(int64_t i) const {
+    const uint2 w = *reinterpret_cast<const uint2 *>(p + i);
+    const short2 a = make_short2((short)(w.x & 0xFFFFu), (short)(w.x >> 16));
+    const short2 b = make_short2((short)(w.y & 0xFFFFu), (short)(w.y >> 16));
+    const float2 fa = cvt(a), fb = cvt(b);
+    return make_float4(fa.x, fa.y, fb.x, fb.y);
+  }
+  MIMO_DEV bool pair_ok() const { return ((uintptr_t)p & 7u) == 0; }
+  MIMO_DEV Iq row(uint64_t off) const { return Iq{p + off, scale}; }
+};
+
+// row `off` (in samples) of a capture held as fc32 (S = false) or sc16 (S = true)
+template <bool S>
+MIMO_DEV Iq<S> iq_row(const float2 *iq, float scale, uint64_t off) {
+  if constexpr (S) {
+    return Iq<true>{reinterpret_cast<const short2 *>(iq) + off, scale};
+  } else {
+    (void)scale;
+    return Iq<false>{iq + off};
+  }
+}
+
 // ---------------- counter-based PRNG, bit-identical to oracle ref_hash5 ----------------
 MIMO_DEV uint64_t mix64(uint64_t z) {
   z += 0x9E3779B97F4A7C15ull;

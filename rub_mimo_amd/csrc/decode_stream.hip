@@ -181,12 +181,16 @@ MIMO_DEV gptr<P> sgpr_ptr(P *p) {
   return (gptr<P>)(((uint64_t)hi << 32) | lo);
 }
 
-template <int LOG2M, int NA, int REF, int OUTS>
+template <int LOG2M, int NA, int REF, int OUTS, bool SC16 = false>
 __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(DecodeArgs a) {
   using PL = StreamPlan<LOG2M, NA>;
   constexpr int M = PL::M, T = PL::T, S = PL::S, PB = PL::PB, W8 = M / 8;
-  constexpr int RS = M + 2;                       // staging row: M + 2 samples from an even start
-  constexpr int NCH = NA * (RS / 2);              // 16-byte chunks of one symbol's staging
+  // staging row: M + SPC samples from a start aligned to SPC samples, SPC = samples per
+  // 16-byte chunk (2 complex64, or 4 sc16 on the wire)
+  constexpr int SPC = SC16 ? 4 : 2;
+  constexpr int SB = SC16 ? 4 : 8;                // bytes per staged sample
+  constexpr int RS = M + SPC;
+  constexpr int NCH = NA * (RS / SPC);            // 16-byte chunks of one symbol's staging
   constexpr int NDMA = (NCH + T - 1) / T;         // DMA instructions per thread
   constexpr int NREF = NA * M / 16;               // 16-byte chunks of the reference indices
   // store instructions per symbol: the wait at the top of a symbol leaves them in flight
@@ -194,7 +198,8 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
   extern __shared__ __attribute__((aligned(16))) float2 lds_raw[];
   v2f *img = reinterpret_cast<v2f *>(lds_raw);                     // [NA][PB] FFT exchange
   v2f *stg = img + NA * PB;                                        // [NA][RS] next symbol
-  uint8_t *rstg = reinterpret_cast<uint8_t *>(stg + NA * RS);      // [NA][M] next references
+  short2 *stg16 = reinterpret_cast<short2 *>(stg);                 // (sc16 staging)
+  uint8_t *rstg = reinterpret_cast<uint8_t *>(stg) + (size_t)NA * RS * SB;   // [NA][M] next references
   v2f *twl = reinterpret_cast<v2f *>(rstg + ((REF == 1) ? NA * M : 0));   // twiddle table
   __shared__ uint32_t pfx[kStreamMaxFrames + 1];
   __shared__ int64_t fbody[kStreamMaxFrames];
@@ -269,34 +274,49 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
   const uint32_t stg_base = (uint32_t)(uintptr_t)stg;
   const uint32_t rstg_base = (uint32_t)(uintptr_t)rstg;
 
-  // staging of symbol (ff, ss): rows of M + 2 samples from the even sample a0 <= abs0, so
-  // that every lane moves one aligned 16-byte pair; returns the odd offset abs0 - a0
-  auto fetch = [&](uint32_t ff, uint32_t ss) -> int {
+  // staging of symbol (ff, ss): antenna row g is staged as M + SPC samples from the SPC-aligned
+  // sample a_g <= its first sample e_g (alignment taken in the whole batch, so rows of any
+  // stride stay on the DMA path and every lane moves one aligned 16-byte chunk); returns the
+  // offsets e_g - a_g (< SPC), 4 bits per row
+  auto fetch = [&](uint32_t ff, uint32_t ss) -> uint32_t {
     const int64_t b0 = fbody[ff];
     const int64_t abs0 = (int64_t)((((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)b0)) |
                                     ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)((uint64_t)b0 >> 32)) << 32))) +
                          (int64_t)ss * a.SL;
-    const int64_t a0 = abs0 & ~(int64_t)1;
-    const float2 *xf = a.iq + (uint64_t)(__builtin_amdgcn_readfirstlane(fcr[ff]) & 0xFFFFu) * NA * a.stride;
+    const int64_t row0 = (int64_t)(__builtin_amdgcn_readfirstlane(fcr[ff]) & 0xFFFFu) * NA * (int64_t)a.stride;
+    const int64_t e0 = row0 + abs0;                   // batch sample index of row 0's first
     const int t0 = opq(tid);
-    if (a0 >= 0 && a0 + RS <= (int64_t)a.frame_len && ((uintptr_t)a.iq & 15u) == 0 &&
-        (a.stride & 1u) == 0) {
-      const auto xa = sgpr_ptr(xf + a0);
+    uint32_t odds = 0;
+#pragma unroll
+    for (int g = 0; g < NA; g++)
+      odds |= (uint32_t)((e0 + (int64_t)g * a.stride) & (SPC - 1)) << (4 * g);
+    if (abs0 >= SPC && abs0 + RS <= (int64_t)a.frame_len && ((uintptr_t)a.iq & 15u) == 0) {
+      // base SPC samples before row 0's aligned start: every row's a_g - base is in [0, 2^32)
+      const int64_t base = (e0 & ~(int64_t)(SPC - 1)) - SPC;
+      const auto xa = sgpr_ptr(reinterpret_cast<const char *>(a.iq) + base * SB);
 #pragma unroll
       for (int u = 0; u < NDMA; u++) {
         const int c = u * T + t0;
         const uint32_t dst = __builtin_amdgcn_readfirstlane(stg_base + (uint32_t)(u * T + wv * 64) * 16u);
         if (u < NCH / T || c < NCH) {
-          const uint32_t g = (uint32_t)c / (RS / 2), q = (uint32_t)c % (RS / 2);
-          dma16((g * (uint32_t)a.stride + 2 * q) * 8u, xa, dst);
+          const uint32_t g = (uint32_t)c / (RS / SPC), q = (uint32_t)c % (RS / SPC);
+          const int64_t ag = (e0 + (int64_t)g * a.stride) & ~(int64_t)(SPC - 1);
+          dma16((uint32_t)(ag - base + SPC * q) * (uint32_t)SB, xa, dst);
         }
       }
     } else {                                          // edge of the capture: guarded loads
+      const char *xf = reinterpret_cast<const char *>(a.iq) + row0 * SB;
       for (int c = t0; c < NA * RS; c += T) {
         const int g = c / RS, q = c % RS;
-        const int64_t n = a0 + q;
-        stg[c] = (n >= 0 && n < (int64_t)a.frame_len) ? reinterpret_cast<const v2f *>(xf + (uint64_t)g * a.stride)[n]
-                                                      : v2f{0.0f, 0.0f};
+        const int64_t n = abs0 - (int64_t)((odds >> (4 * g)) & 15u) + q;   // row sample
+        const bool in = n >= 0 && n < (int64_t)a.frame_len;
+        if constexpr (SC16) {
+          stg16[c] = in ? reinterpret_cast<const short2 *>(xf)[(uint64_t)g * a.stride + n]
+                        : make_short2(0, 0);
+        } else {
+          stg[c] = in ? reinterpret_cast<const v2f *>(xf)[(uint64_t)g * a.stride + n]
+                      : v2f{0.0f, 0.0f};
+        }
       }
     }
     if constexpr (REF == 1) {
@@ -307,7 +327,7 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
         dma16(t * (uint32_t)(a.max_out * a.M_occ) + 16 * q, rb, dst);
       }
     }
-    return (int)(abs0 - a0);
+    return odds;
   };
 
   // this frame's weights * gain * dn for the thread's subcarriers k = tid + q T
@@ -366,7 +386,7 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
   };
 
   load_w(f);
-  int odd = fetch(f, s);
+  uint32_t odd = fetch(f, s);
   // the first symbol's staging (issued after the weight loads: the counted wait in the loop
   // assumes only stores behind the DMA)
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -378,9 +398,19 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
     v2f v[8];
     {
       const int t0 = opq(tid);
-      const v2f *x = stg + (t0 / W8) * RS + odd + (t0 % W8);
+      if constexpr (SC16) {   // widen the wire samples as they leave the staging area
+        const short2 *x = stg16 + (t0 / W8) * RS + ((odd >> (4 * (t0 / W8))) & 15u) + (t0 % W8);
+        const Iq<true> cv{nullptr, a.iq_scale};
 #pragma unroll
-      for (int r = 0; r < 8; r++) v[r] = x[r * W8];
+        for (int r = 0; r < 8; r++) {
+          const float2 w = cv.cvt(x[r * W8]);
+          v[r] = v2f{w.x, w.y};
+        }
+      } else {
+        const v2f *x = stg + (t0 / W8) * RS + ((odd >> (4 * (t0 / W8))) & 15u) + (t0 % W8);
+#pragma unroll
+        for (int r = 0; r < 8; r++) v[r] = x[r * W8];
+      }
     }
     uint32_t cref[(NA * S + 3) / 4];                  // reference indices, byte (t S + q)
     if constexpr (REF == 1) {
@@ -399,7 +429,7 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
     __syncthreads();                                  // staging consumed by every wave
     // the item after this one (uniform) and its staging, in flight during this symbol
     uint32_t fn = f, sn = s + 1, n_out_n = n_out_f;
-    int odd_n = 0;
+    uint32_t odd_n = 0;
     if (i + 1 < i_end) {
       if (sn >= n_out_f) {
         do { fn++; } while (pfx[fn + 1] == pfx[fn]);
@@ -477,21 +507,27 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
 // returns the EVM partial sets per record (waves per workgroup), 0 when the configuration is
 // not handled here (the caller then uses the per-symbol kernels)
 template <int LOG2M, int NA>
-static size_t stream_lds_bytes(int ref_mode) {
+static size_t stream_lds_bytes(int ref_mode, bool sc16) {
   using PL = StreamPlan<LOG2M, NA>;
   size_t tw = 0;
   for (int p = 1; p < PL::NP; p++) tw += (size_t)(PL::radix(p) - 1) * PL::ns(p);
-  return sizeof(float2) * ((size_t)PL::PB * NA + (size_t)(PL::M + 2) * NA + tw) +
+  const size_t stage = sc16 ? sizeof(short2) * (size_t)(PL::M + 4) * NA
+                            : sizeof(float2) * (size_t)(PL::M + 2) * NA;
+  return sizeof(float2) * ((size_t)PL::PB * NA + tw) + stage +
          (ref_mode == 1 ? (size_t)NA * PL::M : 0);
 }
 
 template <int LOG2M, int NA>
 static uint32_t stream_launch(const DecodeArgs &a, hipStream_t s) {
   using PL = StreamPlan<LOG2M, NA>;
-  const size_t shm = stream_lds_bytes<LOG2M, NA>(a.ref_mode);
+  const size_t shm = stream_lds_bytes<LOG2M, NA>(a.ref_mode, a.sc16 != 0);
   auto pick_out = [&](auto ref) -> void (*)(DecodeArgs) {
     constexpr int R = decltype(ref)::value;
     const int outs = (a.out_sym ? 1 : 0) | (a.out_idx ? 2 : 0);
+    if (a.sc16) {   // sc16 wire input: every output, EVM against HBM indices or decisions
+      if constexpr (R == 2) return nullptr;
+      else return outs == 3 ? decode_stream_kernel<LOG2M, NA, R, 3, true> : nullptr;
+    }
     switch (outs) {
       case 3: return decode_stream_kernel<LOG2M, NA, R, 3>;
       case 2: return decode_stream_kernel<LOG2M, NA, R, 2>;
@@ -502,6 +538,7 @@ static uint32_t stream_launch(const DecodeArgs &a, hipStream_t s) {
   auto kern = a.ref_mode == 1 ? pick_out(std::integral_constant<int, 1>{})
             : a.ref_mode == 2 ? pick_out(std::integral_constant<int, 2>{})
                               : pick_out(std::integral_constant<int, 0>{});
+  if (!kern) return 0;
   if (hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
                           (int)shm) != hipSuccess)
     return 0;
@@ -514,23 +551,34 @@ static uint32_t stream_launch(const DecodeArgs &a, hipStream_t s) {
   return PL::T / 64;
 }
 
-uint32_t launch_decode_stream(const DecodeArgs &a, int log2M, uint32_t n_frames, hipStream_t s) {
+static bool stream_geometry_ok(const DecodeArgs &a, int log2M, uint32_t n_frames) {
   static const bool off = [] { const char *e = getenv("RMIMO_DECODE_STREAM"); return e && e[0] == '0'; }();
   // (capture and reference row of a frame are packed in 16 bits each in LDS)
-  if (off || a.detector == 3 || !a.all_occ || !a.nrec || n_frames > kStreamMaxFrames ||
+  if (off || a.detector == 3 || !a.all_occ || n_frames > kStreamMaxFrames ||
       a.n_caps > 0xFFFFu || a.n_refs > 0xFFFFu ||
       a.qam.L * a.qam.L > kStreamMaxQam)
-    return 0;
-  if (a.ref_mode == 1 && ((uintptr_t)a.ref_idx & 3u)) return 0;
-  if (a.ref_mode == 1 && ((uintptr_t)a.ref_idx & 15u)) return 0;
+    return false;
+  if (a.ref_mode == 1 && ((uintptr_t)a.ref_idx & 15u)) return false;
   // 32-bit DMA offsets within one frame's antennas and one frame's reference rows
   if ((uint64_t)a.N * a.stride * sizeof(float2) >= (1ull << 32) ||
       (uint64_t)a.N * a.max_out * a.M_occ >= (1ull << 32))
-    return 0;
+    return false;
+  return (a.N == 4 && (log2M == 11 || log2M == 10)) ||
+         (a.N == 2 && (log2M == 12 || log2M == 11 || log2M == 10));
+}
+
+bool decode_stream_accepts(const DecodeArgs &a, int log2M, uint32_t n_frames) {
+  if (!stream_geometry_ok(a, log2M, n_frames)) return false;
+  return !a.sc16 || (a.ref_mode != 2 && a.out_sym && a.out_idx);
+}
+
+uint32_t launch_decode_stream(const DecodeArgs &a, int log2M, uint32_t n_frames, hipStream_t s) {
+  if (!a.nrec || !decode_stream_accepts(a, log2M, n_frames)) return 0;
   if (a.N == 4 && log2M == 11) return stream_launch<11, 4>(a, s);
   if (a.N == 4 && log2M == 10) return stream_launch<10, 4>(a, s);
   if (a.N == 2 && log2M == 12) return stream_launch<12, 2>(a, s);
   if (a.N == 2 && log2M == 11) return stream_launch<11, 2>(a, s);
+  if (a.N == 2 && log2M == 10) return stream_launch<10, 2>(a, s);
   return 0;
 }
 

@@ -192,6 +192,9 @@ struct mimo_rx {
   uint32_t F = 0, lagc = 0, n_lagc = 0, n_slots = 0;
   bool search_ls = false;               // fused search + LS (search_ls_kernel) for this geometry
   bool cfo = false;                     // opt-in CFO estimate + derotation (batched path)
+  int cur_sc16 = 0;                     // the batch being launched reads sc16 wire samples
+  float cur_scale = 1.0f;
+  DevBuf<float2> wide;                  // sc16 batches the fused kernels do not take: widened
   DevBuf<float2> cfo_iq;                // derotated scratch capture
   DevBuf<double> cfo_eps;
   uint32_t n_cu = 256;
@@ -255,7 +258,7 @@ struct mimo_rx {
   hipStream_t g_stream = nullptr;
   bool g_valid = false;
   hipGraphExec_t g_exec = nullptr;
-  std::array<const void *, 25> g_sig{};
+  std::array<const void *, 26> g_sig{};
 };
 
 struct mimo_tx {
@@ -354,6 +357,7 @@ int run_sync(mimo_rx *h, const float2 *iq, uint64_t stride, uint32_t F, uint64_t
   if (chunk_lo < nchunks) {
     ScArgs a{};
     a.iq = iq; a.stride = stride; a.frame_len = frame_len;
+    a.sc16 = h->cur_sc16; a.iq_scale = h->cur_scale;
     a.N = h->N; a.M = h->M; a.cp = h->cp;
     // diagnostics only: RMIMO_SC_BAND overrides the exact-recompute band (a band below the
     // fp32 error bound breaks parity)
@@ -412,6 +416,7 @@ int run_sync(mimo_rx *h, const float2 *iq, uint64_t stride, uint32_t F, uint64_t
     if (screen) {
       ScreenArgs sa{};
       sa.iq = iq; sa.stride = stride; sa.frame_len = frame_len;
+      sa.sc16 = h->cur_sc16; sa.iq_scale = h->cur_scale;
       sa.N = h->N; sa.M = h->M;
       sa.thr_screen = h->thr - 0.01;
       sa.chunk_len = K; sa.chunk_lo = chunk_lo; sa.nchunks = nchunks;
@@ -469,6 +474,7 @@ int run_sync(mimo_rx *h, const float2 *iq, uint64_t stride, uint32_t F, uint64_t
   PlateauArgs pa{};
   pa.trig = h->trig.p; pa.rec = h->rec.p; pa.rec_stride = h->cap_chunks; pa.chunk_len = K;
   pa.iq = iq; pa.stride = stride; pa.frame_len = frame_len;
+  pa.sc16 = h->cur_sc16; pa.iq_scale = h->cur_scale;
   pa.N = h->N; pa.M = h->M; pa.SL = h->SL; pa.thr = h->thr; pa.win_len = h->win_len;
   pa.band = sc_band(h->M);
   pa.info = h->info.p;
@@ -491,6 +497,7 @@ int run_estimate(mimo_rx *h, const float2 *iq, uint64_t stride, uint32_t F, uint
     HIPCHK(hipMemsetAsync(h->keys.p, 0, sizeof(unsigned long long) * F * h->N * h->n_slots, s));
   SearchArgs sa{};
   sa.iq = iq; sa.stride = stride; sa.frame_len = frame_len;
+  sa.sc16 = h->cur_sc16; sa.iq_scale = h->cur_scale;
   sa.N = h->N; sa.M = h->M; sa.SL = h->SL; sa.n_slots = h->n_slots;
   sa.lagc = h->lagc; sa.n_lagc = h->n_lagc;
   sa.codespec = h->codes.codespec.p; sa.vscale = h->vscale.p;
@@ -562,6 +569,7 @@ int run_decode(mimo_rx *h, const float2 *iq, uint64_t stride, uint32_t F, uint64
   if (max_out == 0) return MIMO_OK;
   DecodeArgs d{};
   d.iq = iq; d.stride = stride; d.frame_len = frame_len;
+  d.sc16 = h->cur_sc16; d.iq_scale = h->cur_scale;
   d.N = h->N; d.M = h->M; d.cp = h->cp; d.SL = h->SL; d.M_occ = h->M_occ;
   d.detector = h->det; d.siso_tx = h->siso_tx; d.siso_rx = h->siso_rx; d.dn = h->dn;
   d.occ_index = h->occ.p; d.W = h->W.p; d.gain = h->gain.p; d.G = h->G.p; d.info = h->info.p;
@@ -611,6 +619,9 @@ int run_decode(mimo_rx *h, const float2 *iq, uint64_t stride, uint32_t F, uint64
 }  // namespace
 
 // ======================================================================================
+// the error slot of this thread, for the other host translation units (ring.cpp)
+int mimo::host_fail(int code, const char *msg) { return fail(code, msg); }
+
 extern "C" {
 
 const char *mimo_last_error(void) { return g_err.c_str(); }
@@ -1016,6 +1027,37 @@ static uint32_t batch_fpc(const mimo_batch *b) {
 static int run_batch(mimo_rx *h, const mimo_batch *b, hipStream_t s) {
   const float2 *iq = reinterpret_cast<const float2 *>(b->d_iq);
   const uint32_t fpc = batch_fpc(b), slots = b->n_frames * fpc;
+  h->cur_sc16 = 0;
+  h->cur_scale = 1.0f;
+  if (b->sample_format == MIMO_SAMPLE_SC16) {
+    // sc16 wire input: read in place by S&C, the fused search + LS and the streaming decode
+    // where the configuration takes them; otherwise widened once into an internal fc32 batch
+    DecodeArgs probe{};
+    probe.N = h->N; probe.detector = h->det; probe.all_occ = h->M_occ == h->M ? 1 : 0;
+    probe.n_caps = b->n_frames; probe.n_refs = slots; probe.qam = h->qam;
+    probe.ref_mode = b->ref_mode; probe.ref_idx = reinterpret_cast<const uint8_t *>(b->d_ref_idx);
+    probe.stride = b->stride; probe.max_out = b->max_out_syms; probe.M_occ = h->M_occ;
+    probe.out_sym = reinterpret_cast<float2 *>(b->d_out_sym);
+    probe.out_idx = reinterpret_cast<uint8_t *>(b->d_out_idx);
+    probe.sc16 = 1;
+    const bool fused = sc_screen_ok(h->M) && h->search_ls && !h->cfo &&
+                       decode_stream_accepts(probe, h->log2M, slots);
+    if (fused) {
+      h->cur_sc16 = 1;
+      h->cur_scale = b->sc16_scale;
+    } else {
+      const size_t need = (size_t)b->n_frames * h->N * b->stride;
+      if (h->wide.ensure(need) != hipSuccess) return fail(MIMO_ERR_NOMEM, "sc16 widening buffer");
+      hipEvent_t e = h->timer.begin(s);
+      const bool ok = launch_sc16_to_fc32(b->d_iq, b->stride, h->wide.p, b->stride,
+                                          b->n_frames * h->N, b->frame_len, b->sc16_scale, s);
+      h->timer.end(0, e, s);     // timed with the S&C stage (one extra launch)
+      if (!ok) return fail(MIMO_ERR_ARG, "sc16 widening: bad geometry");
+      iq = h->wide.p;
+    }
+  } else if (b->sample_format != MIMO_SAMPLE_FC32) {
+    return fail(MIMO_ERR_ARG, "mimo_batch.sample_format must be MIMO_SAMPLE_FC32 or _SC16");
+  }
   int rc = run_sync(h, iq, b->stride, b->n_frames, b->frame_len, 0, true, s, fpc,
                     fpc > 1 ? b->d_ref_starts : nullptr, b->ref_stride, true);
   CfoBatchArgs ca{};
@@ -1044,6 +1086,8 @@ static int run_batch(mimo_rx *h, const mimo_batch *b, hipStream_t s) {
                     reinterpret_cast<uint8_t *>(b->d_out_idx), b->ref_mode,
                     reinterpret_cast<const uint8_t *>(b->d_ref_idx), b->ref_seed, b->frame_id0,
                     s, b->n_frames);
+  h->cur_sc16 = 0;
+  h->cur_scale = 1.0f;
   return rc;
 }
 
@@ -1052,11 +1096,11 @@ static int run_batch(mimo_rx *h, const mimo_batch *b, hipStream_t s) {
 // the configuration and F (S&C items and hot items are pulled from device-side queues), so
 // the graph stays valid. Not used while stage timing or a diagnostic counter is on.
 // every device pointer a captured batch bakes into its kernels' arguments
-static std::array<const void *, 25> ws_signature(const mimo_rx *h) {
+static std::array<const void *, 26> ws_signature(const mimo_rx *h) {
   return {h->trig.p, h->keys.p, h->rec.p, h->info.p, h->G.p, h->W.p, h->gain.p, h->nvp.p,
           h->evm_part.p, h->evm_out.p, h->n_exact.p, h->queue.p, h->hot.p, h->lspart.p,
           h->tw, h->codes.codespec.p, h->scr_flag.p, h->scr_min.p, h->scr_max.p, h->nrec.p,
-          h->cand.p, h->certfail.p, h->lsq.p, h->cfo_iq.p, h->cfo_eps.p};
+          h->cand.p, h->certfail.p, h->lsq.p, h->cfo_iq.p, h->cfo_eps.p, h->wide.p};
 }
 
 static bool same_batch(const mimo_batch &x, const mimo_batch &y) {
@@ -1065,7 +1109,8 @@ static bool same_batch(const mimo_batch &x, const mimo_batch &y) {
          x.d_out_sym == y.d_out_sym && x.d_out_idx == y.d_out_idx && x.ref_mode == y.ref_mode &&
          x.d_ref_idx == y.d_ref_idx && x.ref_seed == y.ref_seed && x.frame_id0 == y.frame_id0 &&
          batch_fpc(&x) == batch_fpc(&y) && x.d_ref_starts == y.d_ref_starts &&
-         x.ref_stride == y.ref_stride;
+         x.ref_stride == y.ref_stride && x.sample_format == y.sample_format &&
+         x.sc16_scale == y.sc16_scale;
 }
 
 int mimo_rx_process_batch(mimo_rx *h, const mimo_batch *b, void *hip_stream) {

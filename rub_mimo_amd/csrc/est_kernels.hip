@@ -203,7 +203,7 @@ MIMO_DEV uint32_t key_index(unsigned long long k) {
 // (X / S1, S1 = +-1, framing.cc:811), stored per code in lsq[f][rx][tx][code][M] for
 // ls_combine_q_kernel's fixed-order sum. The separate LS pass re-read and re-transformed the
 // same windows; here the window is still in L2 from the segment load.
-template <int LOG2F, int LOG2M>
+template <int LOG2F, int LOG2M, bool SC16 = false>
 __global__ __launch_bounds__((1 << LOG2F) / 16) __attribute__((amdgpu_waves_per_eu(4)))
 void search_ls_kernel(SearchArgs a) {
   constexpr int PTS = 16;
@@ -221,14 +221,14 @@ void search_ls_kernel(SearchArgs a) {
   const uint32_t ns = min(2u, a.n_slots - s0);
   const int64_t abs0 = I.base + (int64_t)a.SL * s0;
   const int64_t L = (int64_t)a.frame_len;
-  const float2 *__restrict__ xf = a.iq + ((uint64_t)I.cap * a.N + r) * a.stride;
-  const v2f *__restrict__ x = reinterpret_cast<const v2f *>(xf);
+  const auto xs = iq_row<SC16>(a.iq, a.iq_scale, ((uint64_t)I.cap * a.N + r) * a.stride);
   const bool inb = abs0 >= 0 && abs0 + F <= L;
   v2f v[PTS], X[PTS];
 #pragma unroll
   for (int e = 0; e < PTS; e++) {
     const int64_t n = abs0 + reg_index<LOG2F, PTS>(tid, e);
-    v[e] = x[inb ? n : (n < 0 ? 0 : (n >= L ? L - 1 : n))];
+    const float2 t = xs.at(inb ? n : (n < 0 ? 0 : (n >= L ? L - 1 : n)));
+    v[e] = v2f{t.x, t.y};
   }
   if (!inb) {
 #pragma unroll
@@ -280,7 +280,7 @@ void search_ls_kernel(SearchArgs a) {
     float2 *lb = reinterpret_cast<float2 *>(buf);
     for (int i = tid; i < M; i += T) {
       const int64_t n = w + i;
-      lb[lds_pad(i)] = (n >= 0 && n < L) ? xf[n] : make_float2(0.0f, 0.0f);
+      lb[lds_pad(i)] = (n >= 0 && n < L) ? xs.at(n) : make_float2(0.0f, 0.0f);
     }
     __syncthreads();
     fft_lds<LOG2M, T, 1, false>(lb, a.tw);
@@ -824,11 +824,12 @@ static bool search_ls_try(const SearchArgs &a, int log2F, int log2M, uint32_t nf
       if (log2F == LOG2F && log2M == LOG2M) {
         if (nf) {
           const size_t shm = sizeof(float2) * lds_padded_len(1 << LOG2F);
-          (void)hipFuncSetAttribute((const void *)search_ls_kernel<LOG2F, LOG2M>,
+          auto kern = a.sc16 ? search_ls_kernel<LOG2F, LOG2M, true>
+                             : search_ls_kernel<LOG2F, LOG2M, false>;
+          (void)hipFuncSetAttribute((const void *)kern,
                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
           dim3 grid(((a.n_slots + 1) / 2) * a.N, nf);
-          hipLaunchKernelGGL((search_ls_kernel<LOG2F, LOG2M>), grid, dim3((1 << LOG2F) / 16),
-                             shm, s, a);
+          hipLaunchKernelGGL(kern, grid, dim3((1 << LOG2F) / 16), shm, s, a);
         }
         return true;
       }

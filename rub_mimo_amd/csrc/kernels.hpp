@@ -41,6 +41,8 @@ struct ScHot {
 
 struct ScArgs {
   const float2 *iq;
+  int sc16;                 // iq holds sc16 wire samples (float(i16) * iq_scale)
+  float iq_scale;
   uint64_t stride;          // complex samples between antenna arrays
   uint64_t frame_len;
   uint32_t N, M, cp;
@@ -76,6 +78,8 @@ constexpr int kScrMaxD = 32;               // M <= 8192
 constexpr int kScrBPI = 4;                 // blocks per wave iteration (loads in flight)
 struct ScreenArgs {
   const float2 *iq;
+  int sc16;                 // iq holds sc16 wire samples (float(i16) * iq_scale)
+  float iq_scale;
   uint64_t stride, frame_len;
   uint32_t N, M;
   double thr_screen;                       // thr - 0.01
@@ -110,6 +114,8 @@ struct PlateauArgs {
   const ScRecord *rec;
   uint64_t rec_stride, chunk_len;
   const float2 *iq;
+  int sc16;
+  float iq_scale;
   uint64_t stride, frame_len;
   uint32_t N, M, SL;
   double thr, band;
@@ -132,6 +138,8 @@ void launch_stream_walk(const PlateauArgs &a, uint32_t n_caps, hipStream_t s);
 // access-code search, framing.cc:702-744 (est_kernels.hip)
 struct SearchArgs {
   const float2 *iq;
+  int sc16;
+  float iq_scale;
   uint64_t stride, frame_len;
   uint32_t N, M, SL, n_slots;      // n_slots = N*nac + 1 (slot 0 = S0)
   uint32_t lagc, n_lagc;           // lags per transform, transforms per slot
@@ -216,6 +224,8 @@ void launch_cfo_batch_rot2(const CfoBatchArgs &a, uint32_t n_frames, hipStream_t
 // replay decode, framing.cc:535-589 / 508-533 fused with square-QAM demap + EVM
 struct DecodeArgs {
   const float2 *iq;
+  int sc16;                 // iq holds sc16 wire samples (float(i16) * iq_scale)
+  float iq_scale;
   uint64_t stride, frame_len;
   uint32_t N, M, cp, SL, M_occ;
   int detector;
@@ -250,6 +260,9 @@ uint32_t launch_decode(const DecodeArgs &a, int log2M, uint32_t n_frames, hipStr
                        bool *per_frame_records);
 // decode_stream.hip: persistent streaming form (0 when the configuration is not handled)
 uint32_t launch_decode_stream(const DecodeArgs &a, int log2M, uint32_t n_frames, hipStream_t s);
+// true when launch_decode_stream takes this configuration (nrec aside): the sc16 wire input
+// is decoded only there
+bool decode_stream_accepts(const DecodeArgs &a, int log2M, uint32_t n_frames);
 constexpr uint32_t kMaxEvmParts = 16;
 
 struct EvmArgs {
@@ -317,6 +330,9 @@ bool launch_cfo_corr(const void *x, uint64_t stride, uint32_t rows, uint64_t sta
                      uint32_t half, double *d_out, hipStream_t s);
 bool launch_cfo_derotate(void *x, uint64_t stride, uint32_t rows, uint64_t n, int64_t n0,
                          double nu, hipStream_t s);
+// host side: record msg as this thread's mimo_last_error() and return code (engine.cpp)
+int host_fail(int code, const char *msg);
+
 bool launch_sc16_to_fc32(const void *src, uint64_t src_stride, void *dst, uint64_t dst_stride,
                          uint32_t rows, uint64_t n, float scale, hipStream_t s);
 

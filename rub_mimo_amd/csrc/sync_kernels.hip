@@ -107,23 +107,27 @@ MIMO_DEV float sc_exact_lds(const float2 *s, int M) {
 }
 
 // the same straight from global memory (one lane; list overflow and the rare backward scan)
-MIMO_DEV float sc_exact(const float2 *__restrict__ x, int64_t n, int64_t M) {
+template <bool S>
+MIMO_DEV float sc_exact(const Iq<S> x, int64_t n, int64_t M) {
   const int64_t M2 = M / 2;
   float Pr = 0.0f, Pi = 0.0f, R = 0.0f;
   for (int64_t k = n - M2 + 1; k <= n; k++) {
-    float2 d = (k - M2 >= 0) ? x[k - M2] : make_float2(0.0f, 0.0f);
-    float2 v = (k >= 0) ? x[k] : make_float2(0.0f, 0.0f);
+    float2 d = (k - M2 >= 0) ? x.at(k - M2) : make_float2(0.0f, 0.0f);
+    float2 v = (k >= 0) ? x.at(k) : make_float2(0.0f, 0.0f);
     float pr = d.x * v.x - (-d.y) * v.y;
     float pi = d.x * v.y + (-d.y) * v.x;
     Pr = Pr + (-1.0f) * pr;
     Pi = Pi + (-1.0f) * pi;
   }
   for (int64_t k = n - M + 1; k <= n; k++) {
-    float2 v = (k >= 0) ? x[k] : make_float2(0.0f, 0.0f);
+    float2 v = (k >= 0) ? x.at(k) : make_float2(0.0f, 0.0f);
     float z = v.x * v.x + v.y * v.y;
     R = R + 0.5f * z;
   }
   return (Pr * Pr + Pi * Pi) / (R * R);
+}
+MIMO_DEV float sc_exact(const float2 *__restrict__ x, int64_t n, int64_t M) {
+  return sc_exact(Iq<false>{x}, n, M);
 }
 
 
@@ -281,28 +285,37 @@ MIMO_DEV float2 seq_sum2(const float2 *q, int n) {
 }
 
 // two consecutive samples (q even), zero outside [0, L)
-MIMO_DEV float4 ld_pair(const float2 *__restrict__ x, int64_t q, int64_t L, bool vec) {
-  if (vec && q >= 0 && q + 1 < L) return *reinterpret_cast<const float4 *>(x + q);
-  const float2 v0 = (q >= 0 && q < L) ? x[q] : make_float2(0.0f, 0.0f);
-  const float2 v1 = (q + 1 >= 0 && q + 1 < L) ? x[q + 1] : make_float2(0.0f, 0.0f);
+template <bool S>
+MIMO_DEV float4 ld_pair(const Iq<S> x, int64_t q, int64_t L, bool vec) {
+  if (vec && q >= 0 && q + 1 < L) return x.pair(q);
+  const float2 v0 = (q >= 0 && q < L) ? x.at(q) : make_float2(0.0f, 0.0f);
+  const float2 v1 = (q + 1 >= 0 && q + 1 < L) ? x.at(q + 1) : make_float2(0.0f, 0.0f);
   return make_float4(v0.x, v0.y, v1.x, v1.y);
+}
+MIMO_DEV float4 ld_pair(const float2 *__restrict__ x, int64_t q, int64_t L, bool vec) {
+  return ld_pair(Iq<false>{x}, q, L, vec);
 }
 
 // one iteration's 4096 samples from q0 into registers, 16 bytes per lane, when the block is
 // inside [0, L) (block-uniform); otherwise false and the ring is filled by guarded loads
-MIMO_DEV bool fetch_block(float4 (&pre)[kScIt / (2 * kScT)], const float2 *__restrict__ x,
+template <bool S>
+MIMO_DEV bool fetch_block(float4 (&pre)[kScIt / (2 * kScT)], const Iq<S> x,
                           int64_t q0, int64_t L, bool vec) {
   const bool ok = vec && q0 >= 0 && q0 + kScIt <= L;
-  const float4 *p = reinterpret_cast<const float4 *>(x + (ok ? q0 : 0)) + threadIdx.x;
+  const int64_t p0 = (ok ? q0 : 0) + 2 * (int64_t)threadIdx.x;
   // one branch around all loads (a per-element select makes hipcc wait for each load in turn)
   if (ok) {
 #pragma unroll
-    for (int j = 0; j < kScIt / (2 * kScT); j++) pre[j] = p[kScT * j];
+    for (int j = 0; j < kScIt / (2 * kScT); j++) pre[j] = x.pair(p0 + 2 * kScT * j);
   } else {
 #pragma unroll
     for (int j = 0; j < kScIt / (2 * kScT); j++) pre[j] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
   }
   return ok;
+}
+MIMO_DEV bool fetch_block(float4 (&pre)[kScIt / (2 * kScT)], const float2 *__restrict__ x,
+                          int64_t q0, int64_t L, bool vec) {
+  return fetch_block(pre, Iq<false>{x}, q0, L, vec);
 }
 
 // conj(d) * v, the oracle's operation order
@@ -995,6 +1008,7 @@ __global__ __launch_bounds__(kScT) void sc_finalize_kernel(ScArgs a) {
 // the record's run starts where the chunk saw the run begin, otherwise an exact backward scan
 // (64 positions per step, the oracle's fp32 metric). Returns true when a run reaches below
 // floor > 0, i.e. began before the re-arm point of a stream frame.
+template <bool S>
 MIMO_DEV bool trigger_run_starts(const PlateauArgs &a, uint32_t cap, const ScRecord &rec,
                                  int64_t floor, int64_t (&st)[kMaxStreams]) {
   const int lane = threadIdx.x & 63;
@@ -1005,7 +1019,7 @@ MIMO_DEV bool trigger_run_starts(const PlateauArgs &a, uint32_t cap, const ScRec
       start = (int64_t)rec.start[s];
     } else {
       // every computed sample of the chunk's range is in the run: walk back exactly
-      const float2 *__restrict__ x = a.iq + ((uint64_t)cap * a.N + s) * a.stride;
+      const auto x = iq_row<S>(a.iq, a.iq_scale, ((uint64_t)cap * a.N + s) * a.stride);
       bool hit = false;
       for (int64_t q0 = (int64_t)rec.start[s] - 1; q0 >= floor; q0 -= 64) {
         const int64_t q = q0 - lane;
@@ -1080,6 +1094,7 @@ MIMO_DEV int frame_from_trigger(const PlateauArgs &a, FrameInfo &I, uint32_t cap
 // framing.cc:601-623 over the ballots with in_plateau false at r. For chunks whose recorded
 // (first) candidate precedes r -- frames shorter than a chunk -- so its cost is bounded by a
 // chunk of small-M work. Returns the trigger (-1: none before end) and the run starts.
+template <bool S>
 MIMO_DEV int64_t forward_trigger(const PlateauArgs &a, uint32_t cap, int64_t r, int64_t end,
                                  int64_t (&st)[kMaxStreams]) {
   const int lane = threadIdx.x & 63;
@@ -1089,7 +1104,7 @@ MIMO_DEV int64_t forward_trigger(const PlateauArgs &a, uint32_t cap, int64_t r, 
   for (int64_t q0 = r; q0 < end; q0 += 64) {
     unsigned long long bal[kMaxStreams];
     for (uint32_t s = 0; s < a.N; s++) {
-      const float2 *__restrict__ x = a.iq + ((uint64_t)cap * a.N + s) * a.stride;
+      const auto x = iq_row<S>(a.iq, a.iq_scale, ((uint64_t)cap * a.N + s) * a.stride);
       const int64_t q = q0 + lane;
       const bool b = q < end && (double)sc_exact(x, q, a.M) > a.thr;
       bal[s] = __ballot(b);
@@ -1131,6 +1146,7 @@ MIMO_DEV void frame_empty(FrameInfo &I, int status, uint32_t cap, uint32_t ref, 
 
 // one frame per capture: run starts (from the trigger chunk's record, exact backward scan
 // where the run began before that chunk's halo), sync index, completeness
+template <bool S>
 __global__ __launch_bounds__(64) void plateau_kernel(PlateauArgs a) {
   const uint32_t f = blockIdx.x;
   FrameInfo &I = a.info[f];
@@ -1141,7 +1157,7 @@ __global__ __launch_bounds__(64) void plateau_kernel(PlateauArgs a) {
   }
   const ScRecord &rec = a.rec[(uint64_t)f * a.rec_stride + n / a.chunk_len];
   int64_t st[kMaxStreams];
-  (void)trigger_run_starts(a, f, rec, 0, st);
+  (void)trigger_run_starts<S>(a, f, rec, 0, st);
   uint64_t nsp;
   (void)frame_from_trigger(a, I, f, f, 0, (int64_t)n, st, false, nsp);
 }
@@ -1159,6 +1175,7 @@ __global__ __launch_bounds__(64) void plateau_kernel(PlateauArgs a) {
 // over the fp32 error band; a frame it cannot prove, or one whose run or window reaches
 // before r_k, is reported MIMO_FRAME_RESCAN (the caller resumes that capture at r_k as a
 // fresh capture) and the slots after it MIMO_FRAME_NONE.
+template <bool S>
 __global__ __launch_bounds__(64) void stream_walk_kernel(PlateauArgs a) {
   const uint32_t cap = blockIdx.x;
   const int lane = threadIdx.x;
@@ -1177,7 +1194,7 @@ __global__ __launch_bounds__(64) void stream_walk_kernel(PlateauArgs a) {
     if (c_from < a.nchunks && cand[c_from] != ~0ull && (int64_t)cand[c_from] < r) {
       // chunk(r) recorded an earlier trigger (several frames per chunk): exact scan of the
       // rest of that chunk, then the recorded candidates of the chunks after it
-      n = forward_trigger(a, cap, r, std::min<int64_t>((int64_t)(c_from + 1) * K,
+      n = forward_trigger<S>(a, cap, r, std::min<int64_t>((int64_t)(c_from + 1) * K,
                                                        (int64_t)a.frame_len), st);
       c_from++;
     }
@@ -1198,7 +1215,7 @@ __global__ __launch_bounds__(64) void stream_walk_kernel(PlateauArgs a) {
     bool spans = false;
     if (n < 0) {
       n = (int64_t)cand[cf];
-      spans = trigger_run_starts(a, cap, a.rec[(uint64_t)cap * a.rec_stride + cf], r, st);
+      spans = trigger_run_starts<S>(a, cap, a.rec[(uint64_t)cap * a.rec_stride + cf], r, st);
     }
     if (spans) {
       if (lane == 0) frame_empty(I, 3, cap, ref_slot, r, 0);
@@ -1230,6 +1247,7 @@ __global__ __launch_bounds__(64) void stream_walk_kernel(PlateauArgs a) {
 // and the fresh framesync's metric (samples before r read as zero: P sums products m >=
 // r + M/2, R samples m >= r) stay clearly below the threshold. Running fp64 sums per thread
 // segment, seeded by one block scan of the segments' differences (as sc_exact_kernel).
+template <bool S>
 __global__ __launch_bounds__(kScT) void stream_cert_kernel(PlateauArgs a) {
   __shared__ double ws[2][6][kScT / 64];
   __shared__ int s_fail;
@@ -1239,8 +1257,8 @@ __global__ __launch_bounds__(kScT) void stream_cert_kernel(PlateauArgs a) {
   const int tid = threadIdx.x;
   const int64_t M = a.M, M2 = M / 2, r = (int64_t)I.origin;
   const int64_t L = (int64_t)a.frame_len;
-  const float2 *__restrict__ x = a.iq + ((uint64_t)cap * a.N + s) * a.stride;
-  auto ld = [&](int64_t q) { return (q >= 0 && q < L) ? x[q] : make_float2(0.0f, 0.0f); };
+  const auto x = iq_row<S>(a.iq, a.iq_scale, ((uint64_t)cap * a.N + s) * a.stride);
+  auto ld = [&](int64_t q) { return (q >= 0 && q < L) ? x.at(q) : make_float2(0.0f, 0.0f); };
   if (tid == 0) s_fail = 0;
   // capture-history sums ending at r - 1 and the region's energy (the cancellation guard)
   double c[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0}, tot[6];
@@ -1361,6 +1379,7 @@ MIMO_DEV void tr_reduce_step(float *v, int lane) {
 }
 
 // block sums of antenna 0 over a span, the screen test, and the chunk list
+template <bool S>
 __global__ __launch_bounds__(kScrT) __attribute__((amdgpu_waves_per_eu(6))) void sc_screen_kernel(ScreenArgs a) {
   constexpr int B = kScrB;
   __shared__ float4 recs[kScrSpan / B + 2 * (kScrMaxD)];
@@ -1372,8 +1391,8 @@ __global__ __launch_bounds__(kScrT) __attribute__((amdgpu_waves_per_eu(6))) void
   if (q0 >= L) return;
   const int NB = kScrSpan / B + 2 * D;
   const int64_t h0 = q0 - (int64_t)2 * D * B;     // first block of the history
-  const float2 *__restrict__ x = a.iq + (uint64_t)f * a.N * a.stride;   // antenna 0
-  const bool vec = ((uintptr_t)x & 15u) == 0;
+  const auto x = iq_row<S>(a.iq, a.iq_scale, (uint64_t)f * a.N * a.stride);   // antenna 0
+  const bool vec = x.pair_ok();
   // block sums: a wave per block, two positions per lane (B = 128); kScrBPI blocks per wave
   // iteration with all their loads issued before the first use (one memory latency per
   // iteration instead of per block)
@@ -1381,12 +1400,10 @@ __global__ __launch_bounds__(kScrT) __attribute__((amdgpu_waves_per_eu(6))) void
     float4 cur[kScrBPI], del[kScrBPI];
     const int64_t nb = h0 + (int64_t)j0 * B;
     if (vec && nb - RL >= 0 && nb + (int64_t)kScrBPI * B <= L && j0 + kScrBPI <= NB) {
-      const float4 *xc = reinterpret_cast<const float4 *>(x + nb) + lane;
-      const float4 *xd = reinterpret_cast<const float4 *>(x + nb - RL) + lane;
 #pragma unroll
       for (int b = 0; b < kScrBPI; b++) {
-        cur[b] = xc[b * (B / 2)];
-        del[b] = xd[b * (B / 2)];
+        cur[b] = x.pair(nb + 2 * lane + (int64_t)b * B);
+        del[b] = x.pair(nb - RL + 2 * lane + (int64_t)b * B);
       }
     } else {
 #pragma unroll
@@ -1485,6 +1502,7 @@ constexpr int kResSpread = 1024;    // positions spanned by one exact-recompute 
 // place with the oracle's exact fp32 chains from the ring (two lanes per sample); the last
 // antenna workgroup of an item to finish then applies the plateau rule to the item's words
 // (item_conditions / item_record, as sc_finalize_kernel) -- no separate resolve/finalize pass.
+template <bool S>
 __global__ __launch_bounds__(kScT) __attribute__((amdgpu_waves_per_eu(2)))
 void sc_exact_kernel(ScArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char sc_dyn[];
@@ -1520,8 +1538,8 @@ void sc_exact_kernel(ScArgs a) {
   const int64_t fmin = (int64_t)a.fmin[ci], fmax = (int64_t)a.fmax[ci];
   int it_lo = (int)std::max<int64_t>(0, (fmin - (int64_t)a.cp - 2 - w0) / kScIt);
   int it_hi = (int)std::min<int64_t>(kScIters - 1, (fmax - w0) / kScIt);
-  const float2 *__restrict__ x = a.iq + ((uint64_t)f * a.N + s) * a.stride;
-  const bool vec = ((uintptr_t)x & 15u) == 0;
+  const auto x = iq_row<S>(a.iq, a.iq_scale, ((uint64_t)f * a.N + s) * a.stride);
+  const bool vec = x.pair_ok();
   const int64_t ib_lo = w0 + (int64_t)it_lo * kScIt;   // first evaluated position
   if (tid == 0) hp->lo[s] = ib_lo;
   for (int it = 0; it < kScIters; it++)
@@ -1536,7 +1554,7 @@ void sc_exact_kernel(ScArgs a) {
 #pragma unroll
       for (int u = 0; u < HU; u++) {
         const int j = j0 + u * kScT + tid;
-        hv[u] = *reinterpret_cast<const float4 *>(x + ib_lo - M + 2 * (2 * j < M ? j : 0));
+        hv[u] = x.pair(ib_lo - M + 2 * (2 * j < M ? j : 0));
       }
 #pragma unroll
       for (int u = 0; u < HU; u++) {
@@ -1883,31 +1901,43 @@ void launch_fill(const FillArgs &a, hipStream_t s) {
 void launch_sc_screen(const ScreenArgs &a, uint32_t n_frames, hipStream_t s) {
   const uint64_t span = (uint64_t)a.frame_len - std::min<uint64_t>(a.frame_len, a.chunk_lo * a.chunk_len);
   const uint32_t gx = (uint32_t)((span + kScrSpan - 1) / kScrSpan);
-  if (gx) hipLaunchKernelGGL(sc_screen_kernel, dim3(gx, n_frames), dim3(kScrT), 0, s, a);
+  if (!gx) return;
+  if (a.sc16)
+    hipLaunchKernelGGL(sc_screen_kernel<true>, dim3(gx, n_frames), dim3(kScrT), 0, s, a);
+  else
+    hipLaunchKernelGGL(sc_screen_kernel<false>, dim3(gx, n_frames), dim3(kScrT), 0, s, a);
 }
 
 void launch_sc_exact(const ScArgs &a, hipStream_t s) {
   const size_t shm = sc_table_bytes(a.M) +
                      sizeof(float) * (size_t)((a.M + kResSpread + 3) & ~3u) +
                      sizeof(float2) * (size_t)(a.M + kResSpread);
-  static size_t set_shm = 0;
-  if (shm != set_shm) {
-    (void)hipFuncSetAttribute((const void *)sc_exact_kernel,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
-    set_shm = shm;
+  static size_t set_shm[2] = {0, 0};
+  const int v = a.sc16 ? 1 : 0;
+  auto kern = a.sc16 ? sc_exact_kernel<true> : sc_exact_kernel<false>;
+  if (shm != set_shm[v]) {
+    (void)hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)shm);
+    set_shm[v] = shm;
   }
-  hipLaunchKernelGGL(sc_exact_kernel, dim3(a.N, std::min<uint32_t>(a.hot_cap, 256)), dim3(kScT),
-                     shm, s, a);
+  hipLaunchKernelGGL(kern, dim3(a.N, std::min<uint32_t>(a.hot_cap, 256)), dim3(kScT), shm, s, a);
 }
 
 void launch_plateau(const PlateauArgs &a, uint32_t n_frames, hipStream_t s) {
-  hipLaunchKernelGGL(plateau_kernel, dim3(n_frames), dim3(64), 0, s, a);
+  if (a.sc16) hipLaunchKernelGGL(plateau_kernel<true>, dim3(n_frames), dim3(64), 0, s, a);
+  else hipLaunchKernelGGL(plateau_kernel<false>, dim3(n_frames), dim3(64), 0, s, a);
 }
 
 void launch_stream_walk(const PlateauArgs &a, uint32_t n_caps, hipStream_t s) {
-  hipLaunchKernelGGL(stream_walk_kernel, dim3(n_caps), dim3(64), 0, s, a);
+  if (a.sc16) hipLaunchKernelGGL(stream_walk_kernel<true>, dim3(n_caps), dim3(64), 0, s, a);
+  else hipLaunchKernelGGL(stream_walk_kernel<false>, dim3(n_caps), dim3(64), 0, s, a);
   if (a.fpc > 1) {
-    hipLaunchKernelGGL(stream_cert_kernel, dim3(a.fpc - 1, a.N, n_caps), dim3(kScT), 0, s, a);
+    if (a.sc16)
+      hipLaunchKernelGGL(stream_cert_kernel<true>, dim3(a.fpc - 1, a.N, n_caps), dim3(kScT), 0,
+                         s, a);
+    else
+      hipLaunchKernelGGL(stream_cert_kernel<false>, dim3(a.fpc - 1, a.N, n_caps), dim3(kScT), 0,
+                         s, a);
     hipLaunchKernelGGL(stream_fixup_kernel, dim3(n_caps), dim3(64), 0, s, a);
   }
 }

@@ -202,3 +202,15 @@ def test_cfo_argument_errors_without_gpu():
     assert b"stride" in L.mimo_last_error()
     assert L.mimo_cfo_derotate(None, 0, 0, 0, 0, 0.1, 64, None) == 0        # empty: no-op
     assert L.mimo_cfo_derotate(16, 10, 2, 20, 0, 0.1, 64, None) == -1       # stride < n
+
+
+def test_capture_ring_arguments_and_no_gpu_error():
+    """mimo_ring_create validates its geometry, and without a GPU (no pinned host memory)
+    fails with an error instead of handing out pageable buffers."""
+    from rub_mimo_amd.ring import CaptureRing
+    for bad in ((0, 1024, 2), (9, 1024, 2), (4, 0, 2), (4, 1024, 0)):
+        with pytest.raises(_lib.MimoError):
+            CaptureRing(*bad)
+    if _lib.device_count() == 0:
+        with pytest.raises(_lib.MimoError):
+            CaptureRing(4, 1024, 2)

@@ -451,7 +451,10 @@ def test_capture_files_replay_matches_golden(tmp_path):
 
 @pytest.mark.parametrize("rows,n,src_stride,dst_stride,off", [
     (4, 100003, 100004, 100008, 0),     # vector path with a ragged tail
-    (3, 4099, 4101, 4099, 0),           # odd strides: scalar path
+    (3, 4099, 4101, 4099, 0),           # odd, unequal strides: scalar path
+    (5, 4099, 4099, 4099, 0),           # odd equal strides: per-row aligned head + vectors
+    (4, 2, 1027, 1027, 0),              # rows shorter than their head
+    (6, 9, 9, 9, 0),
     (2, 1024, 1024, 1024, 1),           # misaligned source: scalar path
     (1, 0, 0, 0, 0),                    # empty
 ])
@@ -564,3 +567,150 @@ def test_cfo_batch_corrects_rotated_c3_frames(eps_true):
         assert abs(e1 - e3) <= 0.1, (f, e3, e1)
         assert e3 - e0 <= (0.2 if e0 >= -30.0 else 3.0), (f, e0, e3)
         assert e2 > e0 + 10.0, (f, e0, e2)
+
+
+def _sc16_capture(iq, amax):
+    """Quantise complex64 captures [F][N][L] to the sc16 wire format (int16 I/Q) at full scale
+    amax, as a radio's ADC path would; returns the int16 tensor [F][N][L][2] and the scale."""
+    import torch
+    q = torch.view_as_real(iq) * (32767.0 / amax)
+    return q.round_().clamp_(-32768, 32767).to(torch.int16).contiguous(), amax / 32767.0
+
+
+@pytest.mark.parametrize("geom", ["c3", "c3_streams", "c2", "m512"])
+def test_sc16_batch_equals_widened_batch(geom):
+    """mimo_batch.sample_format = SC16 (UHD wire samples read in place by the S&C, fused search
+    + LS and streaming decode kernels; other geometries widen internally) gives bit-identical
+    results to widening with mimo_ingest_sc16 first and running the complex64 path: sync,
+    corr indices, symbols, indices and EVM sums."""
+    import torch
+    from rub_mimo_amd.receiver import ingest_sc16
+    if geom == "c2":
+        M, cp, N, nac, pid, qam, det, F, K = 1024, 76, 2, 20, 200, 16, _lib.DET_ZF2, 4, 1
+    elif geom == "m512":
+        M, cp, N, nac, pid, qam, det, F, K = 512, 38, 2, 8, 100, 16, _lib.DET_ZF2, 4, 1
+    else:
+        M, cp, N, nac, pid, qam, det, F, K = 2048, 152, 4, 20, 300, 64, _lib.DET_MMSE, 4, 1
+    sp = SynthParams(M=M, cp_len=cp, num_streams=N, num_access_codes=nac, pid=pid,
+                     qam_order=qam, seed=404, snr_db=30.0)
+    S = Synthesizer(sp)
+    if geom == "c3_streams":
+        J, K = 2, 3
+        lens, L = S.stream_layout(F, J)
+        iq = torch.zeros((F, N, L), dtype=torch.complex64, device="cuda")
+        tx = torch.zeros((F * K, N, pid, M), dtype=torch.uint8, device="cuda")
+        starts, _ = S.generate_streams(iq, L, F, J, K, tx_idx=tx)
+        rs = torch.from_numpy(starts.view(np.int64).copy()).cuda()
+    else:
+        L = sp.max_frame_len()
+        iq = torch.empty((F, N, L), dtype=torch.complex64, device="cuda")
+        tx = torch.empty((F, N, pid, M), dtype=torch.uint8, device="cuda")
+        S.generate(iq, L, L, F, tx_idx=tx)
+        rs = None
+    wire, scale = _sc16_capture(iq, float(torch.view_as_real(iq).abs().max()) * 1.01)
+    wide = torch.empty_like(iq)
+    ingest_sc16(wire, L, wide, L, F * N, L, scale)
+    outs = []
+    for src, sc16 in ((wide, False), (wire, True)):
+        rxo = Receiver(RxParams(M=M, cp_len=cp, num_streams=N, num_access_codes=nac,
+                                pid_max=pid, detector=det, qam_order=qam))
+        sym = torch.zeros((F * K, N, pid, M), dtype=torch.complex64, device="cuda")
+        idx = torch.zeros((F * K, N, pid, M), dtype=torch.uint8, device="cuda")
+        rxo.set_timing(True)
+        rxo.process(src, L, L, F, max_out=pid, out_sym=sym, out_idx=idx, ref_mode=1,
+                    ref_idx=tx, frames_per_capture=K, ref_starts=rs, sc16=sc16,
+                    sc16_scale=scale)
+        torch.cuda.synchronize()
+        launches = rxo.stage_times()[_lib.STAGE_NAMES[0]][1]
+        outs.append((rxo.results(F * K), rxo.corr(F * K)[0], sym.cpu(), idx.cpu(),
+                     rxo.G(F * K), rxo.W(F * K), launches))
+    (ra, ca, sa, ia, ga, wa, na), (rb, cb, sb, ib, gb, wb, nb) = outs
+    # C2/C3 geometries read the wire samples in place; M = 512 (no streaming decode) widens
+    # them first, one extra launch timed with the S&C stage
+    assert nb == na + (1 if geom == "m512" else 0), (geom, na, nb)
+    ok = [i for i, r in enumerate(ra) if r["status"] == _lib.FRAME_OK]
+    assert len(ok) >= 1
+    assert torch.equal(ia, ib)
+    assert torch.equal(sa, sb), (sa - sb).abs().max()
+    for x, y in zip(ra, rb):
+        for k in ("status", "sync_index", "trigger", "num_samples_processed", "n_sym", "origin"):
+            assert x[k] == y[k], (k, x[k], y[k])
+    for i in ok:       # per-frame outputs exist for frames that reach the detector
+        assert np.array_equal(ca[i], cb[i])
+        assert np.array_equal(ga[i], gb[i]) and np.array_equal(wa[i], wb[i]), i
+        assert np.array_equal(ra[i]["evm_num"], rb[i]["evm_num"]), i
+        assert np.array_equal(ra[i]["errors"], rb[i]["errors"]), i
+
+
+def test_capture_ring_feeds_sc16_batch():
+    """The pinned-host capture ring (mimo_ring_*): a producer thread writes sc16
+    wire captures in ragged recv-sized chunks, the uploads land byte-exact in the bound device
+    captures, and the batch received from them equals the batch received from the same wire
+    samples made resident directly. Misuse (capacity overrun, double acquire) is an error."""
+    import threading
+    import torch
+    from rub_mimo_amd.ring import CaptureRing
+    M, cp, N, nac, pid, qam, F = 2048, 152, 4, 20, 60, 64, 2
+    sp = SynthParams(M=M, cp_len=cp, num_streams=N, num_access_codes=nac, pid=pid,
+                     qam_order=qam, seed=77, snr_db=30.0)
+    S = Synthesizer(sp)
+    L = sp.max_frame_len()
+    iq = torch.empty((F, N, L), dtype=torch.complex64, device="cuda")
+    tx = torch.empty((F, N, pid, M), dtype=torch.uint8, device="cuda")
+    S.generate(iq, L, L, F, tx_idx=tx)
+    wire, scale = _sc16_capture(iq, float(torch.view_as_real(iq).abs().max()) * 1.01)
+    host = wire.cpu().numpy()
+    cap = torch.zeros_like(wire)
+    ring = CaptureRing(N, chunk_samples=50000, n_chunks=3)
+    rng = np.random.default_rng(5)
+    errors = []
+
+    def producer():
+        try:
+            for f in range(F):
+                ring.bind(cap[f], L, L)
+                pos = 0
+                while pos < L:
+                    rows = ring.acquire()
+                    n = int(min(L - pos, rng.integers(1, ring.chunk + 1)))
+                    for a in range(N):
+                        rows[a][:n] = host[f, a, pos:pos + n]
+                    ring.commit(n)
+                    pos += n
+        except Exception as e:      # surfaced by the main thread
+            errors.append(e)
+
+    th = threading.Thread(target=producer)
+    th.start()
+    th.join(timeout=120)
+    assert not th.is_alive() and not errors, errors
+    stream = torch.cuda.current_stream().cuda_stream
+    assert ring.publish(stream) == L
+    torch.cuda.synchronize()
+    assert torch.equal(cap, wire)
+    # overrun and protocol errors are loud
+    rows = ring.acquire()
+    with pytest.raises(_lib.MimoError):
+        ring.acquire()
+    with pytest.raises(_lib.MimoError):
+        ring.commit(1)              # the bound capture is full
+    ring.bind(cap[0], L, 10)
+    ring.commit(10)
+    ring.close()
+    outs = []
+    for src in (wire, cap):
+        rxo = Receiver(RxParams(M=M, cp_len=cp, num_streams=N, num_access_codes=nac,
+                                pid_max=pid, detector=_lib.DET_MMSE, qam_order=qam))
+        sym = torch.zeros((F, N, pid, M), dtype=torch.complex64, device="cuda")
+        idx = torch.zeros((F, N, pid, M), dtype=torch.uint8, device="cuda")
+        if src is cap:
+            cap.copy_(wire)           # the ring's last test commit overwrote 10 samples
+        rxo.process(src, L, L, F, max_out=pid, out_sym=sym, out_idx=idx, ref_mode=1,
+                    ref_idx=tx, sc16=True, sc16_scale=scale)
+        torch.cuda.synchronize()
+        outs.append((rxo.results(F), sym.cpu(), idx.cpu()))
+    (ra, sa, ia), (rb, sb, ib) = outs
+    assert sum(r["status"] == _lib.FRAME_OK for r in ra) >= 1
+    for x, y in zip(ra, rb):
+        assert x["status"] == y["status"] and x["sync_index"] == y["sync_index"]
+    assert torch.equal(sa, sb) and torch.equal(ia, ib)

@@ -32,6 +32,7 @@ def main():
     ap.add_argument("--frames", type=int, required=True)
     ap.add_argument("--pid", type=int, required=True)
     ap.add_argument("--ref-mode", type=int, default=1)
+    ap.add_argument("--sample-format", default="fc32", choices=["fc32", "sc16"])
     ap.add_argument("-o", "--out", required=True)
     a = ap.parse_args()
     f = per_dispatch(a.fetch_csv, "FETCH_SIZE", a.kernel)
@@ -40,7 +41,7 @@ def main():
     write_b = statistics.median(w) * 1024.0
     out = {
         "config": {"M": a.M, "streams": a.streams, "frames": a.frames, "pid": a.pid,
-                   "ref_mode": a.ref_mode},
+                   "ref_mode": a.ref_mode, "sample_format": a.sample_format},
         "kernel": a.kernel,
         "dispatches": {"fetch": len(f), "write": len(w)},
         "fetch_size_kib_median": statistics.median(f),
