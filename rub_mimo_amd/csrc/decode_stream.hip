@@ -39,6 +39,11 @@
 
 namespace mimo {
 
+#ifdef DS_MARK
+#define MARK(s) asm volatile(s)
+#else
+#define MARK(s)
+#endif
 constexpr uint32_t kStreamMaxFrames = 192;   // per-frame tables in LDS beside a 157 KB working set
 constexpr uint32_t kStreamMaxQam = 256;          // constellation points (256-QAM)
 
@@ -138,6 +143,50 @@ MIMO_DEV void st_passes2(v2f *img, v2f *v, const v2f *twl, uint32_t tid) {
   }
 }
 
+// Wave-local form of the transform (M >= 2048, when its LDS layout fits): pass 0 is a radix-8
+// DIF step over stride MS = M/8 (thread n of antenna g: b_q = sum_r x[n + r MS] W8^{rq}, then
+// c_q[n] = b_q W_M^{nq}); X_g[8k + q] is then the MS-point DFT of c_q over n. The NA * 8
+// sub-transforms run on groups of LG = MS/8 lanes inside one wave (Stockham passes of
+// StreamPlan<log2 MS, 1>), exchanging through their own LDS region with no workgroup barrier,
+// and leave X_g[8k + q] at region (g, q), index k. Three barriers per symbol instead of nine.
+// Region stride QS = 4 mod 8 entries: the apply's reads of subcarriers k' = 8k + q (q fastest
+// across lanes) hit distinct banks.
+template <int LOG2M, int NA>
+struct WavePlan {
+  static constexpr int M = 1 << LOG2M, MS = M / 8, LG = MS / 8;
+  using SP = StreamPlan<LOG2M - 3, 1>;
+  static constexpr int QS = ((lds_padded_len(MS) + 3) / 8) * 8 + 4;
+  static constexpr int GS = 8 * QS;
+  static constexpr int TW0 = 4 * MS;                     // W_M^{nq}, q = 1..4, n < MS
+  static constexpr int TWS = [] {
+    int s = 0;
+    for (int p = 1; p < SP::NP; p++) s += (SP::radix(p) - 1) * SP::ns(p);
+    return s;
+  }();
+};
+
+// LDS writes of this wave visible to its own reads; no code motion across
+MIMO_DEV void lds_wave_sync() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_wave_barrier();
+}
+
+// sub-transform passes P .. NP-1 on a lane group (pass P-1's outputs in registers), ending with
+// the natural-order store
+template <int L2, int P>
+MIMO_DEV void wave_passes(v2f *buf, v2f *v, const v2f *twl, uint32_t s) {
+  using SP = StreamPlan<L2, 1>;
+  if constexpr (P < SP::NP) {
+    st_store<L2, 1, P - 1>(buf, v, s);
+    lds_wave_sync();
+    st_load_t<L2, 1, P>(buf, v, twl, s);
+    wave_passes<L2, P + 1>(buf, v, twl, s);
+  } else {
+    lds_wave_sync();
+    st_store<L2, 1, SP::NP - 1>(buf, v, s);
+  }
+}
+
 MIMO_DEV uint32_t cvt_u32_sat(float x) {   // v_cvt_u32_f32: NaN and negatives -> 0, saturating
   uint32_t r;
   asm("v_cvt_u32_f32 %0, %1" : "=v"(r) : "v"(x));
@@ -171,6 +220,11 @@ MIMO_DEV void dma16(uint32_t voff, __attribute__((address_space(1))) const void 
 // VGPRs); global address space, so accesses through it are global_* with an SGPR base and a
 // 32-bit lane offset, not flat_* (flat stores also count on lgkmcnt: every LDS wait would
 // drain them)
+MIMO_DEV uint64_t rfl64(uint64_t v) {   // a uniform 64-bit value, held in SGPRs
+  return (uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)v) |
+         ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32)) << 32);
+}
+
 template <typename P>
 using gptr = __attribute__((address_space(1))) P *;
 template <typename P>
@@ -179,6 +233,31 @@ MIMO_DEV gptr<P> sgpr_ptr(P *p) {
   const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
   const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
   return (gptr<P>)(((uint64_t)hi << 32) | lo);
+}
+
+constexpr size_t kStreamStaticLds = 6144;   // pfx, fbody, fcr, ptab (+ slack)
+
+// dynamic LDS of the kernel: FFT images, staging, reference staging, twiddle table
+template <int LOG2M, int NA>
+constexpr size_t stream_dyn_lds(bool wave_fft, int ref_mode, bool sc16) {
+  using PL = StreamPlan<LOG2M, NA>;
+  using WP = WavePlan<LOG2M, NA>;
+  size_t tw = 0;
+  if (wave_fft) {
+    tw = (size_t)WP::TW0 + WP::TWS;
+  } else {
+    for (int p = 1; p < PL::NP; p++) tw += (size_t)(PL::radix(p) - 1) * PL::ns(p);
+  }
+  const size_t img = wave_fft ? (size_t)NA * WP::GS : (size_t)NA * PL::PB;
+  const size_t stage = sc16 ? sizeof(short2) * (size_t)(PL::M + 4) * NA
+                            : sizeof(float2) * (size_t)(PL::M + 2) * NA;
+  return sizeof(float2) * (img + tw) + stage + (ref_mode == 1 ? (size_t)NA * PL::M : 0);
+}
+
+// the wave-local transform where its sub-transforms are >= 256 points and its layout fits
+template <int LOG2M, int NA, int REF, bool SC16>
+constexpr bool stream_wave_fft() {
+  return LOG2M >= 11 && stream_dyn_lds<LOG2M, NA>(true, REF, SC16) + kStreamStaticLds <= 163840;
 }
 
 template <int LOG2M, int NA, int REF, int OUTS, bool SC16 = false>
@@ -190,14 +269,17 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
   constexpr int SPC = SC16 ? 4 : 2;
   constexpr int SB = SC16 ? 4 : 8;                // bytes per staged sample
   constexpr int RS = M + SPC;
-  constexpr int NCH = NA * (RS / SPC);            // 16-byte chunks of one symbol's staging
-  constexpr int NDMA = (NCH + T - 1) / T;         // DMA instructions per thread
+  constexpr int NBLK = (RS / SPC + 63) / 64;      // wave DMA instructions per staged row
+  constexpr int NWI = (NA * NBLK + T / 64 - 1) / (T / 64);   // ... per wave and symbol
   constexpr int NREF = NA * M / 16;               // 16-byte chunks of the reference indices
   // store instructions per symbol: the wait at the top of a symbol leaves them in flight
   constexpr int NSTORE = ((OUTS & 1) ? NA * S : 0) + ((OUTS & 2) ? NA * S : 0);
+  using WP = WavePlan<LOG2M, NA>;
+  constexpr bool WF = stream_wave_fft<LOG2M, NA, REF, SC16>();
+  constexpr int MS = WP::MS, LG = WP::LG, QS = WP::QS, GS = WP::GS;
   extern __shared__ __attribute__((aligned(16))) float2 lds_raw[];
-  v2f *img = reinterpret_cast<v2f *>(lds_raw);                     // [NA][PB] FFT exchange
-  v2f *stg = img + NA * PB;                                        // [NA][RS] next symbol
+  v2f *img = reinterpret_cast<v2f *>(lds_raw);    // [NA][PB] FFT exchange ([NA][8][QS] if WF)
+  v2f *stg = img + NA * (WF ? GS : PB);                            // [NA][RS] next symbol
   short2 *stg16 = reinterpret_cast<short2 *>(stg);                 // (sc16 staging)
   uint8_t *rstg = reinterpret_cast<uint8_t *>(stg) + (size_t)NA * RS * SB;   // [NA][M] next references
   v2f *twl = reinterpret_cast<v2f *>(rstg + ((REF == 1) ? NA * M : 0));   // twiddle table
@@ -213,7 +295,24 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
   }
 
   // twiddles of passes 1..NP-1: twl[off(p) + (r-1) NS + jm] = e^{-2 pi i jm r / (NS R)}
-  {
+  if constexpr (WF) {
+    // W_M^{nq} (q = 1..4, n < MS), then the sub-transform plan's passes
+    for (int e = tid; e < WP::TW0; e += T) {
+      const int q = e / MS + 1, n = e % MS;
+      twl[e] = twiddle<false>(a.tw, ((n * q) % M) * (kTwN / M));
+    }
+    using SP = typename WP::SP;
+    int off = WP::TW0;
+#pragma unroll
+    for (int p = 1; p < SP::NP; p++) {
+      const int R = SP::radix(p), NS = SP::ns(p);
+      for (int e = tid; e < (R - 1) * NS; e += T) {
+        const int r = e / NS + 1, jm = e % NS;
+        twl[off + e] = twiddle<false>(a.tw, ((jm * r) % (NS * R)) * (kTwN / (NS * R)));
+      }
+      off += (R - 1) * NS;
+    }
+  } else {
     int off = 0;
 #pragma unroll
     for (int p = 1; p < PL::NP; p++) {
@@ -268,6 +367,7 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
   uint32_t s = __builtin_amdgcn_readfirstlane(i_begin - pfx[f]);
   uint32_t n_out_f = __builtin_amdgcn_readfirstlane(pfx[f + 1] - pfx[f]);
 
+  const uint64_t rowstep = rfl64((uint64_t)a.max_out * a.M_occ);   // samples between streams
   const v2f inv_sc = v2f{a.qam.inv_scale, a.qam.inv_scale};
   const v2f Lf = v2f{(float)a.qam.L, (float)a.qam.L};
   const uint32_t Lm1 = a.qam.L - 1;
@@ -290,18 +390,28 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
 #pragma unroll
     for (int g = 0; g < NA; g++)
       odds |= (uint32_t)((e0 + (int64_t)g * a.stride) & (SPC - 1)) << (4 * g);
+#ifdef DS_ABL_NODMA   // timing ablation (tools/abl_decode.sh): no sample loads
+    if (true) {
+    } else
+#endif
     if (abs0 >= SPC && abs0 + RS <= (int64_t)a.frame_len && ((uintptr_t)a.iq & 15u) == 0) {
-      // base SPC samples before row 0's aligned start: every row's a_g - base is in [0, 2^32)
+      // base SPC samples before row 0's aligned start: every row's a_g - base is in [0, 2^32).
+      // One wave instruction moves 64 consecutive chunks of one row (row g, block b uniform;
+      // a row's last block is its one remaining chunk), so the lane offsets are a scalar plus
+      // 16 * lane
       const int64_t base = (e0 & ~(int64_t)(SPC - 1)) - SPC;
       const auto xa = sgpr_ptr(reinterpret_cast<const char *>(a.iq) + base * SB);
+      const uint32_t lane16 = (uint32_t)(opq(tid) & 63) * 16u;
 #pragma unroll
-      for (int u = 0; u < NDMA; u++) {
-        const int c = u * T + t0;
-        const uint32_t dst = __builtin_amdgcn_readfirstlane(stg_base + (uint32_t)(u * T + wv * 64) * 16u);
-        if (u < NCH / T || c < NCH) {
-          const uint32_t g = (uint32_t)c / (RS / SPC), q = (uint32_t)c % (RS / SPC);
-          const int64_t ag = (e0 + (int64_t)g * a.stride) & ~(int64_t)(SPC - 1);
-          dma16((uint32_t)(ag - base + SPC * q) * (uint32_t)SB, xa, dst);
+      for (int u = 0; u < NWI; u++) {
+        const uint32_t k = wv + (uint32_t)u * (T / 64);
+        if (u < NWI - 1 || k < (uint32_t)(NA * NBLK)) {
+          const uint32_t g = k / NBLK, b = k % NBLK;
+          const uint32_t rowoff = (uint32_t)(((e0 + (int64_t)g * a.stride) & ~(int64_t)(SPC - 1)) - base);
+          const uint32_t dst = __builtin_amdgcn_readfirstlane(
+              stg_base + (g * RS + b * 64u * SPC) * (uint32_t)SB);
+          const uint32_t voff = __builtin_amdgcn_readfirstlane((rowoff + b * 64u * SPC) * (uint32_t)SB);
+          if (b + 1 < NBLK || lane16 == 0) dma16(voff + lane16, xa, dst);
         }
       }
     } else {                                          // edge of the capture: guarded loads
@@ -393,6 +503,7 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
   __syncthreads();                                    // twiddle table and guarded staging
   for (uint32_t i = i_begin; i < i_end; i++) {
     // this symbol's staging has landed (the previous symbol's stores may still be in flight)
+    MARK(";@@A top");
     asm volatile("s_waitcnt vmcnt(%0)" :: "n"(NSTORE) : "memory");
     __syncthreads();
     v2f v[8];
@@ -425,8 +536,26 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
           cref[e / 4] |= (uint32_t)rstg[t * M + t0 + q * T] << (8 * (e % 4));
         }
     }
+    MARK(";@@B pass0");
     dft_fwd_pk<8>(v);
+    if constexpr (WF) {     // pass 0's twiddles W_M^{nq}; c_q[n] to region (g, q)
+      const int t0 = opq(tid);
+      const int n = t0 % MS, g = t0 / MS;
+      const v2f *w = twl + n;
+      const v2f w1 = w[0], w2 = w[MS], w3 = w[2 * MS], w4 = w[3 * MS];
+      v[1] = cmul_pk(v[1], w1);
+      v[2] = cmul_pk(v[2], w2);
+      v[3] = cmul_pk(v[3], w3);
+      v[4] = cmul_pk(v[4], w4);
+      v[5] = cmul_pk(v[5], cmul_pk(w4, w1));
+      v[6] = cmul_pk(v[6], cmul_pk(w4, w2));
+      v[7] = cmul_pk(v[7], cmul_pk(w4, w3));
+      v2f *e = img + g * GS + lds_pad(n);
+#pragma unroll
+      for (int q = 0; q < 8; q++) e[q * QS] = v[q];
+    }
     __syncthreads();                                  // staging consumed by every wave
+    MARK(";@@C fetch");
     // the item after this one (uniform) and its staging, in flight during this symbol
     uint32_t fn = f, sn = s + 1, n_out_n = n_out_f;
     uint32_t odd_n = 0;
@@ -444,28 +573,56 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
     // passes 1 .. NP-1 through the LDS images (pass 1 needs no leading barrier: the previous
     // symbol's image readers finished before the barrier at the top), then the exchange that
     // leaves the spectra in natural order
-    st_store<LOG2M, NA, 0>(img, v, (uint32_t)opq(tid));
-    st_passes2<LOG2M, NA, 1>(img, v, twl, tid);
-    {
-      const uint32_t t = (uint32_t)opq(tid);
+    MARK(";@@D subfft");
+    if constexpr (WF) {
+      // sub-transform (g, q) on lane group t0 / LG, inside one wave
+      const int t0 = opq(tid);
+      const uint32_t s = (uint32_t)(t0 % LG);
+      const int sg = t0 / LG;
+      v2f *rg = img + (sg >> 3) * GS + (sg & 7) * QS;
+#pragma unroll
+      for (int r = 0; r < 8; r++) v[r] = rg[lds_pad((int)s + r * LG)];
+      dft_fwd_pk<8>(v);
+      wave_passes<LOG2M - 3, 1>(rg, v, twl + WP::TW0, s);
+      __syncthreads();                                // every spectrum in its region
+    } else {
+      st_store<LOG2M, NA, 0>(img, v, (uint32_t)opq(tid));
+#ifndef DS_ABL_NOFFT   // timing ablation: no passes 1.. and no final exchange
+      st_passes2<LOG2M, NA, 1>(img, v, twl, tid);
+      {
+        const uint32_t t = (uint32_t)opq(tid);
+        __syncthreads();
+        st_store<LOG2M, NA, PL::NP - 1>(img, v, t);
+        __syncthreads();
+      }
+#else
       __syncthreads();
-      st_store<LOG2M, NA, PL::NP - 1>(img, v, t);
-      __syncthreads();
+#endif
     }
 
+    MARK(";@@E apply");
     // apply, demap, EVM, stores: subcarrier k = tid + q T of every stream
     const uint64_t frame_id = a.frame_id0 + (fcr[f] >> 16);
+    // output row (f, t, s) = ob0 + t * max_out * M_occ: uniform, one 64-bit product per symbol
+    const uint64_t ob0 = rfl64((((uint64_t)f * NA) * a.max_out + s) * a.M_occ);
 #pragma unroll
     for (int q = 0; q < S; q++) {
       const uint32_t k = (uint32_t)opq(tid) + q * T;
       v2f X[NA];
-      const v2f *xp = img + lds_pad((int)(uint32_t)opq(tid)) + q * (T + T / 32);
+      if constexpr (WF) {
+        const uint32_t kk = (uint32_t)opq(tid) + q * T;
+        const v2f *xp = img + (kk & 7u) * QS + lds_pad((int)(kk >> 3));
 #pragma unroll
-      for (int r = 0; r < NA; r++) X[r] = xp[r * PB];
+        for (int r = 0; r < NA; r++) X[r] = xp[r * GS];
+      } else {
+        const v2f *xp = img + lds_pad((int)(uint32_t)opq(tid)) + q * (T + T / 32);
+#pragma unroll
+        for (int r = 0; r < NA; r++) X[r] = xp[r * PB];
+      }
 #pragma unroll
       for (int t = 0; t < NA; t++) {
         // uniform row bases (SGPRs): the stores take a 32-bit per-lane offset
-        const uint64_t ob = (((uint64_t)f * NA + t) * a.max_out + s) * a.M_occ;
+        const uint64_t ob = ob0 + (uint64_t)t * rowstep;
         const auto osym = sgpr_ptr(reinterpret_cast<v2f *>(a.out_sym + ob));
         const auto oidx = sgpr_ptr(a.out_idx + ob);
         v2f acc = v2f{0.0f, 0.0f};
@@ -484,12 +641,15 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
         const v2f er = acc - sp;
         e_num[t] = __builtin_fmaf(er.x, er.x, __builtin_fmaf(er.y, er.y, e_num[t]));
         e_den[t] = __builtin_fmaf(sp.x, sp.x, __builtin_fmaf(sp.y, sp.y, e_den[t]));
+#ifndef DS_ABL_NOSTORE   // timing ablation: no symbol / index stores
         if constexpr (OUTS & 1)
           *(gptr<v2f>)((gptr<char>)osym + k * (uint32_t)sizeof(v2f)) = acc;
         if constexpr (OUTS & 2) oidx[k] = (uint8_t)d;
+#endif
       }
     }
 
+    MARK(";@@F tail");
     const bool last = (i + 1 == i_end);
     if (last || fn != f) {
       flush(f);
@@ -498,6 +658,7 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
         load_w(fn);
       }
     }
+    MARK(";@@G next");
     f = __builtin_amdgcn_readfirstlane(fn);
     s = __builtin_amdgcn_readfirstlane(sn);
     odd = __builtin_amdgcn_readfirstlane(odd_n);
@@ -508,13 +669,11 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
 // not handled here (the caller then uses the per-symbol kernels)
 template <int LOG2M, int NA>
 static size_t stream_lds_bytes(int ref_mode, bool sc16) {
-  using PL = StreamPlan<LOG2M, NA>;
-  size_t tw = 0;
-  for (int p = 1; p < PL::NP; p++) tw += (size_t)(PL::radix(p) - 1) * PL::ns(p);
-  const size_t stage = sc16 ? sizeof(short2) * (size_t)(PL::M + 4) * NA
-                            : sizeof(float2) * (size_t)(PL::M + 2) * NA;
-  return sizeof(float2) * ((size_t)PL::PB * NA + tw) + stage +
-         (ref_mode == 1 ? (size_t)NA * PL::M : 0);
+  const bool wf = ref_mode == 1 ? (sc16 ? stream_wave_fft<LOG2M, NA, 1, true>()
+                                        : stream_wave_fft<LOG2M, NA, 1, false>())
+                                : (sc16 ? stream_wave_fft<LOG2M, NA, 0, true>()
+                                        : stream_wave_fft<LOG2M, NA, 0, false>());
+  return stream_dyn_lds<LOG2M, NA>(wf, ref_mode, sc16);
 }
 
 template <int LOG2M, int NA>
