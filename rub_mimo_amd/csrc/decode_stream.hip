@@ -539,8 +539,8 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
     MARK(";@@B pass0");
     dft_fwd_pk<8>(v);
     if constexpr (WF) {     // pass 0's twiddles W_M^{nq}; c_q[n] to region (g, q)
-      const int t0 = opq(tid);
-      const int n = t0 % MS, g = t0 / MS;
+      const uint32_t t0 = (uint32_t)opq(tid);
+      const uint32_t n = t0 % MS, g = t0 / MS;
       const v2f *w = twl + n;
       const v2f w1 = w[0], w2 = w[MS], w3 = w[2 * MS], w4 = w[3 * MS];
       v[1] = cmul_pk(v[1], w1);
@@ -550,7 +550,7 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
       v[5] = cmul_pk(v[5], cmul_pk(w4, w1));
       v[6] = cmul_pk(v[6], cmul_pk(w4, w2));
       v[7] = cmul_pk(v[7], cmul_pk(w4, w3));
-      v2f *e = img + g * GS + lds_pad(n);
+      v2f *e = img + g * GS + lds_pad((int)n);
 #pragma unroll
       for (int q = 0; q < 8; q++) e[q * QS] = v[q];
     }
@@ -576,12 +576,13 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
     MARK(";@@D subfft");
     if constexpr (WF) {
       // sub-transform (g, q) on lane group t0 / LG, inside one wave
-      const int t0 = opq(tid);
-      const uint32_t s = (uint32_t)(t0 % LG);
-      const int sg = t0 / LG;
+      static_assert(LG % 32 == 0, "lds_pad(s + r LG) = lds_pad(s) + r (LG + LG/32)");
+      const uint32_t t0 = (uint32_t)opq(tid);
+      const uint32_t s = t0 & (LG - 1), sg = t0 / LG;
       v2f *rg = img + (sg >> 3) * GS + (sg & 7) * QS;
+      const v2f *rp = rg + lds_pad((int)s);
 #pragma unroll
-      for (int r = 0; r < 8; r++) v[r] = rg[lds_pad((int)s + r * LG)];
+      for (int r = 0; r < 8; r++) v[r] = rp[r * (LG + LG / 32)];
       dft_fwd_pk<8>(v);
       wave_passes<LOG2M - 3, 1>(rg, v, twl + WP::TW0, s);
       __syncthreads();                                // every spectrum in its region
@@ -628,6 +629,16 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
         v2f acc = v2f{0.0f, 0.0f};
 #pragma unroll
         for (int r = 0; r < NA; r++) acc = cmac_pk(acc, Wr[t][r][q], X[r]);
+#ifdef DS_ABL_NODEMAP   // timing ablation: no demap / EVM
+        {
+#ifndef DS_ABL_NOSTORE
+          if constexpr (OUTS & 1)
+            *(gptr<v2f>)((gptr<char>)osym + k * (uint32_t)sizeof(v2f)) = acc;
+          if constexpr (OUTS & 2) oidx[k] = (uint8_t)0;
+#endif
+          continue;
+        }
+#endif
         const uint32_t d = qam_slice_pk(acc, inv_sc, Lf, Lm1, a.qam.b);
         uint32_t refi;
         if constexpr (REF == 1) refi = (cref[(t * S + q) / 4] >> (8 * ((t * S + q) % 4))) & 0xFFu;

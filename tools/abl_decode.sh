@@ -8,13 +8,15 @@ OBJ=../../build/obj
 OUT=../../build/abl
 mkdir -p $OUT
 make -j8 >/dev/null
-for v in base nostore nodma nofft nostore_nodma; do
+for v in ${VARIANTS:-base nostore nodma nofft nostore_nodma nodemap}; do
   case $v in
     base) D="" ;;
     nostore) D="-DDS_ABL_NOSTORE" ;;
     nodma) D="-DDS_ABL_NODMA" ;;
     nofft) D="-DDS_ABL_NOFFT" ;;
     nostore_nodma) D="-DDS_ABL_NOSTORE -DDS_ABL_NODMA" ;;
+    nodemap) D="-DDS_ABL_NODEMAP" ;;
+    all_off) D="-DDS_ABL_NOSTORE -DDS_ABL_NODMA -DDS_ABL_NODEMAP" ;;
   esac
   /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -I../../include $D $EXTRA \
     -c decode_stream.hip -o $OUT/ds_$v.o

@@ -3,8 +3,11 @@
 set -o pipefail
 O=gpurun_out/${TAG:-q}
 mkdir -p $O
-if [ -n "$TESTS" ]; then
-  timeout -k 10 500 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread $TESTS > $O/gpu_tests.log 2>&1 || { echo "gpu tests failed"; tail -n 40 $O/gpu_tests.log; exit 1; }
+# TESTS: unset = no tests, "all" (or blank) = every gpu test, anything else = a -k expression
+if [ -n "${TESTS+x}" ]; then
+  K=()
+  if [ -n "${TESTS// /}" ] && [ "$TESTS" != all ]; then K=(-k "$TESTS"); fi
+  timeout -k 10 500 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread "${K[@]}" > $O/gpu_tests.log 2>&1 || { echo "gpu tests failed"; tail -n 40 $O/gpu_tests.log; exit 1; }
   tail -n 2 $O/gpu_tests.log
 fi
 for w in ${WORKLOADS:-c3}; do
