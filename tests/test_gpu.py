@@ -296,7 +296,8 @@ def test_framegen_matches_oracle_tx():
         assert np.array_equal(tx[t, :cp], tx[t, M:])      # cyclic prefix
 
 
-def _c_frame_parity(M, cp, N, nac, pid, qam, det, snr, seed, bias=True, max_delta=SYM_TOL):
+def _c_frame_parity(M, cp, N, nac, pid, qam, det, snr, seed, bias=True, max_delta=SYM_TOL,
+                    search_mode=0):
     S = Synthesizer(SynthParams(M=M, cp_len=cp, num_streams=N, num_access_codes=nac, pid=pid,
                                 qam_order=qam, seed=seed, snr_db=snr))
     L = S.frame_len(0)
@@ -314,7 +315,7 @@ def _c_frame_parity(M, cp, N, nac, pid, qam, det, snr, seed, bias=True, max_delt
     r = rxo.results()[0]
     ci, si = rxo.corr()
     o = ref.FrameSyncRef(M, cp, N, nac, pid_max=pid, detector=det, keep_identity_bias=bias,
-                         trace_corr=True)
+                         trace_corr=True, search_mode=search_mode)
     assert o.execute(rx) == ref.STATE_MIMO
     assert r["status"] == _lib.FRAME_OK
     assert r["sync_index"] == o.get_sync_index()
@@ -355,6 +356,16 @@ def test_c3_4x4_mmse_2048_64qam_full_frame():
 def test_c4_8x8_mmse_4096_256qam_reduced_codes():
     """C4 geometry with 2 access codes so the brute-force oracle stays within ~30 s."""
     _c_frame_parity(4096, 304, 8, 2, 12, 256, _lib.DET_MMSE, 35.0, seed=41, bias=False)
+
+
+def test_c4_full_codes_against_parseval_oracle():
+    """C4 with all 20 access codes per stream (160 codes, 8 rx) on a reduced PID. The oracle
+    runs its Parseval search variant (search_mode 1: one overlap-save correlation per (rx,
+    code), pinned to the brute force by test_parseval_search_variant_matches_brute_force);
+    the brute force itself would be ~1.4 TFLOP per frame. Sync bit-exact, corr indices exact
+    wherever the peak is unambiguous, symbols within the EVM tolerance."""
+    _c_frame_parity(4096, 304, 8, 20, 12, 256, _lib.DET_MMSE, 35.0, seed=43, bias=False,
+                    search_mode=1)
 
 
 @pytest.mark.parametrize("det", [_lib.DET_ZF, _lib.DET_MMSE])
