@@ -140,7 +140,9 @@ def decode_kernel_name(M, N, args):
         return "decode_stream_kernel<%d,%d>" % (lg, N)
     if 512 <= M <= 4096 and N in (2, 4):
         return "decode_reg_kernel<%d,%d>" % (lg, N)
-    return "decode_persistent_kernel"
+    if M < 512 and N in (2, 4):
+        return "decode_persistent_kernel"
+    return "decode_kernel<%d,%d>" % (lg, N)
 
 
 def cpu_model():
