@@ -142,6 +142,9 @@ def decode_kernel_name(M, N, args):
         return "decode_reg_kernel<%d,%d>" % (lg, N)
     if M < 512 and N in (2, 4):
         return "decode_persistent_kernel"
+    if (N == 8 and 512 <= M <= 4096 and args.detector != "siso" and args.pid >= M // 64
+            and os.environ.get("RMIMO_DECODE_SPLIT", "1") != "0"):
+        return "spectra_kernel<%d>|apply_split_kernel<8>" % lg
     return "decode_kernel<%d,%d>" % (lg, N)
 
 
@@ -502,7 +505,7 @@ def main():
             if ((cfgm.get("M"), cfgm.get("streams"), cfgm.get("frames"), cfgm.get("pid"),
                     cfgm.get("ref_mode"), cfgm.get("sample_format", "fc32"))
                     == (M, N, F, pid, args.ref_mode, args.sample_format)
-                    and pm.get("kernel") == kname.split("<")[0]):
+                    and pm.get("kernel") == "|".join(x.split("<")[0] for x in kname.split("|"))):
                 traffic = pm.get("decode_hbm_bytes_per_launch")
         except Exception:
             traffic = None

@@ -832,7 +832,8 @@ uint32_t launch_decode(const DecodeArgs &a, int log2M, uint32_t n_frames, hipStr
                        bool *per_frame_records) {
   *per_frame_records = false;
   if (a.expt == 0) {
-    const uint32_t parts = launch_decode_stream(a, log2M, n_frames, s);
+    uint32_t parts = launch_decode_stream(a, log2M, n_frames, s);
+    if (!parts) parts = launch_decode_split(a, log2M, n_frames, s);
     if (parts) {
       *per_frame_records = true;
       return parts;

@@ -676,6 +676,206 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
   }
 }
 
+// ------------------------------------------------------------------------------------
+// Split decode for 8x8 (C4: one symbol is 8 x 4096 x 8 B = 256 KB, more than LDS, and its
+// weights are 2 MB per frame, so neither a symbol nor a frame's W fits a workgroup):
+//   1. spectra_kernel: one workgroup per (frame, symbol, antenna) transforms the body in LDS
+//      and writes X to a scratch laid out [frame][chunk of 64 subcarriers][symbol][antenna][64]
+//      -- the apply of one chunk then reads 4 KB contiguous per symbol;
+//   2. apply_split_kernel: one workgroup per (frame, chunk, symbol range) keeps W*gain*dn of
+//      its 64 subcarriers in registers (wave h: outputs 2h and 2h+1, 32 VGPRs) and streams
+//      the range's symbols through the 8x8 apply, demap, EVM and stores.
+// Weights are read once per (chunk, range) instead of once per symbol (the per-symbol kernel
+// reads 2 MB of W from L2 for every 256 KB symbol); the spectra make one extra HBM round
+// trip (2 x 256 KB per symbol). EVM records: chunk x range per frame (nrec), NA/2 per record.
+constexpr uint32_t kSplitSets = 16;   // EVM partial sets per record (<= kMaxEvmParts)
+
+template <int LOG2M, int T>
+__global__ __launch_bounds__(T) void spectra_kernel(DecodeArgs a) {
+  constexpr int M = 1 << LOG2M, NCH = M / 64;
+  extern __shared__ __attribute__((aligned(16))) float2 lds_sp[];
+  const uint32_t f = blockIdx.y, s = blockIdx.x, r = blockIdx.z;
+  const FrameInfo &I = a.info[f];
+  const uint32_t n_out = (I.status == 0) ? min(I.n_sym, a.max_out) : 0u;
+  if (s >= n_out) return;                             // uniform
+  const int64_t abs0 = I.base + (int64_t)I.i0 + (int64_t)s * a.SL + a.cp;
+  const int64_t L = (int64_t)a.frame_len;
+  const float2 *x = a.iq + ((uint64_t)I.cap * a.N + r) * a.stride;
+  const int tid = threadIdx.x;
+  if (abs0 >= 0 && abs0 + M <= L && ((uintptr_t)(x + abs0) & 15u) == 0) {
+    const float4 *x4 = reinterpret_cast<const float4 *>(x + abs0);
+#pragma unroll
+    for (int i = tid; i < M / 2; i += T) {
+      const float4 v = x4[i];
+      lds_sp[lds_pad(2 * i)] = make_float2(v.x, v.y);
+      lds_sp[lds_pad(2 * i + 1)] = make_float2(v.z, v.w);
+    }
+  } else {
+    for (int i = tid; i < M; i += T) {
+      const int64_t n = abs0 + i;
+      lds_sp[lds_pad(i)] = (n >= 0 && n < L) ? x[n] : make_float2(0.0f, 0.0f);
+    }
+  }
+  __syncthreads();
+  fft_lds<LOG2M, T, 1, false>(lds_sp, a.tw);
+  float2 *o = a.spec + (((uint64_t)f * NCH * a.max_out + s) * a.N + r) * 64;
+  const uint64_t cstep = (uint64_t)a.max_out * a.N * 64;
+#pragma unroll
+  for (int k = tid; k < M; k += T) o[(uint64_t)(k >> 6) * cstep + (k & 63)] = lds_sp[lds_pad(k)];
+}
+
+template <int NA, int REF>
+__global__ __launch_bounds__(32 * NA) void apply_split_kernel(DecodeArgs a) {
+  constexpr int T = 32 * NA;                          // NA/2 waves
+  constexpr int PF = 4;                               // symbols in flight per workgroup
+  static_assert(NA == 8, "one 16-byte load per thread covers a symbol's 8 x 64 spectra");
+  const uint32_t c = blockIdx.x, f = blockIdx.y, part = blockIdx.z;
+  const uint32_t NCH = gridDim.x, P = gridDim.z;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const uint32_t h = __builtin_amdgcn_readfirstlane((uint32_t)tid >> 6);
+  __shared__ v2f ptab[kStreamMaxQam];
+  __shared__ __attribute__((aligned(16))) v2f xs[2][NA * 64];    // spectra of one symbol
+  __shared__ __attribute__((aligned(16))) uint8_t rs[2][NA * 64];  // its reference indices
+  for (uint32_t e = tid; e < a.qam.L * a.qam.L; e += T) {
+    const float2 p = qam_point(e, a.qam);
+    ptab[e] = v2f{p.x, p.y};
+  }
+  const FrameInfo &I = a.info[f];
+  const uint32_t n_out = (I.status == 0) ? min(I.n_sym, a.max_out) : 0u;
+  if (c == 0 && part == 0 && tid == 0) a.nrec[f] = NCH * P * (T / 64) / kSplitSets;
+  const uint32_t s0 = (uint32_t)((uint64_t)n_out * part / P);
+  const uint32_t s1 = (uint32_t)((uint64_t)n_out * (part + 1) / P);
+  const uint32_t M = a.M, k = c * 64 + lane;
+  v2f Wr[2][NA];
+  {
+    const float gk = a.gain[(uint64_t)f * M + k] * a.dn;
+#pragma unroll
+    for (int tt = 0; tt < 2; tt++)
+#pragma unroll
+      for (int r = 0; r < NA; r++) {
+        const float2 w = a.W[(((uint64_t)f * NA + 2 * h + tt) * NA + r) * M + k];
+        Wr[tt][r] = v2f{w.x * gk, w.y * gk};
+      }
+  }
+  const v2f inv_sc = v2f{a.qam.inv_scale, a.qam.inv_scale};
+  const v2f Lf = v2f{(float)a.qam.L, (float)a.qam.L};
+  const uint32_t Lm1 = a.qam.L - 1;
+  const uint64_t frame_id = a.frame_id0 + I.ref;
+  // symbol s of this chunk: 4 KB at spec4 + s * 256 (16 B per thread), reference indices of
+  // stream t at ref + (t * max_out + s) * M_occ (16 B per thread for tid < 32)
+  const float4 *spec4 = reinterpret_cast<const float4 *>(a.spec) +
+                        ((uint64_t)f * NCH + c) * a.max_out * (NA * 64 / 2) + tid;
+  const uint8_t *refb = (REF == 1) ? a.ref_idx + ((uint64_t)I.ref * NA + (tid >> 2)) * a.max_out * a.M_occ +
+                                         c * 64 + (tid & 3) * 16
+                                   : nullptr;
+  // symbols in flight: slot u holds symbol sb + u; loads are unconditional (past the range
+  // they re-read the last symbol) so the slots stay in registers with counted waits
+  const uint32_t slast = s1 > s0 ? s1 - 1 : s0;
+  float4 pf0, pf1, pf2, pf3;                           // symbol slots (named: no scratch)
+  uint4 pr0, pr1, pr2, pr3;
+  auto load_sym = [&](float4 &x, uint4 &r, uint32_t s) {
+    const uint32_t sc = min(s, slast);
+    x = spec4[(uint64_t)sc * (NA * 64 / 2)];
+    if constexpr (REF == 1)
+      if (tid < 32) r = *reinterpret_cast<const uint4 *>(refb + (uint64_t)sc * a.M_occ);
+  };
+  if (s0 < s1) {
+    load_sym(pf0, pr0, s0);
+    load_sym(pf1, pr1, s0 + 1);
+    load_sym(pf2, pr2, s0 + 2);
+    load_sym(pf3, pr3, s0 + 3);
+  }
+  float e_num[2] = {0.0f, 0.0f}, e_den[2] = {0.0f, 0.0f};
+  uint32_t n_err[2] = {0u, 0u};
+  // one symbol: slot -> LDS, refill the slot PF symbols ahead, barrier, apply + demap + EVM
+  auto one = [&](float4 &x, uint4 &r, uint32_t s, int b) {
+    reinterpret_cast<float4 *>(xs[b])[tid] = x;
+    if constexpr (REF == 1)
+      if (tid < 32) reinterpret_cast<uint4 *>(rs[b])[tid] = r;
+    load_sym(x, r, s + PF);
+    __syncthreads();                                  // xs[b] complete; xs[b^1] readers done
+    if (s >= s1) return;                              // uniform: the range's last block
+    v2f X[NA];
+#pragma unroll
+    for (int q = 0; q < NA; q++) X[q] = xs[b][q * 64 + lane];
+#pragma unroll
+    for (int tt = 0; tt < 2; tt++) {
+      const uint32_t t = 2 * h + tt;
+      v2f acc = v2f{0.0f, 0.0f};
+#pragma unroll
+      for (int q = 0; q < NA; q++) acc = cmac_pk(acc, Wr[tt][q], X[q]);
+      const uint32_t d = qam_slice_pk(acc, inv_sc, Lf, Lm1, a.qam.b);
+      const uint64_t o = (((uint64_t)f * NA + t) * a.max_out + s) * a.M_occ + k;
+      uint32_t refi;
+      if constexpr (REF == 1) refi = rs[b][t * 64 + lane];
+      else if constexpr (REF == 2)
+        refi = (uint32_t)(hash5(a.ref_seed, DOM_DATA, frame_id, t, (uint64_t)s * a.M_occ + k) &
+                          (uint64_t)(a.qam.L * a.qam.L - 1));
+      else refi = d;
+      n_err[tt] += (uint32_t)__builtin_popcountll(__builtin_amdgcn_ballot_w64(refi != d));
+      const v2f pt = ptab[refi];
+      const v2f er = acc - pt;
+      e_num[tt] = __builtin_fmaf(er.x, er.x, __builtin_fmaf(er.y, er.y, e_num[tt]));
+      e_den[tt] = __builtin_fmaf(pt.x, pt.x, __builtin_fmaf(pt.y, pt.y, e_den[tt]));
+#ifndef SPLIT_ABL_NOSTORE   // timing ablation: no output stores
+      if (a.out_sym) reinterpret_cast<v2f *>(a.out_sym)[o] = acc;
+      if (a.out_idx) a.out_idx[o] = (uint8_t)d;
+#endif
+    }
+  };
+  for (uint32_t sb = s0; sb < s1; sb += PF) {
+    one(pf0, pr0, sb, 0);
+    one(pf1, pr1, sb + 1, 1);
+    one(pf2, pr2, sb + 2, 0);
+    one(pf3, pr3, sb + 3, 1);
+  }
+#pragma unroll
+  for (int tt = 0; tt < 2; tt++)
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+      e_num[tt] += __shfl_xor(e_num[tt], off);
+      e_den[tt] += __shfl_xor(e_den[tt], off);
+    }
+  // partial set (c * P + part) * waves + h: this wave's two streams, zeros elsewhere
+  const uint64_t set = ((uint64_t)c * P + part) * (T / 64) + h;
+  double *ep = a.evm_part + ((uint64_t)f * a.max_out * kSplitSets + set) * NA * 3;
+  if (lane < NA * 3) {
+    const uint32_t t = lane / 3, comp = lane % 3;
+    float v = 0.0f;
+#pragma unroll
+    for (int tt = 0; tt < 2; tt++)
+      if (t == 2 * h + tt) v = comp == 0 ? e_num[tt] : (comp == 1 ? e_den[tt] : (float)n_err[tt]);
+    ep[lane] = (double)v;
+  }
+}
+
+// 8x8 split decode; returns the partial sets per record (0: not handled)
+uint32_t launch_decode_split(const DecodeArgs &a, int log2M, uint32_t n_frames, hipStream_t s) {
+  if (!a.spec || !a.nrec || a.sc16 || a.N != 8 || a.detector == 3 || !a.all_occ ||
+      log2M < 9 || log2M > 12 || a.qam.L * a.qam.L > kStreamMaxQam)
+    return 0;
+  const uint32_t NCH = a.M / 64;
+  // symbol ranges per chunk: many short workgroups (no tail round), records
+  // NCH * P * 4 / kSplitSets <= max_out, whole records
+  uint32_t P = std::min<uint32_t>(16, a.max_out * kSplitSets / (NCH * 4));
+  while (P > 0 && (NCH * P * 4) % kSplitSets) P--;
+  if (P == 0) return 0;
+  constexpr int T1 = 512;
+  const size_t shm = sizeof(float2) * lds_padded_len(1 << log2M);
+  const dim3 g1(a.max_out, n_frames, a.N);
+  switch (log2M) {
+    case 9: hipLaunchKernelGGL((spectra_kernel<9, T1>), g1, dim3(T1), shm, s, a); break;
+    case 10: hipLaunchKernelGGL((spectra_kernel<10, T1>), g1, dim3(T1), shm, s, a); break;
+    case 11: hipLaunchKernelGGL((spectra_kernel<11, T1>), g1, dim3(T1), shm, s, a); break;
+    default: hipLaunchKernelGGL((spectra_kernel<12, T1>), g1, dim3(T1), shm, s, a); break;
+  }
+  const dim3 g2(NCH, n_frames, P);
+  if (a.ref_mode == 1) hipLaunchKernelGGL((apply_split_kernel<8, 1>), g2, dim3(256), 0, s, a);
+  else if (a.ref_mode == 2) hipLaunchKernelGGL((apply_split_kernel<8, 2>), g2, dim3(256), 0, s, a);
+  else hipLaunchKernelGGL((apply_split_kernel<8, 0>), g2, dim3(256), 0, s, a);
+  return kSplitSets;
+}
+
 // returns the EVM partial sets per record (waves per workgroup), 0 when the configuration is
 // not handled here (the caller then uses the per-symbol kernels)
 template <int LOG2M, int NA>

@@ -194,6 +194,7 @@ struct mimo_rx {
   bool cfo = false;                     // opt-in CFO estimate + derotation (batched path)
   int cur_sc16 = 0;                     // the batch being launched reads sc16 wire samples
   float cur_scale = 1.0f;
+  DevBuf<float2> spec;                  // 8x8 split decode: spectra scratch
   DevBuf<float2> wide;                  // sc16 batches the fused kernels do not take: widened
   DevBuf<float2> cfo_iq;                // derotated scratch capture
   DevBuf<double> cfo_eps;
@@ -258,7 +259,7 @@ struct mimo_rx {
   hipStream_t g_stream = nullptr;
   bool g_valid = false;
   hipGraphExec_t g_exec = nullptr;
-  std::array<const void *, 26> g_sig{};
+  std::array<const void *, 27> g_sig{};
 };
 
 struct mimo_tx {
@@ -591,6 +592,13 @@ int run_decode(mimo_rx *h, const float2 *iq, uint64_t stride, uint32_t F, uint64
   }
   hipEvent_t e = h->timer.begin(s);
   d.nrec = h->nrec.p;
+  static const bool no_split = [] { const char *e = getenv("RMIMO_DECODE_SPLIT"); return e && e[0] == '0'; }();
+  if (h->N == 8 && d.all_occ && h->det != 3 && max_out >= h->M / 64 && !no_split) {
+    // [F][M/64][max_out][N][64] complex64 spectra of the 8x8 split decode
+    if (h->spec.ensure((size_t)F * max_out * h->N * h->M) != hipSuccess)
+      return fail(MIMO_ERR_NOMEM, "split decode scratch");
+    d.spec = h->spec.p;
+  }
   bool per_frame = false;
   const uint32_t parts = launch_decode(d, h->log2M, F, s, &per_frame);
   h->timer.end(5, e, s);
@@ -1096,11 +1104,12 @@ static int run_batch(mimo_rx *h, const mimo_batch *b, hipStream_t s) {
 // the configuration and F (S&C items and hot items are pulled from device-side queues), so
 // the graph stays valid. Not used while stage timing or a diagnostic counter is on.
 // every device pointer a captured batch bakes into its kernels' arguments
-static std::array<const void *, 26> ws_signature(const mimo_rx *h) {
+static std::array<const void *, 27> ws_signature(const mimo_rx *h) {
   return {h->trig.p, h->keys.p, h->rec.p, h->info.p, h->G.p, h->W.p, h->gain.p, h->nvp.p,
           h->evm_part.p, h->evm_out.p, h->n_exact.p, h->queue.p, h->hot.p, h->lspart.p,
           h->tw, h->codes.codespec.p, h->scr_flag.p, h->scr_min.p, h->scr_max.p, h->nrec.p,
-          h->cand.p, h->certfail.p, h->lsq.p, h->cfo_iq.p, h->cfo_eps.p, h->wide.p};
+          h->cand.p, h->certfail.p, h->lsq.p, h->cfo_iq.p, h->cfo_eps.p, h->wide.p,
+          h->spec.p};
 }
 
 static bool same_batch(const mimo_batch &x, const mimo_batch &y) {

@@ -251,6 +251,7 @@ struct DecodeArgs {
   uint32_t n_cu;                   // compute units (persistent grid size)
   unsigned long long *prof;        // diagnostics: [items, load, fft, apply, reduce] cycles
   uint32_t *nrec;                  // [F] EVM records per frame (decode_stream_kernel) or null
+  float2 *spec;                    // split decode (8x8) spectra scratch [F][M/64][max_out][N][64]
   int expt;                        // diagnostics (RMIMO_DEC_EXPT): bit 0 IQ from one symbol,
                                    // bit 1 no output stores, bit 2 weights of subcarrier 0
 };
@@ -263,6 +264,9 @@ uint32_t launch_decode_stream(const DecodeArgs &a, int log2M, uint32_t n_frames,
 // true when launch_decode_stream takes this configuration (nrec aside): the sc16 wire input
 // is decoded only there
 bool decode_stream_accepts(const DecodeArgs &a, int log2M, uint32_t n_frames);
+// decode_stream.hip: 8x8 split form (spectra to a scratch, then a chunked apply); 0 when the
+// configuration is not handled or a.spec is null
+uint32_t launch_decode_split(const DecodeArgs &a, int log2M, uint32_t n_frames, hipStream_t s);
 constexpr uint32_t kMaxEvmParts = 16;
 
 struct EvmArgs {

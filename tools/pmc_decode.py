@@ -35,17 +35,19 @@ def main():
     ap.add_argument("--sample-format", default="fc32", choices=["fc32", "sc16"])
     ap.add_argument("-o", "--out", required=True)
     a = ap.parse_args()
-    f = per_dispatch(a.fetch_csv, "FETCH_SIZE", a.kernel)
-    w = per_dispatch(a.write_csv, "WRITE_SIZE", a.kernel)
-    fetch_b = 2.0 * statistics.median(f) * 1024.0
-    write_b = statistics.median(w) * 1024.0
+    # a stage of several kernels ("a|b"): the sum of each kernel's median per dispatch
+    ks = a.kernel.split("|")
+    f = [per_dispatch(a.fetch_csv, "FETCH_SIZE", k) for k in ks]
+    w = [per_dispatch(a.write_csv, "WRITE_SIZE", k) for k in ks]
+    fetch_b = 2.0 * sum(statistics.median(x) for x in f) * 1024.0
+    write_b = sum(statistics.median(x) for x in w) * 1024.0
     out = {
         "config": {"M": a.M, "streams": a.streams, "frames": a.frames, "pid": a.pid,
                    "ref_mode": a.ref_mode, "sample_format": a.sample_format},
         "kernel": a.kernel,
-        "dispatches": {"fetch": len(f), "write": len(w)},
-        "fetch_size_kib_median": statistics.median(f),
-        "write_size_kib_median": statistics.median(w),
+        "dispatches": {"fetch": [len(x) for x in f], "write": [len(x) for x in w]},
+        "fetch_size_kib_median": [statistics.median(x) for x in f],
+        "write_size_kib_median": [statistics.median(x) for x in w],
         "decode_hbm_read_bytes_per_launch": fetch_b,
         "decode_hbm_write_bytes_per_launch": write_b,
         "decode_hbm_bytes_per_launch": fetch_b + write_b,
