@@ -2,7 +2,7 @@
 
 Default workload C3 (BASELINE.json configs[2], the config the metric is quoted on): 2048-pt
 FFT, cp 152, 4x4, 20 access codes, 1000 data symbols, 64-QAM, synthetic flat Rayleigh channel
-at 30 dB SNR, 8 captures per step per GPU. --workload c2 / c4 / c5 run the other GPU configs.
+at 30 dB SNR, 32 captures per step per GPU. --workload c2 / c4 / c5 run the other GPU configs.
 
 One step = one pass of the whole receive chain (Schmidl-Cox + plateau, access-code search, LS
 estimate, detector weights, replay decode, demap, EVM) over a batch of synthetic captures
@@ -48,7 +48,7 @@ WORKLOADS = {
                desc="C2: 2x2 ZF (reference adjugate), 1024-pt FFT, cp 76, 16-QAM, 20 access "
                     "codes, 1000 data symbols/frame (synthetic stand-in for recorded USRP IQ)"),
     "c3": dict(M=2048, cp=152, streams=4, nac=20, pid=1000, qam=64, snr=30.0, detector="mmse",
-               frames=8, fps=1,
+               frames=32, fps=1,
                desc="C3: 4x4 MMSE, 2048-pt FFT, cp 152, 64-QAM, 20 access codes, "
                     "1000 data symbols/frame"),
     "c4": dict(M=4096, cp=304, streams=8, nac=20, pid=1000, qam=256, snr=35.0, detector="mmse",
