@@ -239,6 +239,9 @@ void search_ls_kernel(SearchArgs a) {
   }
   v2f w1[PL::NTW > 0 ? PL::NTW : 1];
   reg_twiddles<LOG2F, PTS>(w1, a.tw, tid);
+  // the LS transform's twiddles in LDS (no L2 round trip inside its passes)
+  float2 *twm = reinterpret_cast<float2 *>(lds_raw) + lds_padded_len(F);
+  fill_twiddles_lds<LOG2M, T>(twm, a.tw);
   if (tid == 0) { s_key[0] = 0ull; s_key[1] = 0ull; }
   reg_compute<LOG2F, PTS, 0, false>(v, w1);
   reg_rest<LOG2F, PTS, 1, false>(buf, v, w1, tid);
@@ -249,8 +252,10 @@ void search_ls_kernel(SearchArgs a) {
     const v2f *__restrict__ csp = reinterpret_cast<const v2f *>(a.codespec + (size_t)slot * F);
 #pragma unroll
     for (int e = 0; e < PTS; e++) v[e] = vmulc(X[e], csp[reg_index<LOG2F, PTS>(tid, e)]);
+#ifndef SL_ABL_NOINV   // timing ablation: no inverse transforms
     reg_compute<LOG2F, PTS, 0, true>(v, w1);
     reg_rest<LOG2F, PTS, 1, true>(buf, v, w1, tid);
+#endif
     const float vs = a.vscale[slot];
     const int off = (int)(u * a.SL);
     const uint32_t ws = a.SL * slot;                  // window index of lag 0
@@ -272,26 +277,45 @@ void search_ls_kernel(SearchArgs a) {
     }
     if ((tid & 63) == 0 && best) atomicMax(&s_key[u], best);
     __syncthreads();                                  // key final; every reader of buf is done
-    const unsigned long long key = s_key[u];
-    if (tid == 0) a.keys[((uint64_t)f * a.N + r) * a.n_slots + slot] = key;
-    if (slot == 0) continue;                          // S0: timing only
-    const uint32_t ac = slot - 1, code = ac / a.N, t = ac % a.N;
-    const int64_t w = I.base + (int64_t)key_index(key);
-    float2 *lb = reinterpret_cast<float2 *>(buf);
-    for (int i = tid; i < M; i += T) {
-      const int64_t n = w + i;
-      lb[lds_pad(i)] = (n >= 0 && n < L) ? xs.at(n) : make_float2(0.0f, 0.0f);
-    }
-    __syncthreads();
-    fft_lds<LOG2M, T, 1, false>(lb, a.tw);
-    const int8_t *sg = a.s1sign + ((size_t)t * a.nac + code) * M;
-    float2 *q = a.lsq + ((((uint64_t)f * a.N + r) * a.N + t) * a.nac + code) * M;
-    for (int k = tid; k < M; k += T) {
-      const float2 Xk = lb[lds_pad(k)];
-      const int s = sg[k];
-      q[k] = s > 0 ? Xk : (s < 0 ? cneg(Xk) : make_float2(0.0f, 0.0f));
-    }
-    __syncthreads();                                  // lb readers done before the next slot
+    if (tid == 0) a.keys[((uint64_t)f * a.N + r) * a.n_slots + slot] = s_key[u];
+  }
+#ifdef SL_ABL_NOLS   // timing ablation (tools/abl_search.sh): no LS term
+  return;
+#endif
+  // LS terms of the pair's access codes (slot 0 = S0 has none): both windows (at their final
+  // argmax) gathered with every load in flight, then one batched M-point transform
+  constexpr int PBM = lds_padded_len(M), NL = 2 * M / T;
+  static_assert(2 * M % T == 0, "whole windows per thread");
+  const bool valid0 = s0 != 0, valid1 = ns > 1;
+  if (!valid0 && !valid1) return;                     // uniform
+  const int64_t w0 = I.base + (int64_t)key_index(s_key[0]);
+  const int64_t w1v = I.base + (int64_t)key_index(s_key[1]);
+  float2 win[NL];
+#pragma unroll
+  for (int e = 0; e < NL; e++) {
+    const int i = tid + e * T, u = i / M, j = i % M;
+    const int64_t n = (u ? w1v : w0) + j;
+    const bool ok = (u ? valid1 : valid0) && n >= 0 && n < L;
+    win[e] = ok ? xs.at(n) : make_float2(0.0f, 0.0f);
+  }
+  float2 *lb = reinterpret_cast<float2 *>(buf);
+#pragma unroll
+  for (int e = 0; e < NL; e++) {
+    const int i = tid + e * T, u = i / M, j = i % M;
+    lb[u * PBM + lds_pad(j)] = win[e];
+  }
+  __syncthreads();
+  fft_lds_twl<LOG2M, T, 2, false>(lb, twm, tid);
+#pragma unroll
+  for (int e = 0; e < NL; e++) {
+    const int i = tid + e * T, u = i / M, k = i % M;
+    if (!(u ? valid1 : valid0)) continue;
+    const uint32_t ac = s0 + u - 1, code = ac / a.N, tx = ac % a.N;
+    const int8_t *sg = a.s1sign + ((size_t)tx * a.nac + code) * M;
+    float2 *q = a.lsq + ((((uint64_t)f * a.N + r) * a.N + tx) * a.nac + code) * M;
+    const float2 Xk = lb[u * PBM + lds_pad(k)];
+    const int s = sg[k];
+    q[k] = s > 0 ? Xk : (s < 0 ? cneg(Xk) : make_float2(0.0f, 0.0f));
   }
 }
 
@@ -823,7 +847,8 @@ static bool search_ls_try(const SearchArgs &a, int log2F, int log2M, uint32_t nf
       constexpr int LOG2M = LOG2F - D;
       if (log2F == LOG2F && log2M == LOG2M) {
         if (nf) {
-          const size_t shm = sizeof(float2) * lds_padded_len(1 << LOG2F);
+          // the segment image, then the LS transform's M/2 twiddles
+          const size_t shm = sizeof(float2) * (lds_padded_len(1 << LOG2F) + (1 << LOG2M) / 2);
           auto kern = a.sc16 ? search_ls_kernel<LOG2F, LOG2M, true>
                              : search_ls_kernel<LOG2F, LOG2M, false>;
           (void)hipFuncSetAttribute((const void *)kern,

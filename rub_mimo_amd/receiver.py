@@ -254,6 +254,11 @@ class Receiver:
         check(lib().mimo_rx_batch_W(self._h, W.ctypes.data, n), "batch_W")
         return W
 
+    def set_siso(self, tx, rx):
+        """framesync::set_siso_tx/rx: the stream pair the SISO detector decodes (a change
+        invalidates the captured batch graph, whose kernels carry the indices)."""
+        check(lib().mimo_rx_set_siso(self._h, tx, rx), "set_siso")
+
     def set_timing(self, on):
         check(lib().mimo_rx_set_timing(self._h, 1 if on else 0), "set_timing")
 

@@ -215,6 +215,38 @@ def test_batch_frames_are_independent():
     assert res[4]["status"] == _lib.FRAME_NO_SYNC
 
 
+def test_set_siso_after_graph_capture_decodes_the_new_pair():
+    """mimo_rx_set_siso between identical batch calls: the captured graph (whose decode
+    arguments carry the SISO indices) must not be replayed; the third call equals a receiver
+    created with the new pair."""
+    import torch
+    from rub_mimo_amd.receiver import Synthesizer, SynthParams
+    M, cp, N, nac, pid, F = 256, 19, 2, 4, 16, 2
+    sp = SynthParams(M=M, cp_len=cp, num_streams=N, num_access_codes=nac, pid=pid,
+                     qam_order=16, seed=9, snr_db=30.0)
+    syn = Synthesizer(sp)
+    L = sp.max_frame_len()
+    iq = torch.empty((F, N, L), dtype=torch.complex64, device="cuda")
+    syn.generate(iq, L, L, F, frame_id0=0)
+
+    def run(rx):
+        sym = torch.zeros((F, N, pid, M), dtype=torch.complex64, device="cuda")
+        rx.process(iq, L, L, F, max_out=pid, out_sym=sym, ref_mode=2, ref_seed=9)
+        torch.cuda.synchronize()
+        return sym.cpu(), [float(np.sum(r["evm_num"])) for r in rx.results()]
+
+    base = dict(M=M, cp_len=cp, num_streams=N, num_access_codes=nac, pid_max=pid,
+                detector=_lib.DET_SISO, qam_order=16)
+    rx = Receiver(RxParams(**base, siso_tx=0, siso_rx=0))
+    first = run(rx)
+    run(rx)                            # captured into a graph
+    rx.set_siso(1, 1)
+    got = run(rx)
+    want = run(Receiver(RxParams(**base, siso_tx=1, siso_rx=1)))
+    assert torch.equal(got[0], want[0]) and got[1] == want[1]
+    assert not torch.equal(got[0], first[0])
+
+
 def test_repeated_batch_graph_replay_is_identical():
     """A repeated process() call is captured into a HIP graph and replayed (engine.cpp); its
     results, symbols and indices must equal the direct launches bit for bit, and a changed

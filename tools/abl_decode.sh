@@ -20,7 +20,7 @@ for v in ${VARIANTS:-base nostore nodma nofft nostore_nodma nodemap}; do
   esac
   /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -I../../include $D $EXTRA \
     -c decode_stream.hip -o $OUT/ds_$v.o
-  objs=$(ls $OBJ/*.o | grep -v decode_stream.o)
+  objs=$(ls $OBJ/*.o | grep -v '/decode_stream.o$')
   /opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -o $OUT/$v.so $objs $OUT/ds_$v.o
 done
 ls -la $OUT/*.so
