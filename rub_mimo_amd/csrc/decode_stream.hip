@@ -193,6 +193,16 @@ MIMO_DEV uint32_t cvt_u32_sat(float x) {   // v_cvt_u32_f32: NaN and negatives -
   return r;
 }
 
+// the level pair of the hard decision (as qam_slice_pk below) packed as mI * L + mQ, the index
+// of the decision in the LDS table of Gray-coded symbol indices (one multiply-add instead of
+// the two Gray encodings and the combine)
+MIMO_DEV uint32_t qam_level_pair_pk(v2f y, v2f inv_scale, v2f Lf, uint32_t Lm1, uint32_t L) {
+#pragma clang fp contract(off)
+  const v2f t = (y * inv_scale + Lf) * 0.5f;
+  const uint32_t mI = min(cvt_u32_sat(t.x), Lm1), mQ = min(cvt_u32_sat(t.y), Lm1);
+  return mI * L + mQ;
+}
+
 // hard decision as qam_slice (decode_kernels.hip) / qam_demap (common.hpp): the level is
 // floor((y * inv_scale + L) * 0.5) clamped to [0, L-1] (NaN -> 0); truncation of the
 // non-negative value by v_cvt_u32_f32 with its saturation gives exactly that clamp
@@ -235,7 +245,7 @@ MIMO_DEV gptr<P> sgpr_ptr(P *p) {
   return (gptr<P>)(((uint64_t)hi << 32) | lo);
 }
 
-constexpr size_t kStreamStaticLds = 6144;   // pfx, fbody, fcr, ptab (+ slack)
+constexpr size_t kStreamStaticLds = 8192;   // pfx, fbody, fcr, ptab, gidx (+ slack)
 
 // dynamic LDS of the kernel: FFT images, staging, reference staging, twiddle table
 template <int LOG2M, int NA>
@@ -286,12 +296,16 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
   __shared__ uint32_t pfx[kStreamMaxFrames + 1];
   __shared__ int64_t fbody[kStreamMaxFrames];
   __shared__ uint32_t fcr[kStreamMaxFrames];     // capture | reference row << 16
-  __shared__ v2f ptab[kStreamMaxQam];                              // constellation by index
+  // constellation by symbol index, and the Gray-coded symbol index by level pair mI * L + mQ
+  __shared__ v2f ptab[kStreamMaxQam];
+  __shared__ uint8_t gidx[kStreamMaxQam];
   const int tid = threadIdx.x;
   const uint32_t wv = __builtin_amdgcn_readfirstlane((uint32_t)tid >> 6);
   for (uint32_t e = tid; e < a.qam.L * a.qam.L; e += T) {
     const float2 p = qam_point(e, a.qam);
     ptab[e] = v2f{p.x, p.y};
+    const uint32_t mI = e / a.qam.L, mQ = e % a.qam.L;
+    gidx[e] = (uint8_t)((gray_enc(mI) << a.qam.b) | gray_enc(mQ));
   }
 
   // twiddles of passes 1..NP-1: twl[off(p) + (r-1) NS + jm] = e^{-2 pi i jm r / (NS R)}
@@ -639,7 +653,7 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
           continue;
         }
 #endif
-        const uint32_t d = qam_slice_pk(acc, inv_sc, Lf, Lm1, a.qam.b);
+        const uint32_t d = gidx[qam_level_pair_pk(acc, inv_sc, Lf, Lm1, a.qam.L)];
         uint32_t refi;
         if constexpr (REF == 1) refi = (cref[(t * S + q) / 4] >> (8 * ((t * S + q) % 4))) & 0xFFu;
         else if constexpr (REF == 2)
