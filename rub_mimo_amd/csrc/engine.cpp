@@ -376,8 +376,8 @@ int run_sync(mimo_rx *h, const float2 *iq, uint64_t stride, uint32_t F, uint64_t
       HIPCHK(hipMemsetAsync(h->n_exact.p, 0, sizeof(unsigned long long), s));
     }
     a.n_exact = h->n_exact.p;
-    if (!h->queue.p) HIPCHK(h->queue.ensure(2));
-    add_fill(h->queue.p, 2 * sizeof(uint32_t), 0u);
+    if (!h->queue.p) HIPCHK(h->queue.ensure(3));
+    add_fill(h->queue.p, 3 * sizeof(uint32_t), 0u);
     a.queue = h->queue.p;
     a.hot_count = h->queue.p + 1;
     // screened path (default when the geometry allows it; RMIMO_SC_LEGACY=1 selects the
@@ -423,10 +423,31 @@ int run_sync(mimo_rx *h, const float2 *iq, uint64_t stride, uint32_t F, uint64_t
       sa.chunk_len = K; sa.chunk_lo = chunk_lo; sa.nchunks = nchunks;
       sa.flag = h->scr_flag.p; sa.fmin = h->scr_min.p; sa.fmax = h->scr_max.p;
       sa.count = a.hot_count; sa.hot = a.hot; sa.cap = a.hot_cap;
-      launch_sc_screen(sa, F, s);
       if (a.diag & 32) a.diag |= 16;   // diagnostics: finalize as a separate kernel
+      // Two phases for one frame per capture: the first eighth of every capture's chunks (a
+      // frame's S0 plateau sits near its capture's start), then the rest only for captures with
+      // no trigger yet. A trigger found in phase 1 is the capture's first (every earlier chunk
+      // was evaluated) and phase 2 evaluates exactly the chunks one pass would have for the
+      // others, so results are those of one pass; the screen's reads of antenna 0 past the
+      // trigger of a synced capture are skipped. RMIMO_SC_PHASES=1: one pass.
+      static const bool one_phase = [] { const char *e = getenv("RMIMO_SC_PHASES"); return e && e[0] == '1'; }();
+      const uint64_t c1 = (!stream && chunk_lo == 0 && !one_phase && nchunks >= 16)
+                              ? std::max<uint64_t>(2, nchunks / 8) : nchunks;
+      sa.chunk_hi = c1;
+      launch_sc_screen(sa, F, s);
       launch_sc_exact(a, s);   // resolves and finalises its items itself
       if (a.diag & 32) launch_sc_finalize(a, s);
+      if (c1 < nchunks) {
+        launch_sc_snapshot(h->queue.p + 2, a.hot_count, s);   // phase-1 items: done
+        sa.chunk_lo = c1;
+        sa.chunk_hi = nchunks;
+        sa.trig = h->trig.p;
+        launch_sc_screen(sa, F, s);
+        ScArgs a2 = a;
+        a2.item_lo = h->queue.p + 2;
+        launch_sc_exact(a2, s);
+        if (a.diag & 32) launch_sc_finalize(a2, s);
+      }
     } else {
       launch_sc(a, F, h->n_cu, s);
       launch_sc_hot(a, s);

@@ -55,6 +55,7 @@ struct ScArgs {
   unsigned long long *n_exact;  // count of exact fp32 recomputes (null: not counted)
   uint32_t *queue;          // [0] work-queue head, [1] hot-item count; zeroed before launch
   uint32_t *hot_count;
+  const uint32_t *item_lo;  // screened path: first hot item of this exact launch, or null (0)
   ScHot *hot;               // [hot_cap] (null: resolve inside the item kernel)
   uint32_t hot_cap;
   unsigned long long *prof; // diagnostics: [items, antenna passes, row, words, resolve, total
@@ -84,6 +85,8 @@ struct ScreenArgs {
   uint32_t N, M;
   double thr_screen;                       // thr - 0.01
   uint64_t chunk_len, chunk_lo, nchunks;
+  uint64_t chunk_hi;                       // screen chunks [chunk_lo, chunk_hi) (0: nchunks)
+  const unsigned long long *trig;          // [F] skip frames already triggered, or null
   uint32_t *flag;                          // [F][nchunks] chunk listed
   unsigned long long *fmin, *fmax;         // [F][nchunks] first / last unproven position
   uint32_t *count;                         // listed chunks (= hot items)
@@ -102,6 +105,8 @@ struct FillArgs {
 void launch_fill(const FillArgs &a, hipStream_t s);
 // true when the geometry allows the screen (M/2 a multiple of kScrB, M <= 8192)
 inline bool sc_screen_ok(uint32_t M) { return M / 2 >= (uint32_t)kScrB && (M / 2) % kScrB == 0 && M / 2 / kScrB <= (uint32_t)kScrMaxD; }
+// copies one device word (the hot-item count after a screen phase)
+void launch_sc_snapshot(uint32_t *dst, const uint32_t *src, hipStream_t s);
 void launch_sc_screen(const ScreenArgs &a, uint32_t n_frames, hipStream_t s);
 void launch_sc_exact(const ScArgs &a, hipStream_t s);
 // persistent grid of n_cu x (resident blocks per CU) over the F x chunks items

@@ -1386,7 +1386,11 @@ __global__ __launch_bounds__(kScrT) __attribute__((amdgpu_waves_per_eu(6))) void
   const uint32_t f = blockIdx.y;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int D = (int)(a.M / 2) / B, RL = (int)a.M / 2;
-  const int64_t L = (int64_t)a.frame_len;
+  if (a.trig && a.trig[f] != ~0ull) return;           // triggered in an earlier phase
+  const int64_t L = a.chunk_hi ? std::min<int64_t>((int64_t)a.frame_len,
+                                                   (int64_t)(a.chunk_hi * a.chunk_len))
+                               : (int64_t)a.frame_len;   // end of this phase's positions
+  const int64_t LF = (int64_t)a.frame_len;
   const int64_t q0 = (int64_t)a.chunk_lo * (int64_t)a.chunk_len + (int64_t)blockIdx.x * kScrSpan;
   if (q0 >= L) return;
   const int NB = kScrSpan / B + 2 * D;
@@ -1399,7 +1403,7 @@ __global__ __launch_bounds__(kScrT) __attribute__((amdgpu_waves_per_eu(6))) void
   for (int j0 = wv * kScrBPI; j0 < NB; j0 += (kScrT / 64) * kScrBPI) {
     float4 cur[kScrBPI], del[kScrBPI];
     const int64_t nb = h0 + (int64_t)j0 * B;
-    if (vec && nb - RL >= 0 && nb + (int64_t)kScrBPI * B <= L && j0 + kScrBPI <= NB) {
+    if (vec && nb - RL >= 0 && nb + (int64_t)kScrBPI * B <= LF && j0 + kScrBPI <= NB) {
 #pragma unroll
       for (int b = 0; b < kScrBPI; b++) {
         cur[b] = x.pair(nb + 2 * lane + (int64_t)b * B);
@@ -1409,8 +1413,8 @@ __global__ __launch_bounds__(kScrT) __attribute__((amdgpu_waves_per_eu(6))) void
 #pragma unroll
       for (int b = 0; b < kScrBPI; b++) {
         const int64_t n = nb + (int64_t)b * B + 2 * lane;
-        cur[b] = ld_pair(x, n, L, vec);
-        del[b] = ld_pair(x, n - RL, L, vec);
+        cur[b] = ld_pair(x, n, LF, vec);
+        del[b] = ld_pair(x, n - RL, LF, vec);
       }
     }
     // per-lane partials v[4 b + c] (c: Re P, Im P, |x|^2, |Re p| + |Im p|), then a transposing
@@ -1521,9 +1525,10 @@ void sc_exact_kernel(ScArgs a) {
   __shared__ long long flo[kMaxStreams];
   __shared__ unsigned long long s_min;
   const uint32_t count = min(*a.hot_count, a.hot_cap);
+  const uint32_t item0 = a.item_lo ? *a.item_lo : 0u;   // items of earlier screen phases: done
   const uint32_t s = blockIdx.x;   // antenna fastest: an item's passes are dispatched together,
                                    // ahead of the grid's empty tail
-  for (uint32_t slot = blockIdx.y; slot < count; slot += gridDim.y) {
+  for (uint32_t slot = item0 + blockIdx.y; slot < count; slot += gridDim.y) {
   ScHot *hp = a.hot + slot;
   const int tid = threadIdx.x;
   if (tid == 0) s_namb = 0;
@@ -1898,8 +1903,16 @@ void launch_fill(const FillArgs &a, hipStream_t s) {
   hipLaunchKernelGGL(fill_kernel, dim3(grid), dim3(256), 0, s, a);
 }
 
+__global__ void sc_snapshot_kernel(uint32_t *dst, const uint32_t *src) { *dst = *src; }
+
+void launch_sc_snapshot(uint32_t *dst, const uint32_t *src, hipStream_t s) {
+  hipLaunchKernelGGL(sc_snapshot_kernel, dim3(1), dim3(1), 0, s, dst, src);
+}
+
 void launch_sc_screen(const ScreenArgs &a, uint32_t n_frames, hipStream_t s) {
-  const uint64_t span = (uint64_t)a.frame_len - std::min<uint64_t>(a.frame_len, a.chunk_lo * a.chunk_len);
+  const uint64_t end = a.chunk_hi ? std::min<uint64_t>(a.frame_len, a.chunk_hi * a.chunk_len)
+                                  : (uint64_t)a.frame_len;
+  const uint64_t span = end - std::min<uint64_t>(end, a.chunk_lo * a.chunk_len);
   const uint32_t gx = (uint32_t)((span + kScrSpan - 1) / kScrSpan);
   if (!gx) return;
   if (a.sc16)

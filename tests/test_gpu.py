@@ -379,6 +379,12 @@ def test_c2_2x2_zf_1024_16qam():
     assert np.all(e < -15)
 
 
+def test_c2_2x2_zf_1024_16qam_full_frame():
+    """BASELINE config C2 at full size (PID 1000, the streaming decode's 2x2 form)."""
+    d, e = _c_frame_parity(1024, 76, 2, 20, 1000, 16, _lib.DET_ZF2, 25.0, seed=22)
+    assert np.all(e < -15)
+
+
 def test_c3_4x4_mmse_2048_64qam_full_frame():
     """BASELINE config C3 at full size (PID 1000): the oracle needs ~20 s of CPU."""
     d, e = _c_frame_parity(2048, 152, 4, 20, 1000, 64, _lib.DET_MMSE, 30.0, seed=31)
