@@ -270,7 +270,13 @@ constexpr bool stream_wave_fft() {
   return LOG2M >= 11 && stream_dyn_lds<LOG2M, NA>(true, REF, SC16) + kStreamStaticLds <= 163840;
 }
 
-template <int LOG2M, int NA, int REF, int OUTS, bool SC16 = false>
+// CPE (opt-in CFO path): decision-directed common-phase tracking. The residual frequency
+// offset left by the CFO estimate turns every symbol by a slowly growing angle; each symbol's
+// equalised outputs are rotated by the current estimate before the decision, and the sum of
+// conj(decided point) x rotated output over the symbol (all streams and subcarriers, reduced
+// through LDS at the next symbol's top barrier) corrects the estimate for the next symbol of
+// the same frame. Off (CPE = false) the kernel is unchanged.
+template <int LOG2M, int NA, int REF, int OUTS, bool SC16 = false, bool CPE = false>
 __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(DecodeArgs a) {
   using PL = StreamPlan<LOG2M, NA>;
   constexpr int M = PL::M, T = PL::T, S = PL::S, PB = PL::PB, W8 = M / 8;
@@ -299,6 +305,7 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
   // constellation by symbol index, and the Gray-coded symbol index by level pair mI * L + mQ
   __shared__ v2f ptab[kStreamMaxQam];
   __shared__ uint8_t gidx[kStreamMaxQam];
+  __shared__ v2f cpe_part[CPE ? T / 64 : 1];                       // per-wave phase sums
   const int tid = threadIdx.x;
   const uint32_t wv = __builtin_amdgcn_readfirstlane((uint32_t)tid >> 6);
   for (uint32_t e = tid; e < a.qam.L * a.qam.L; e += T) {
@@ -509,6 +516,8 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
     }
   };
 
+  v2f rot = v2f{1.0f, 0.0f};                          // CPE: current phase correction
+  bool cpe_valid = false;                             // cpe_part holds this frame's last symbol
   load_w(f);
   uint32_t odd = fetch(f, s);
   // the first symbol's staging (issued after the weight loads: the counted wait in the loop
@@ -520,6 +529,19 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
     MARK(";@@A top");
     asm volatile("s_waitcnt vmcnt(%0)" :: "n"(NSTORE) : "memory");
     __syncthreads();
+    if constexpr (CPE) {
+      if (cpe_valid) {   // the previous symbol's residual phase: rot *= conj(c) / |c|
+        v2f c = v2f{0.0f, 0.0f};
+#pragma unroll
+        for (int w = 0; w < T / 64; w++) c += cpe_part[w];
+        const float m2 = c.x * c.x + c.y * c.y;
+        if (m2 > 0.0f) {
+          const float inv = 1.0f / sqrtf(m2);
+          const v2f u = v2f{c.x * inv, -c.y * inv};
+          rot = v2f{rot.x * u.x - rot.y * u.y, rot.x * u.y + rot.y * u.x};
+        }
+      }
+    }
     v2f v[8];
     {
       const int t0 = opq(tid);
@@ -620,6 +642,7 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
     const uint64_t frame_id = a.frame_id0 + (fcr[f] >> 16);
     // output row (f, t, s) = ob0 + t * max_out * M_occ: uniform, one 64-bit product per symbol
     const uint64_t ob0 = rfl64((((uint64_t)f * NA) * a.max_out + s) * a.M_occ);
+    v2f cpe_acc = v2f{0.0f, 0.0f};
 #pragma unroll
     for (int q = 0; q < S; q++) {
       const uint32_t k = (uint32_t)opq(tid) + q * T;
@@ -653,7 +676,9 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
           continue;
         }
 #endif
+        if constexpr (CPE) acc = cmul_pk(acc, rot);
         const uint32_t d = gidx[qam_level_pair_pk(acc, inv_sc, Lf, Lm1, a.qam.L)];
+        if constexpr (CPE) cpe_acc = cmac_pk(cpe_acc, v2f{ptab[d].x, -ptab[d].y}, acc);
         uint32_t refi;
         if constexpr (REF == 1) refi = (cref[(t * S + q) / 4] >> (8 * ((t * S + q) % 4))) & 0xFFu;
         else if constexpr (REF == 2)
@@ -674,9 +699,22 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
       }
     }
 
+    if constexpr (CPE) {   // this symbol's residual phase sum, per wave, read after the next barrier
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) {
+        cpe_acc.x += __shfl_xor(cpe_acc.x, off);
+        cpe_acc.y += __shfl_xor(cpe_acc.y, off);
+      }
+      if ((tid & 63) == 0) cpe_part[wv] = cpe_acc;
+      cpe_valid = true;
+    }
     MARK(";@@F tail");
     const bool last = (i + 1 == i_end);
     if (last || fn != f) {
+      if constexpr (CPE) {
+        rot = v2f{1.0f, 0.0f};
+        cpe_valid = false;
+      }
       flush(f);
       if (!last) {
         n_out_f = n_out_n;
@@ -908,6 +946,11 @@ static uint32_t stream_launch(const DecodeArgs &a, hipStream_t s) {
   auto pick_out = [&](auto ref) -> void (*)(DecodeArgs) {
     constexpr int R = decltype(ref)::value;
     const int outs = (a.out_sym ? 1 : 0) | (a.out_idx ? 2 : 0);
+    if (a.cpe && !a.sc16 && R == 1 && (outs == 3 || outs == 0)) {   // opt-in CFO path
+      if constexpr (R == 1)
+        return outs == 3 ? decode_stream_kernel<LOG2M, NA, 1, 3, false, true>
+                         : decode_stream_kernel<LOG2M, NA, 1, 0, false, true>;
+    }
     if (a.sc16) {   // sc16 wire input: every output, EVM against HBM indices or decisions
       if constexpr (R == 2) return nullptr;
       else return outs == 3 ? decode_stream_kernel<LOG2M, NA, R, 3, true> : nullptr;

@@ -613,6 +613,7 @@ int run_decode(mimo_rx *h, const float2 *iq, uint64_t stride, uint32_t F, uint64
   }
   hipEvent_t e = h->timer.begin(s);
   d.nrec = h->nrec.p;
+  d.cpe = h->cfo ? 1 : 0;
   static const bool no_split = [] { const char *e = getenv("RMIMO_DECODE_SPLIT"); return e && e[0] == '0'; }();
   if (h->N == 8 && d.all_occ && h->det != 3 && max_out >= h->M / 64 && !no_split) {
     // [F][M/64][max_out][N][64] complex64 spectra of the 8x8 split decode

@@ -257,6 +257,7 @@ struct DecodeArgs {
   unsigned long long *prof;        // diagnostics: [items, load, fft, apply, reduce] cycles
   uint32_t *nrec;                  // [F] EVM records per frame (decode_stream_kernel) or null
   float2 *spec;                    // split decode (8x8) spectra scratch [F][M/64][max_out][N][64]
+  int cpe;                         // opt-in CFO: decision-directed common-phase tracking
   int expt;                        // diagnostics (RMIMO_DEC_EXPT): bit 0 IQ from one symbol,
                                    // bit 1 no output stores, bit 2 weights of subcarrier 0
 };

@@ -572,9 +572,11 @@ def test_cfo_batch_corrects_rotated_c3_frames(eps_true):
       fine) is within 2e-5 of eps_true;
     - decode with EVM within 0.1 dB of the unrotated frames through the same receiver (the
       correction is invariant to the offset);
-    - against the unrotated frames with no correction at all (the reference's path) the cost is
-      the estimator's own variance (prefix correlation, std ~3e-6 subcarrier spacings at 30 dB):
-      within 0.2 dB for frames at EVM >= -30 dB, within 3 dB for the cleanest frames;
+    - against the unrotated frames with no correction at all (the reference's path) within
+      0.5 dB for every frame: the estimator's own variance (prefix correlation, std ~3e-6
+      subcarrier spacings at 30 dB) would cost the cleanest (-32 dB) frames ~2.4 dB of drift
+      over 1000 symbols; the decode's decision-directed common-phase tracking takes that to
+      ~0.3 dB (the first symbol of each decode workgroup's range is not yet tracked);
     - without the correction the rotated frames collapse (> 10 dB worse)."""
     import torch
     from rub_mimo_amd.receiver import cfo_derotate
@@ -614,7 +616,8 @@ def test_cfo_batch_corrects_rotated_c3_frames(eps_true):
         assert abs(corr[f]["cfo_eps"] - eps_true) < 2e-5, (f, corr[f]["cfo_eps"])
         assert abs(clean[f]["cfo_eps"]) < 2e-5, (f, clean[f]["cfo_eps"])
         assert abs(e1 - e3) <= 0.1, (f, e3, e1)
-        assert e3 - e0 <= (0.2 if e0 >= -30.0 else 3.0), (f, e0, e3)
+        assert e3 - e0 <= 0.5, (f, e0, e3)
+        print("cfo frame %d: plain %.3f dB, corrected %.3f dB, raw %.3f dB" % (f, e0, e3, e2))
         assert e2 > e0 + 10.0, (f, e0, e2)
 
 
