@@ -237,6 +237,7 @@ MIMO_DEV uint64_t rfl64(uint64_t v) {   // a uniform 64-bit value, held in SGPRs
 
 template <typename P>
 using gptr = __attribute__((address_space(1))) P *;
+typedef float v4f __attribute__((ext_vector_type(4)));
 template <typename P>
 MIMO_DEV gptr<P> sgpr_ptr(P *p) {
   const uint64_t v = (uint64_t)p;
@@ -289,10 +290,14 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
   constexpr int NWI = (NA * NBLK + T / 64 - 1) / (T / 64);   // ... per wave and symbol
   constexpr int NREF = NA * M / 16;               // 16-byte chunks of the reference indices
   // store instructions per symbol: the wait at the top of a symbol leaves them in flight
-  constexpr int NSTORE = ((OUTS & 1) ? NA * S : 0) + ((OUTS & 2) ? NA * S : 0);
   using WP = WavePlan<LOG2M, NA>;
   constexpr bool WF = stream_wave_fft<LOG2M, NA, REF, SC16>();
   constexpr int MS = WP::MS, LG = WP::LG, QS = WP::QS, GS = WP::GS;
+  // subcarriers of a thread in the apply: k = S tid + q (adjacent: one S*8-byte symbol store and
+  // one S-byte index store per stream) on the wave-FFT layout, else k = tid + q T
+  constexpr bool KADJ = WF && S == 2 && !CPE;
+  constexpr int SPS = KADJ ? NA : NA * S;          // store instructions per output kind
+  constexpr int NSTORE = ((OUTS & 1) ? SPS : 0) + ((OUTS & 2) ? SPS : 0);
   extern __shared__ __attribute__((aligned(16))) float2 lds_raw[];
   v2f *img = reinterpret_cast<v2f *>(lds_raw);    // [NA][PB] FFT exchange ([NA][8][QS] if WF)
   v2f *stg = img + NA * (WF ? GS : PB);                            // [NA][RS] next symbol
@@ -465,17 +470,19 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
   v2f Wr[NA][NA][S];
   auto load_w = [&](uint32_t ff) {
     const int t0 = opq(tid);
-    const v2f *Wf = reinterpret_cast<const v2f *>(a.W) + (uint64_t)ff * NA * NA * M + t0;
-    const float *gf = a.gain + (uint64_t)ff * M + t0;
+    const uint32_t k0 = KADJ ? (uint32_t)t0 * S : (uint32_t)t0;
+    constexpr uint32_t KQ = KADJ ? 1 : T;                 // k of slot q = k0 + q KQ
+    const v2f *Wf = reinterpret_cast<const v2f *>(a.W) + (uint64_t)ff * NA * NA * M + k0;
+    const float *gf = a.gain + (uint64_t)ff * M + k0;
     float gs[S];
 #pragma unroll
-    for (int q = 0; q < S; q++) gs[q] = gf[q * T] * a.dn;
+    for (int q = 0; q < S; q++) gs[q] = gf[q * KQ] * a.dn;
 #pragma unroll
     for (int t = 0; t < NA; t++)
 #pragma unroll
       for (int r = 0; r < NA; r++)
 #pragma unroll
-        for (int q = 0; q < S; q++) Wr[t][r][q] = Wf[(t * NA + r) * M + q * T] * gs[q];
+        for (int q = 0; q < S; q++) Wr[t][r][q] = Wf[(t * NA + r) * M + q * KQ] * gs[q];
   };
 
   // EVM sums: per-thread fp32 error and reference energies, per-wave symbol-error counts
@@ -564,13 +571,21 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
       const int t0 = opq(tid);
 #pragma unroll
       for (int w = 0; w < (NA * S + 3) / 4; w++) cref[w] = 0;
+      if constexpr (KADJ) {   // the thread's S = 2 bytes of stream t are adjacent
 #pragma unroll
-      for (int t = 0; t < NA; t++)
-#pragma unroll
-        for (int q = 0; q < S; q++) {
-          const int e = t * S + q;
-          cref[e / 4] |= (uint32_t)rstg[t * M + t0 + q * T] << (8 * (e % 4));
+        for (int t = 0; t < NA; t++) {
+          const int e = t * S;
+          cref[e / 4] |= (uint32_t)reinterpret_cast<const uint16_t *>(rstg + t * M)[t0] << (8 * (e % 4));
         }
+      } else {
+#pragma unroll
+        for (int t = 0; t < NA; t++)
+#pragma unroll
+          for (int q = 0; q < S; q++) {
+            const int e = t * S + q;
+            cref[e / 4] |= (uint32_t)rstg[t * M + t0 + q * T] << (8 * (e % 4));
+          }
+      }
     }
     MARK(";@@B pass0");
     dft_fwd_pk<8>(v);
@@ -638,64 +653,92 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
     }
 
     MARK(";@@E apply");
-    // apply, demap, EVM, stores: subcarrier k = tid + q T of every stream
+    // apply, demap, EVM, stores: subcarriers k = tid + q T (KADJ: S tid + q) of every stream
     const uint64_t frame_id = a.frame_id0 + (fcr[f] >> 16);
     // output row (f, t, s) = ob0 + t * max_out * M_occ: uniform, one 64-bit product per symbol
     const uint64_t ob0 = rfl64((((uint64_t)f * NA) * a.max_out + s) * a.M_occ);
     v2f cpe_acc = v2f{0.0f, 0.0f};
+    // one output (stream t, slot q, subcarrier k): apply, demap, EVM terms; returns the decision
+    auto one_out = [&](int t, int q, uint32_t k, const v2f *X, v2f &acc) -> uint32_t {
+      acc = v2f{0.0f, 0.0f};
 #pragma unroll
-    for (int q = 0; q < S; q++) {
-      const uint32_t k = (uint32_t)opq(tid) + q * T;
-      v2f X[NA];
-      if constexpr (WF) {
-        const uint32_t kk = (uint32_t)opq(tid) + q * T;
+      for (int r = 0; r < NA; r++) acc = cmac_pk(acc, Wr[t][r][q], X[r]);
+#ifdef DS_ABL_NODEMAP   // timing ablation: no demap / EVM
+      return 0u;
+#endif
+      if constexpr (CPE) acc = cmul_pk(acc, rot);
+      const uint32_t d = gidx[qam_level_pair_pk(acc, inv_sc, Lf, Lm1, a.qam.L)];
+      if constexpr (CPE) cpe_acc = cmac_pk(cpe_acc, v2f{ptab[d].x, -ptab[d].y}, acc);
+      uint32_t refi;
+      if constexpr (REF == 1) refi = (cref[(t * S + q) / 4] >> (8 * ((t * S + q) % 4))) & 0xFFu;
+      else if constexpr (REF == 2)
+        refi = (uint32_t)(hash5(a.ref_seed, DOM_DATA, frame_id, t, (uint64_t)s * a.M_occ + k) &
+                          (uint64_t)(a.qam.L * a.qam.L - 1));
+      else refi = d;
+      // the reference point (the transmitted one: a decision error costs its distance)
+      n_err[t] += (uint32_t)__builtin_popcountll(__builtin_amdgcn_ballot_w64(refi != d));
+      const v2f sp = ptab[refi];
+      const v2f er = acc - sp;
+      e_num[t] = __builtin_fmaf(er.x, er.x, __builtin_fmaf(er.y, er.y, e_num[t]));
+      e_den[t] = __builtin_fmaf(sp.x, sp.x, __builtin_fmaf(sp.y, sp.y, e_den[t]));
+      return d;
+    };
+    if constexpr (KADJ) {
+      // the thread's S adjacent subcarriers k = S tid + q: every antenna's X of both, then per
+      // stream both outputs and one 16-byte symbol store and one 2-byte index store (per stream
+      // the EVM terms accumulate in the same q order as the strided form)
+      v2f X[S][NA];
+#pragma unroll
+      for (int q = 0; q < S; q++) {
+        const uint32_t kk = (uint32_t)opq(tid) * S + q;
         const v2f *xp = img + (kk & 7u) * QS + lds_pad((int)(kk >> 3));
 #pragma unroll
-        for (int r = 0; r < NA; r++) X[r] = xp[r * GS];
-      } else {
-        const v2f *xp = img + lds_pad((int)(uint32_t)opq(tid)) + q * (T + T / 32);
-#pragma unroll
-        for (int r = 0; r < NA; r++) X[r] = xp[r * PB];
+        for (int r = 0; r < NA; r++) X[q][r] = xp[r * GS];
       }
 #pragma unroll
       for (int t = 0; t < NA; t++) {
-        // uniform row bases (SGPRs): the stores take a 32-bit per-lane offset
         const uint64_t ob = ob0 + (uint64_t)t * rowstep;
         const auto osym = sgpr_ptr(reinterpret_cast<v2f *>(a.out_sym + ob));
         const auto oidx = sgpr_ptr(a.out_idx + ob);
-        v2f acc = v2f{0.0f, 0.0f};
-#pragma unroll
-        for (int r = 0; r < NA; r++) acc = cmac_pk(acc, Wr[t][r][q], X[r]);
-#ifdef DS_ABL_NODEMAP   // timing ablation: no demap / EVM
-        {
-#ifndef DS_ABL_NOSTORE
-          if constexpr (OUTS & 1)
-            *(gptr<v2f>)((gptr<char>)osym + k * (uint32_t)sizeof(v2f)) = acc;
-          if constexpr (OUTS & 2) oidx[k] = (uint8_t)0;
-#endif
-          continue;
-        }
-#endif
-        if constexpr (CPE) acc = cmul_pk(acc, rot);
-        const uint32_t d = gidx[qam_level_pair_pk(acc, inv_sc, Lf, Lm1, a.qam.L)];
-        if constexpr (CPE) cpe_acc = cmac_pk(cpe_acc, v2f{ptab[d].x, -ptab[d].y}, acc);
-        uint32_t refi;
-        if constexpr (REF == 1) refi = (cref[(t * S + q) / 4] >> (8 * ((t * S + q) % 4))) & 0xFFu;
-        else if constexpr (REF == 2)
-          refi = (uint32_t)(hash5(a.ref_seed, DOM_DATA, frame_id, t, (uint64_t)s * a.M_occ + k) &
-                            (uint64_t)(a.qam.L * a.qam.L - 1));
-        else refi = d;
-        // the reference point (the transmitted one: a decision error costs its distance)
-        n_err[t] += (uint32_t)__builtin_popcountll(__builtin_amdgcn_ballot_w64(refi != d));
-        const v2f sp = ptab[refi];
-        const v2f er = acc - sp;
-        e_num[t] = __builtin_fmaf(er.x, er.x, __builtin_fmaf(er.y, er.y, e_num[t]));
-        e_den[t] = __builtin_fmaf(sp.x, sp.x, __builtin_fmaf(sp.y, sp.y, e_den[t]));
+        const uint32_t kb = (uint32_t)opq(tid) * S;
+        v2f y0, y1;
+        const uint32_t d0 = one_out(t, 0, kb, X[0], y0);
+        const uint32_t d1 = one_out(t, 1, kb + 1, X[1], y1);
 #ifndef DS_ABL_NOSTORE   // timing ablation: no symbol / index stores
         if constexpr (OUTS & 1)
-          *(gptr<v2f>)((gptr<char>)osym + k * (uint32_t)sizeof(v2f)) = acc;
-        if constexpr (OUTS & 2) oidx[k] = (uint8_t)d;
+          *(gptr<v4f>)((gptr<char>)osym + kb * (uint32_t)sizeof(v2f)) = v4f{y0.x, y0.y, y1.x, y1.y};
+        if constexpr (OUTS & 2) *(gptr<uint16_t>)((gptr<char>)oidx + kb) = (uint16_t)(d0 | (d1 << 8));
 #endif
+      }
+    } else {
+#pragma unroll
+      for (int q = 0; q < S; q++) {
+        const uint32_t k = (uint32_t)opq(tid) + q * T;
+        v2f X[NA];
+        if constexpr (WF) {
+          const uint32_t kk = (uint32_t)opq(tid) + q * T;
+          const v2f *xp = img + (kk & 7u) * QS + lds_pad((int)(kk >> 3));
+#pragma unroll
+          for (int r = 0; r < NA; r++) X[r] = xp[r * GS];
+        } else {
+          const v2f *xp = img + lds_pad((int)(uint32_t)opq(tid)) + q * (T + T / 32);
+#pragma unroll
+          for (int r = 0; r < NA; r++) X[r] = xp[r * PB];
+        }
+#pragma unroll
+        for (int t = 0; t < NA; t++) {
+          // uniform row bases (SGPRs): the stores take a 32-bit per-lane offset
+          const uint64_t ob = ob0 + (uint64_t)t * rowstep;
+          const auto osym = sgpr_ptr(reinterpret_cast<v2f *>(a.out_sym + ob));
+          const auto oidx = sgpr_ptr(a.out_idx + ob);
+          v2f acc;
+          const uint32_t d = one_out(t, q, k, X, acc);
+#ifndef DS_ABL_NOSTORE   // timing ablation: no symbol / index stores
+          if constexpr (OUTS & 1)
+            *(gptr<v2f>)((gptr<char>)osym + k * (uint32_t)sizeof(v2f)) = acc;
+          if constexpr (OUTS & 2) oidx[k] = (uint8_t)d;
+#endif
+        }
       }
     }
 

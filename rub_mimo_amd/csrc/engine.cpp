@@ -536,6 +536,8 @@ int run_estimate(mimo_rx *h, const float2 *iq, uint64_t stride, uint32_t F, uint
     // search of slot pairs with the LS terms fused in, then the fixed-order LS combine
     HIPCHK(h->lsq.ensure((size_t)F * h->N * h->N * h->nac * h->M));
     sa.s1sign = h->s1sign.p; sa.lsq = h->lsq.p; sa.nac = h->nac;
+    static const bool xcd = [] { const char *e = getenv("RMIMO_SEARCH_XCD"); return !(e && e[0] == '0'); }();
+    sa.xcd_order = xcd ? 1u : 0u;
     la.lsq = h->lsq.p;
     hipEvent_t e = h->timer.begin(s);
     launch_search_ls(sa, h->log2F, h->log2M, F, s);

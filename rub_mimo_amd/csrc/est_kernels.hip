@@ -212,18 +212,36 @@ void search_ls_kernel(SearchArgs a) {
   extern __shared__ __attribute__((aligned(16))) float2 lds_raw[];
   v2f *buf = reinterpret_cast<v2f *>(lds_raw);
   __shared__ unsigned long long s_key[2];
-  const uint32_t f = blockIdx.y;
+  // (frame, rx, pair) of this workgroup. xcd_order: workgroups are dispatched round-robin over
+  // the 8 XCDs (hardware id b -> XCD b mod 8); each XCD is given a contiguous range of the
+  // order (pair, frame, rx), so the workgroups resident on one XCD at a time share the two
+  // 64 KB code spectra of one slot pair in that XCD's L2 (all 81 slots' spectra, 5.2 MB at
+  // C3, exceed one XCD's 4 MB L2 when every XCD sees every pair)
+  uint32_t f = blockIdx.y, bx = blockIdx.x;
+  if (a.xcd_order) {
+    const uint32_t G = gridDim.x * gridDim.y, b = blockIdx.y * gridDim.x + blockIdx.x;
+    const uint32_t x = b % 8, q = G / 8, rem = G % 8;
+    const uint32_t lid = x * q + min(x, rem) + b / 8;
+    const uint32_t nf = gridDim.y, nrx = a.N;
+    bx = (lid / (nrx * nf)) * nrx + lid % nrx;
+    f = (lid / nrx) % nf;
+  }
   const FrameInfo &I = a.info[f];
   if (I.status != 0) return;
   const int tid = threadIdx.x;
-  const uint32_t r = blockIdx.x % a.N;
-  const uint32_t s0 = 2 * (blockIdx.x / a.N);
+  const uint32_t r = bx % a.N;
+  const uint32_t s0 = 2 * (bx / a.N);
   const uint32_t ns = min(2u, a.n_slots - s0);
   const int64_t abs0 = I.base + (int64_t)a.SL * s0;
   const int64_t L = (int64_t)a.frame_len;
   const auto xs = iq_row<SC16>(a.iq, a.iq_scale, ((uint64_t)I.cap * a.N + r) * a.stride);
   const bool inb = abs0 >= 0 && abs0 + F <= L;
   v2f v[PTS], X[PTS];
+#ifdef SL_ABL_NOLOAD   // timing ablation: no segment loads
+#pragma unroll
+  for (int e = 0; e < PTS; e++) v[e] = v2f{(float)e, (float)(tid + (int)abs0)};
+  if (false) {
+#else
 #pragma unroll
   for (int e = 0; e < PTS; e++) {
     const int64_t n = abs0 + reg_index<LOG2F, PTS>(tid, e);
@@ -231,6 +249,7 @@ void search_ls_kernel(SearchArgs a) {
     v[e] = v2f{t.x, t.y};
   }
   if (!inb) {
+#endif
 #pragma unroll
     for (int e = 0; e < PTS; e++) {
       const int64_t n = abs0 + reg_index<LOG2F, PTS>(tid, e);
@@ -239,12 +258,21 @@ void search_ls_kernel(SearchArgs a) {
   }
   v2f w1[PL::NTW > 0 ? PL::NTW : 1];
   reg_twiddles<LOG2F, PTS>(w1, a.tw, tid);
-  // the LS transform's twiddles in LDS (no L2 round trip inside its passes)
+  // LS transform: register-resident (M/8 threads and 8 points per window, one window per half
+  // of the workgroup) when T = 2 M/8, else batched in LDS with its twiddles in LDS
+#ifdef SL_ABL_LSLDS   // A/B build: the LDS-batched LS transform everywhere
+  constexpr bool LSREG = false;
+#else
+  // (M >= 512: the register plan's last pass is radix 8 and each window fills whole waves)
+  constexpr bool LSREG = 2 * (M / 8) == T && LOG2M >= 9;
+#endif
   float2 *twm = reinterpret_cast<float2 *>(lds_raw) + lds_padded_len(F);
-  fill_twiddles_lds<LOG2M, T>(twm, a.tw);
+  if constexpr (!LSREG) fill_twiddles_lds<LOG2M, T>(twm, a.tw);
   if (tid == 0) { s_key[0] = 0ull; s_key[1] = 0ull; }
+#ifndef SL_ABL_NOFWD   // timing ablation: no forward transform
   reg_compute<LOG2F, PTS, 0, false>(v, w1);
   reg_rest<LOG2F, PTS, 1, false>(buf, v, w1, tid);
+#endif
 #pragma unroll
   for (int e = 0; e < PTS; e++) X[e] = v[e];
   for (uint32_t u = 0; u < ns; u++) {                 // uniform
@@ -290,6 +318,38 @@ void search_ls_kernel(SearchArgs a) {
   if (!valid0 && !valid1) return;                     // uniform
   const int64_t w0 = I.base + (int64_t)key_index(s_key[0]);
   const int64_t w1v = I.base + (int64_t)key_index(s_key[1]);
+  if constexpr (LSREG) {
+    // window u = tid / (M/8) on its half: 8 loads per thread straight into the first radix-8
+    // pass, two LDS exchanges, and X[k] of the last pass stored from registers
+    using PM = RegPlan<LOG2M, 8>;
+    const uint32_t u = (uint32_t)tid / PM::T, lt = (uint32_t)tid % PM::T;   // u uniform per wave
+    const bool valid = u ? valid1 : valid0;
+    const int64_t wb = u ? w1v : w0;
+    v2f xw[8];
+#pragma unroll
+    for (int e = 0; e < 8; e++) {
+      const int64_t n = wb + reg_index<LOG2M, 8>((int)lt, e);
+      const bool ok = valid && n >= 0 && n < L;
+      const float2 t = xs.at(n < 0 ? 0 : (n >= L ? L - 1 : n));   // clamped, masked below
+      xw[e] = ok ? v2f{t.x, t.y} : v2f{0.0f, 0.0f};
+    }
+    v2f wm[PM::NTW > 0 ? PM::NTW : 1];
+    reg_twiddles<LOG2M, 8>(wm, a.tw, (int)lt);
+    reg_compute<LOG2M, 8, 0, false>(xw, wm);
+    reg_rest<LOG2M, 8, 1, false>(buf + u * PBM, xw, wm, (int)lt);
+    if (!valid) return;                               // uniform per wave
+    const uint32_t ac = s0 + u - 1, code = ac / a.N, tx = ac % a.N;
+    const int8_t *sg = a.s1sign + ((size_t)tx * a.nac + code) * M;
+    float2 *q = a.lsq + ((((uint64_t)f * a.N + r) * a.N + tx) * a.nac + code) * M;
+#pragma unroll
+    for (int e = 0; e < 8; e++) {
+      const int k = reg_index<LOG2M, 8>((int)lt, e);
+      const int sgn = sg[k];
+      const float2 Xk = make_float2(xw[e].x, xw[e].y);
+      q[k] = sgn > 0 ? Xk : (sgn < 0 ? cneg(Xk) : make_float2(0.0f, 0.0f));
+    }
+    return;
+  }
   float2 win[NL];
 #pragma unroll
   for (int e = 0; e < NL; e++) {

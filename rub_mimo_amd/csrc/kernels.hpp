@@ -157,6 +157,7 @@ struct SearchArgs {
   const int8_t *s1sign;            // [N][nac][M]
   float2 *lsq;                     // [F][N][N][nac][M] X/S1 per access code
   uint32_t nac;
+  uint32_t xcd_order;              // search_ls_kernel: slot pair slowest within each XCD
 };
 void launch_search(const SearchArgs &a, int log2F, uint32_t n_frames, hipStream_t s);
 // true when (log2F, log2M) has a search_ls_kernel instance (it then ran)

@@ -11,6 +11,10 @@ for v in ${VARIANTS:-nols noinv}; do
     nols) D="-DSL_ABL_NOLS" ;;
     noinv) D="-DSL_ABL_NOINV" ;;
     both) D="-DSL_ABL_NOLS -DSL_ABL_NOINV" ;;
+    nofwd) D="-DSL_ABL_NOLS -DSL_ABL_NOINV -DSL_ABL_NOFWD" ;;     # loads + scoring only
+    noload) D="-DSL_ABL_NOLS -DSL_ABL_NOINV -DSL_ABL_NOFWD -DSL_ABL_NOLOAD" ;;   # scoring only
+    lslds) D="-DSL_ABL_LSLDS" ;;                                 # LS transform batched in LDS
+    lsonly) D="-DSL_ABL_NOINV -DSL_ABL_NOFWD" ;;                 # loads + scoring + LS
   esac
   /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -I../../include $D \
     -c est_kernels.hip -o $OUT/est_$v.o
