@@ -395,23 +395,35 @@ __global__ __launch_bounds__(256) void ls_combine_q_kernel(LsArgs a) {
     double sr = 0.0, si = 0.0, s2 = 0.0;
     const uint32_t r_ = rt / N, t_ = rt % N;
     const double nu = a.cfo_part ? cfo_stage_eps(a.cfo_part, f, 2) / (double)M : 0.0;
-    for (uint32_t c = 0; c < a.nac; c++) {
-      float2 v = q[(uint64_t)c * M];
-      if (a.cfo_part) {
-        // opt-in CFO: the residual's phase at this code's window (window-relative, about the
-        // frame's base), as the data region is derotated (cfo_kernels.hip stage 2)
-        const unsigned long long key =
-            a.keys[((uint64_t)f * N + r_) * a.n_slots + 1 + c * N + t_];
-        const double w = (double)key_index(key) + 0.5 * (double)M;
-        double ph = -2.0 * nu * w;
-        ph -= 2.0 * rint(ph * 0.5);
-        double sn, cs;
-        sincospi(ph, &sn, &cs);
-        v = make_float2((float)(v.x * cs - v.y * sn), (float)(v.x * sn + v.y * cs));
+    // the codes' terms in batches of CB loads in flight (one latency per batch instead of per
+    // code), summed in code order as before
+    constexpr uint32_t CB = 8;
+    for (uint32_t c0 = 0; c0 < a.nac; c0 += CB) {
+      float2 vb[CB];
+#pragma unroll
+      for (uint32_t j = 0; j < CB; j++)
+        vb[j] = q[(uint64_t)min(c0 + j, a.nac - 1) * M];   // clamped: every load unconditional
+#pragma unroll
+      for (uint32_t j = 0; j < CB; j++) {
+        const uint32_t c = c0 + j;
+        if (c >= a.nac) break;
+        float2 v = vb[j];
+        if (a.cfo_part) {
+          // opt-in CFO: the residual's phase at this code's window (window-relative, about the
+          // frame's base), as the data region is derotated (cfo_kernels.hip stage 2)
+          const unsigned long long key =
+              a.keys[((uint64_t)f * N + r_) * a.n_slots + 1 + c * N + t_];
+          const double w = (double)key_index(key) + 0.5 * (double)M;
+          double ph = -2.0 * nu * w;
+          ph -= 2.0 * rint(ph * 0.5);
+          double sn, cs;
+          sincospi(ph, &sn, &cs);
+          v = make_float2((float)(v.x * cs - v.y * sn), (float)(v.x * sn + v.y * cs));
+        }
+        sr += (double)v.x;
+        si += (double)v.y;
+        s2 += (double)v.x * v.x + (double)v.y * v.y;
       }
-      sr += (double)v.x;
-      si += (double)v.y;
-      s2 += (double)v.x * v.x + (double)v.y * v.y;
     }
     const uint32_t r = rt / N, t = rt % N;
     const double bias = (a.keep_bias && r == t) ? 1.0 : 0.0;
