@@ -48,7 +48,7 @@ WORKLOADS = {
                desc="C2: 2x2 ZF (reference adjugate), 1024-pt FFT, cp 76, 16-QAM, 20 access "
                     "codes, 1000 data symbols/frame (synthetic stand-in for recorded USRP IQ)"),
     "c3": dict(M=2048, cp=152, streams=4, nac=20, pid=1000, qam=64, snr=30.0, detector="mmse",
-               frames=32, fps=1,
+               frames=64, fps=1,
                desc="C3: 4x4 MMSE, 2048-pt FFT, cp 152, 64-QAM, 20 access codes, "
                     "1000 data symbols/frame"),
     "c4": dict(M=4096, cp=304, streams=8, nac=20, pid=1000, qam=256, snr=35.0, detector="mmse",
@@ -91,6 +91,8 @@ def parse():
                     help="steps of the secondary sc16-resident leg of an fc32 run (0: skip; "
                          "default: --steps)")
     ap.add_argument("--cpu-baseline", type=int, default=1, help="0 to skip the oracle timing")
+    ap.add_argument("--h2d", type=int, default=1,
+                    help="0 to skip the separately reported pinned-host -> HBM copy timing")
     ap.add_argument("--cpu-threads", type=int, default=0,
                     help="threads of the multi-core CPU baseline (0: the box's core share)")
     ap.add_argument("--ref-mode", type=int, default=1,
@@ -537,6 +539,31 @@ def main():
                          "delta_db": evm_gpu - evm_cpu,
                          "sync_index_equal": int(o.get_sync_index()) == int(r["sync_index"])}
 
+    # ---- H2D, reported separately (never the headline): the batch's captures
+    # copied from pinned host memory into HBM on the receive stream, at most 8 captures
+    h2d = None
+    if rank == 0 and args.h2d:
+        nc = min(F, 8)
+        dev_iq = iq[:nc]
+        host = torch.empty(dev_iq.shape, dtype=dev_iq.dtype, pin_memory=True)
+        host.copy_(dev_iq)
+        cur = torch.cuda.current_stream(dev)
+        ts = []
+        for _ in range(3):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(cur)
+            dev_iq.copy_(host, non_blocking=True)
+            e1.record(cur)
+            e1.synchronize()
+            ts.append(e0.elapsed_time(e1) / 1e3)
+        t = min(ts)
+        nbytes = host.numel() * host.element_size()
+        h2d = {"gbs": nbytes / t / 1e9, "samples_per_s": nbytes / 8 / t, "captures": nc,
+               "ms": t * 1e3, "bytes": nbytes,
+               "note": "pinned host -> HBM copy of %d fc32 captures (best of 3), PCIe-inclusive "
+                       "ingest rate; the headline starts with the captures resident" % nc}
+        del host
+
     value = samples_total / elapsed
     ms_step = elapsed / args.steps * 1e3
     bytes_alg = scanned_total * in_bytes + args.steps * n_dec_all * N * m_occ * 9
@@ -583,6 +610,12 @@ def main():
         "symbol_errors_last_step": int(errors),
         "rank0_scatter": scatter_info,
         "sc16_resident": sc16_info,
+        # FFT + detect + demap + EVM given W (the decode stage alone), samples of the decoded
+        # symbols (N antennas x (M + cp)) per second of the decode kernels' event time
+        "decode_stage": {"value": (n_dec * N * (M + cp) / dec_avg_s) if dec_avg_s > 0 else None,
+                         "unit": "complex samples/s", "ms_per_step": dec_avg_s * 1e3,
+                         "symbols_per_step": n_dec},
+        "h2d": h2d,
     }
     if rank == 0:
         print(json.dumps(line), flush=True)
