@@ -136,6 +136,45 @@ MIMO_DEV void dft_inv_pk(v2f *a) {
   }
 }
 
+// radix-16 DFT (natural order in and out) as 4 x 4: DFT4 over n1 of x[4 n1 + n2] for each n2,
+// the twiddles W16^(n2 k1), then DFT4 over n2 for each k1 -> X[k1 + 4 k2]
+template <bool INV>
+MIMO_DEV void dft16_pk(v2f *a) {
+  constexpr float C1 = 0.92387953251128674f, S1 = 0.38268343236508978f;
+  constexpr float R2 = 0.70710678118654752f;
+  v2f y[16];                                           // y[4 n2 + k1]
+#pragma unroll
+  for (int n2 = 0; n2 < 4; n2++) {
+    v2f t[4] = {a[n2], a[n2 + 4], a[n2 + 8], a[n2 + 12]};
+    if constexpr (INV) dft_inv_pk<4>(t); else dft_fwd_pk<4>(t);
+#pragma unroll
+    for (int k1 = 0; k1 < 4; k1++) y[4 * n2 + k1] = t[k1];
+  }
+  // W16^e (e = n2 k1): 1, 2, 3 | 2, 4, 6 | 3, 6, 9; conjugated for the inverse
+  const v2f w1 = INV ? v2f{C1, S1} : v2f{C1, -S1};
+  const v2f w3 = INV ? v2f{S1, C1} : v2f{S1, -C1};
+  const v2f w9 = INV ? v2f{-C1, -S1} : v2f{-C1, S1};
+  auto w2 = [&](v2f x) { return R2 * (INV ? sub_mi(x, x) : add_mi(x, x)); };
+  auto w6 = [&](v2f x) { return R2 * (INV ? rot_p_b(x) : rot_m_b(x)); };
+  auto w4 = [&](v2f x) { return INV ? v2f{-x.y, x.x} : v2f{x.y, -x.x}; };
+  y[5] = cmul_pk(y[5], w1);
+  y[6] = w2(y[6]);
+  y[7] = cmul_pk(y[7], w3);
+  y[9] = w2(y[9]);
+  y[10] = w4(y[10]);
+  y[11] = w6(y[11]);
+  y[13] = cmul_pk(y[13], w3);
+  y[14] = w6(y[14]);
+  y[15] = cmul_pk(y[15], w9);
+#pragma unroll
+  for (int k1 = 0; k1 < 4; k1++) {
+    v2f t[4] = {y[k1], y[4 + k1], y[8 + k1], y[12 + k1]};
+    if constexpr (INV) dft_inv_pk<4>(t); else dft_fwd_pk<4>(t);
+#pragma unroll
+    for (int k2 = 0; k2 < 4; k2++) a[k1 + 4 * k2] = t[k2];
+  }
+}
+
 template <bool INV>
 MIMO_DEV v2f twiddle(const float2 *__restrict__ tw, int idx) {
   const float2 w = tw[idx];
@@ -150,7 +189,9 @@ MIMO_DEV v2f rot_mi(v2f a) {
 
 template <int R, bool INV>
 MIMO_DEV void dft_small(v2f *a) {
-  if constexpr (true) {                     // single-instruction packed forms, same arithmetic
+  if constexpr (R == 16) {
+    dft16_pk<INV>(a);
+  } else if constexpr (true) {              // single-instruction packed forms, same arithmetic
     if constexpr (INV) dft_inv_pk<R>(a); else dft_fwd_pk<R>(a);
   } else if constexpr (R == 2) {
     const v2f t0 = a[0] + a[1], t1 = a[0] - a[1];

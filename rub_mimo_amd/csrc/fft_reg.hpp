@@ -1,30 +1,43 @@
 // rub_mimo_amd/csrc/fft_reg.hpp -- register-resident Stockham FFT for one workgroup (gfx950).
 //
 // One N-point transform, T threads, PTS = N/T points per thread held in registers. Every pass
-// is radix 8 except one radix-2/-4 pass (log2 N not a multiple of 3), placed third so that the
-// first and the last pass are radix 8 and the twiddles of the forward and the inverse plan are
-// the same per-thread values (conjugated). In a pass of radix R the thread runs PTS/R
-// butterflies j = tid + i*T; butterfly j reads elements j + r*N/R and writes Stockham order.
-// Between passes the thread's values go through one padded LDS image (two barriers). The
-// first pass may read straight from global memory and the last pass leaves elements
-// j + r*N/8 in the thread, which is exactly what the first pass of the next transform (of the
-// same plan) reads: a forward transform, a pointwise product and an inverse transform chain
-// in registers with no exchange between them (search_kernel).
+// has the main radix (16 with 16 points per thread, else 8) except one smaller pass (log2 N
+// not a multiple of log2 of it), placed before the last so that the first and the last pass
+// have the main radix R and the twiddles of the forward and the inverse plan are the same
+// per-thread values (conjugated). In a pass of radix r the thread runs PTS/r butterflies
+// j = tid + i*T; butterfly j reads elements j + q*N/r and writes Stockham order. Between
+// passes the thread's values go through one padded LDS image (two barriers). The first pass
+// may read straight from global memory and the last pass leaves elements j + q*N/R in the
+// thread, which is exactly what the first pass of the next transform (of the same plan)
+// reads: a forward transform, a pointwise product and an inverse transform chain in registers
+// with no exchange between them (search kernels).
 #pragma once
 
 #include "fft.hpp"
 
 namespace mimo {
 
+// Main radix: 16 with 16 points per thread (one butterfly per pass, one LDS exchange fewer
+// per transform than radix 8 at N = 2^10 .. 2^14), else 8. REG_RADIX8 builds the radix-8 plan
+// everywhere (A/B timing).
+#ifdef REG_RADIX8
+constexpr bool kRegR16 = false;
+#else
+constexpr bool kRegR16 = true;
+#endif
+
 template <int LOG2N, int PTS>
 struct RegPlan {
   static constexpr int N = 1 << LOG2N;
   static constexpr int T = N / PTS;
-  static constexpr int P8 = LOG2N / 3;
-  static constexpr int TAIL = LOG2N % 3;
+  static constexpr int LR = (kRegR16 && PTS >= 16 && LOG2N >= 9) ? 4 : 3;   // log2 main radix
+  static constexpr int RM = 1 << LR;
+  static constexpr int P8 = LOG2N / LR;                 // main-radix passes
+  static constexpr int TAIL = LOG2N % LR;
   static constexpr int NP = P8 + (TAIL ? 1 : 0);
-  static constexpr int TPOS = P8 < 2 ? P8 : 2;          // index of the radix-2/-4 pass
-  static constexpr int radix(int p) { return (TAIL && p == TPOS) ? (1 << TAIL) : 8; }
+  // the smaller pass sits before the last one: the first and the last pass have the main radix
+  static constexpr int TPOS = P8 < 2 ? P8 : (P8 - 1 < 2 ? P8 - 1 : 2);
+  static constexpr int radix(int p) { return (TAIL && p == TPOS) ? (1 << TAIL) : RM; }
   static constexpr int ns(int p) {
     int n = 1;
     for (int q = 0; q < p; q++) n *= radix(q);
@@ -92,11 +105,21 @@ MIMO_DEV void reg_compute(v2f *v, const v2f *w1) {
         w[2] = vmul(w[1], w[1]);
         w[3] = vmul(w[2], w[1]);
       }
-      if constexpr (R == 8) {
+      if constexpr (R >= 8) {
         w[4] = vmul(w[2], w[2]);
         w[5] = vmul(w[4], w[1]);
         w[6] = vmul(w[3], w[3]);
         w[7] = vmul(w[4], w[3]);
+      }
+      if constexpr (R == 16) {
+        w[8] = vmul(w[4], w[4]);
+        w[9] = vmul(w[8], w[1]);
+        w[10] = vmul(w[5], w[5]);
+        w[11] = vmul(w[8], w[3]);
+        w[12] = vmul(w[6], w[6]);
+        w[13] = vmul(w[8], w[5]);
+        w[14] = vmul(w[7], w[7]);
+        w[15] = vmul(w[8], w[7]);
       }
 #pragma unroll
       for (int r = 1; r < R; r++) v[i * R + r] = vmul(v[i * R + r], w[r]);
@@ -137,11 +160,13 @@ MIMO_DEV void reg_rest(v2f *buf, v2f *v, const v2f *w1, int tid) {
   }
 }
 
-// element index held in v[s] after the last pass (and read by pass 0): j + r*N/8
+// element index held in v[s] after the last pass (and read by pass 0): j + r*N/R, R the main
+// radix (the first and the last pass)
 template <int LOG2N, int PTS>
 MIMO_DEV int reg_index(int tid, int s) {
   using PL = RegPlan<LOG2N, PTS>;
-  return tid + (s / 8) * PL::T + (s % 8) * (PL::N / 8);
+  constexpr int R = PL::RM;
+  return tid + (s / R) * PL::T + (s % R) * (PL::N / R);
 }
 
 }  // namespace mimo
