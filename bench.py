@@ -2,7 +2,7 @@
 
 Default workload C3 (BASELINE.json configs[2], the config the metric is quoted on): 2048-pt
 FFT, cp 152, 4x4, 20 access codes, 1000 data symbols, 64-QAM, synthetic flat Rayleigh channel
-at 30 dB SNR, 32 captures per step per GPU. --workload c2 / c4 / c5 run the other GPU configs.
+at 30 dB SNR, 64 captures per step per GPU. --workload c2 / c4 / c5 run the other GPU configs.
 
 One step = one pass of the whole receive chain (Schmidl-Cox + plateau, access-code search, LS
 estimate, detector weights, replay decode, demap, EVM) over a batch of synthetic captures

@@ -76,7 +76,9 @@ typedef struct mimo_rx_config {
                                  S0 half-period correlation ending at its trigger, summed over
                                  the antennas, and derotate its window (into a device scratch
                                  copy; the caller's capture is not modified) before search, LS
-                                 and decode. 0 = off (the reference's behaviour). */
+                                 and decode. 0 = off (the reference's behaviour). Batches
+                                 with frames_per_capture > 1 are refused with
+                                 MIMO_ERR_UNSUPPORTED. */
 } mimo_rx_config;
 
 typedef struct mimo_rx mimo_rx;
@@ -196,6 +198,12 @@ int mimo_rx_get_stage_times(mimo_rx *h, double *ms, uint32_t *launches);
 /* S&C samples whose fp64 metric fell within the decision band and were recomputed with the
  * oracle's exact fp32 order, since the last call (diagnostic; synchronises) */
 int mimo_rx_get_sc_exact_count(mimo_rx *h, uint64_t *out);
+/* the replay-decode kernel family the last batch or execute launched (diagnostic, no sync):
+ * STREAM = decode_stream_kernel (persistent, 2x2/4x4), SPLIT = spectra_kernel +
+ * apply_split_kernel (8x8 at M >= 512), SYMBOL = the per-symbol kernels, NONE = no decode yet */
+enum { MIMO_DECODE_NONE = 0, MIMO_DECODE_STREAM = 1, MIMO_DECODE_SPLIT = 2,
+       MIMO_DECODE_SYMBOL = 3 };
+int mimo_rx_get_decode_path(const mimo_rx *h, int32_t *path);
 
 /* ---------------- transmitter: framegen (framing.h:42-103) ---------------- */
 typedef struct mimo_tx mimo_tx;
@@ -267,8 +275,14 @@ typedef struct mimo_ring mimo_ring;
 int mimo_ring_create(uint32_t n_ant, uint32_t chunk_samples, uint32_t n_chunks, mimo_ring **out);
 int mimo_ring_destroy(mimo_ring *r);   /* waits for the uploads in flight */
 /* target of the following commits: d_capture rows of `capacity` samples, `stride` apart
- * (samples; capacity <= stride); write position 0 */
+ * (samples; capacity <= stride); write position 0. The uploads are not ordered against
+ * readers of d_capture: rebinding a capture that a published batch may still be reading needs
+ * the caller to synchronise first, or mimo_ring_bind_after. */
 int mimo_ring_bind(mimo_ring *r, void *d_capture, uint64_t stride, uint64_t capacity);
+/* mimo_ring_bind, and the uploads into the new binding wait (on the device) for the work
+ * enqueued on consumer_stream so far: a capture can be refilled while its batch runs */
+int mimo_ring_bind_after(mimo_ring *r, void *d_capture, uint64_t stride, uint64_t capacity,
+                         void *consumer_stream);
 /* the next chunk: rows[a] = host pointer of antenna a's chunk_samples interleaved int16 I/Q
  * (UHD's per-channel buffer vector, main.cc:874); waits for that chunk's previous upload */
 int mimo_ring_acquire(mimo_ring *r, void **rows, uint32_t *max_samples);

@@ -21,6 +21,7 @@ STAGE_NAMES = ("sc", "plateau", "search", "ls", "weights", "decode", "evm")
 STATE_SEEK_PLATEAU, STATE_SAVE_ACCESS_CODES, STATE_WAIT, STATE_MIMO = 0, 1, 2, 3
 DET_ZF2, DET_ZF, DET_MMSE, DET_SISO = 0, 1, 2, 3
 FRAME_OK, FRAME_NO_SYNC, FRAME_INCOMPLETE, FRAME_RESCAN, FRAME_NONE = 0, 1, 2, 3, 4
+DECODE_NONE, DECODE_STREAM, DECODE_SPLIT, DECODE_SYMBOL = 0, 1, 2, 3
 
 
 class RxConfig(C.Structure):
@@ -91,6 +92,7 @@ SIGNATURES = {
     "mimo_rx_set_timing": (C.c_int, [_vp, C.c_int]),
     "mimo_rx_get_stage_times": (C.c_int, [_vp, _P(C.c_double), _P(_u32)]),
     "mimo_rx_get_sc_exact_count": (C.c_int, [_vp, _P(_u64)]),
+    "mimo_rx_get_decode_path": (C.c_int, [_vp, _P(_i32)]),
     "mimo_tx_create": (C.c_int, [_u32, _u32, _u32, _u32, _vp, _vp, _vp, _P(_vp)]),
     "mimo_tx_destroy": (C.c_int, [_vp]),
     "mimo_tx_write_sync_words": (C.c_int, [_vp, _P(_vp), _P(_u32)]),
@@ -115,6 +117,7 @@ SIGNATURES = {
     "mimo_ring_create": (C.c_int, [_u32, _u32, _u32, _P(_vp)]),
     "mimo_ring_destroy": (C.c_int, [_vp]),
     "mimo_ring_bind": (C.c_int, [_vp, _vp, _u64, _u64]),
+    "mimo_ring_bind_after": (C.c_int, [_vp, _vp, _u64, _u64, _vp]),
     "mimo_ring_acquire": (C.c_int, [_vp, _P(_vp), _P(_u32)]),
     "mimo_ring_commit": (C.c_int, [_vp, _u32]),
     "mimo_ring_publish": (C.c_int, [_vp, _vp, _P(_u64)]),

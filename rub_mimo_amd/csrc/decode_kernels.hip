@@ -829,17 +829,23 @@ static uint32_t decode_dispatch(const DecodeArgs &a, int log2M, uint32_t nf, hip
 }
 
 uint32_t launch_decode(const DecodeArgs &a, int log2M, uint32_t n_frames, hipStream_t s,
-                       bool *per_frame_records) {
+                       bool *per_frame_records, int *path) {
   *per_frame_records = false;
+  *path = 0;
   if (a.expt == 0) {
     uint32_t parts = launch_decode_stream(a, log2M, n_frames, s);
-    if (!parts) parts = launch_decode_split(a, log2M, n_frames, s);
+    if (parts) *path = 1;
+    if (!parts && (parts = launch_decode_split(a, log2M, n_frames, s))) *path = 2;
     if (parts) {
       *per_frame_records = true;
       return parts;
     }
   }
-  return decode_dispatch<6>(a, log2M, n_frames, s);
+  // the per-symbol kernels read complex64 only: sc16 wire input never falls through to them
+  if (a.sc16) return 0;
+  const uint32_t parts = decode_dispatch<6>(a, log2M, n_frames, s);
+  if (parts) *path = 3;
+  return parts;
 }
 
 void launch_evm(const EvmArgs &a, uint32_t n_frames, hipStream_t s) {

@@ -242,6 +242,7 @@ struct mimo_rx {
   uint32_t cap_hot = 0;
   DevBuf<unsigned long long> sc_prof;   // RMIMO_SC_PROF=1 cycle counters
   uint32_t last_frames = 0, last_max_out = 0;
+  int last_decode_path = MIMO_DECODE_NONE;   // kernel family of the last decode launch
   // streaming state (facade)
   DevBuf<float2> capbuf;
   uint64_t cap_len = 0, total = 0;
@@ -254,12 +255,17 @@ struct mimo_rx {
   mimo_rx_symbol_cb cb = nullptr;
   void *user = nullptr;
   StageTimer timer;
-  // captured batch pipeline (see mimo_rx_process_batch)
-  mimo_batch g_key{};
-  hipStream_t g_stream = nullptr;
-  bool g_valid = false;
-  hipGraphExec_t g_exec = nullptr;
-  std::array<const void *, 27> g_sig{};
+  // captured batch pipelines (see mimo_rx_process_batch): a few recent batch keys, so that
+  // callers alternating between capture buffers (double-buffered ingest) replay graphs too
+  struct GraphEntry {
+    mimo_batch key{};
+    hipStream_t stream = nullptr;
+    std::array<const void *, 27> sig{};
+    hipGraphExec_t exec = nullptr;
+    uint64_t used = 0;            // 0: empty slot
+  };
+  std::array<GraphEntry, 4> graphs{};
+  uint64_t graph_tick = 0;
 };
 
 struct mimo_tx {
@@ -584,6 +590,17 @@ int run_estimate(mimo_rx *h, const float2 *iq, uint64_t stride, uint32_t F, uint
   return MIMO_OK;
 }
 
+// diagnostics that force the per-symbol decode kernels: RMIMO_DECODE_GRID=1 (the
+// one-workgroup-per-symbol grid, A/B against the persistent form) and RMIMO_DEC_EXPT
+bool decode_grid_only() {
+  static const bool v = [] { const char *e = getenv("RMIMO_DECODE_GRID"); return e && e[0] == '1'; }();
+  return v;
+}
+int decode_expt() {
+  static const int v = [] { const char *e = getenv("RMIMO_DEC_EXPT"); return e ? atoi(e) : 0; }();
+  return v;
+}
+
 int run_decode(mimo_rx *h, const float2 *iq, uint64_t stride, uint32_t F, uint64_t frame_len,
                uint32_t max_out, float2 *out_sym, uint8_t *out_idx, int ref_mode,
                const uint8_t *ref_idx, uint64_t ref_seed, uint64_t frame_id0, hipStream_t s,
@@ -602,11 +619,8 @@ int run_decode(mimo_rx *h, const float2 *iq, uint64_t stride, uint32_t F, uint64
   d.qam = h->qam; d.evm_part = h->evm_part.p; d.tw = h->tw;
   d.n_frames = F; d.n_cu = h->n_cu;
   d.n_caps = n_caps ? n_caps : F; d.n_refs = F;
-  // RMIMO_DECODE_GRID=1 forces the one-workgroup-per-symbol grid (A/B against the persistent form)
-  static const bool grid_only = [] { const char *e = getenv("RMIMO_DECODE_GRID"); return e && e[0] == '1'; }();
-  d.all_occ = (h->M_occ == h->M && !grid_only) ? 1 : 0;
-  static const int expt = [] { const char *e = getenv("RMIMO_DEC_EXPT"); return e ? atoi(e) : 0; }();
-  d.expt = expt;
+  d.all_occ = (h->M_occ == h->M && !decode_grid_only()) ? 1 : 0;
+  d.expt = decode_expt();
   static const bool dprof = [] { const char *e = getenv("RMIMO_DEC_PROF"); return e && e[0] == '1'; }();
   if (dprof) {
     if (!h->sc_prof.p) HIPCHK(h->sc_prof.ensure(20));
@@ -624,8 +638,12 @@ int run_decode(mimo_rx *h, const float2 *iq, uint64_t stride, uint32_t F, uint64
     d.spec = h->spec.p;
   }
   bool per_frame = false;
-  const uint32_t parts = launch_decode(d, h->log2M, F, s, &per_frame);
+  int path = MIMO_DECODE_NONE;
+  const uint32_t parts = launch_decode(d, h->log2M, F, s, &per_frame, &path);
   h->timer.end(5, e, s);
+  h->last_decode_path = path;
+  if (!parts)   // run_batch widens every sc16 batch the streaming decode does not take
+    return fail(MIMO_ERR_UNSUPPORTED, "no decode kernel takes this configuration");
   if (dprof) {   // diagnostics: per-item cycle split of the decode kernel
     unsigned long long v[5];
     HIPCHK(hipMemcpyAsync(v, h->sc_prof.p, sizeof(v), hipMemcpyDeviceToHost, s));
@@ -776,7 +794,8 @@ int mimo_rx_destroy(mimo_rx *h) {
     (void)hipEventDestroy(e.second.first);
     (void)hipEventDestroy(e.second.second);
   }
-  if (h->g_exec) (void)hipGraphExecDestroy(h->g_exec);
+  for (auto &g : h->graphs)
+    if (g.exec) (void)hipGraphExecDestroy(g.exec);
   if (h->own_stream && h->stream) (void)hipStreamDestroy(h->stream);
   delete h;
   return MIMO_OK;
@@ -792,13 +811,16 @@ int mimo_rx_set_callback(mimo_rx *h, mimo_rx_symbol_cb cb, void *user) {
 // A captured batch graph bakes every host scalar of the launch arguments (siso indices,
 // detector, noise variance, threshold) into its kernel nodes: any setter of such a scalar
 // drops the graph so the next batch is launched (and later re-captured) with the new value.
-static void invalidate_graph(mimo_rx *h) {
-  if (h->g_exec) {
-    (void)hipStreamSynchronize(h->g_stream ? h->g_stream : h->stream);
-    (void)hipGraphExecDestroy(h->g_exec);
-    h->g_exec = nullptr;
+static void drop_graph(mimo_rx *h, mimo_rx::GraphEntry &g) {
+  if (g.exec) {   // a replay may still be in flight on its stream
+    (void)hipStreamSynchronize(g.stream ? g.stream : h->stream);
+    (void)hipGraphExecDestroy(g.exec);
   }
-  h->g_valid = false;
+  g = mimo_rx::GraphEntry{};
+}
+
+static void invalidate_graph(mimo_rx *h) {
+  for (auto &g : h->graphs) drop_graph(h, g);
 }
 
 int mimo_rx_set_siso(mimo_rx *h, uint32_t tx, uint32_t rx) {
@@ -1065,14 +1087,15 @@ static int run_batch(mimo_rx *h, const mimo_batch *b, hipStream_t s) {
     // sc16 wire input: read in place by S&C, the fused search + LS and the streaming decode
     // where the configuration takes them; otherwise widened once into an internal fc32 batch
     DecodeArgs probe{};
-    probe.N = h->N; probe.detector = h->det; probe.all_occ = h->M_occ == h->M ? 1 : 0;
+    probe.N = h->N; probe.detector = h->det;
+    probe.all_occ = (h->M_occ == h->M && !decode_grid_only()) ? 1 : 0;
     probe.n_caps = b->n_frames; probe.n_refs = slots; probe.qam = h->qam;
     probe.ref_mode = b->ref_mode; probe.ref_idx = reinterpret_cast<const uint8_t *>(b->d_ref_idx);
     probe.stride = b->stride; probe.max_out = b->max_out_syms; probe.M_occ = h->M_occ;
     probe.out_sym = reinterpret_cast<float2 *>(b->d_out_sym);
     probe.out_idx = reinterpret_cast<uint8_t *>(b->d_out_idx);
     probe.sc16 = 1;
-    const bool fused = sc_screen_ok(h->M) && h->search_ls && !h->cfo &&
+    const bool fused = sc_screen_ok(h->M) && h->search_ls && !h->cfo && decode_expt() == 0 &&
                        decode_stream_accepts(probe, h->log2M, slots);
     if (fused) {
       h->cur_sc16 = 1;
@@ -1153,6 +1176,10 @@ int mimo_rx_process_batch(mimo_rx *h, const mimo_batch *b, void *hip_stream) {
   if (b->ref_mode == 1 && !b->d_ref_idx) return fail(MIMO_ERR_ARG, "ref_mode 1 needs d_ref_idx");
   if (batch_fpc(b) > 64)
     return fail(MIMO_ERR_ARG, "frames_per_capture must be at most 64");
+  // the opt-in CFO stages derotate each frame's window into one scratch capture per capture:
+  // back-to-back frames' windows overlap there, so the combination is refused
+  if (h->cfo && batch_fpc(b) > 1)
+    return fail(MIMO_ERR_UNSUPPORTED, "cfo_correct needs frames_per_capture <= 1");
   hipStream_t s = hip_stream ? (hipStream_t)hip_stream : h->stream;
   static const bool no_graph = [] {
     const char *e = getenv("RMIMO_NO_GRAPH");
@@ -1160,15 +1187,20 @@ int mimo_rx_process_batch(mimo_rx *h, const mimo_batch *b, void *hip_stream) {
     const char *p2 = getenv("RMIMO_DEC_PROF");
     return (e && e[0] == '1') || (p1 && p1[0] == '1') || (p2 && p2[0] == '1');
   }();
-  const bool key_same = h->g_valid && same_batch(h->g_key, *b) && h->g_stream == s &&
-                        h->g_sig == ws_signature(h);
+  // the cache entry of this batch: same arguments, stream and workspace pointers
+  const auto sig = ws_signature(h);
+  mimo_rx::GraphEntry *hit = nullptr;
+  for (auto &g : h->graphs)
+    if (g.used && same_batch(g.key, *b) && g.stream == s && g.sig == sig) hit = &g;
   int rc = MIMO_OK;
   if (no_graph || h->timer.on) {
     rc = run_batch(h, b, s);
-  } else if (key_same && h->g_exec) {
-    HIPCHK(hipGraphLaunch(h->g_exec, s));
-  } else if (key_same) {
+  } else if (hit && hit->exec) {
+    hit->used = ++h->graph_tick;
+    HIPCHK(hipGraphLaunch(hit->exec, s));
+  } else if (hit) {
     // second identical call: workspace and one-time kernel attributes are settled; capture
+    hit->used = ++h->graph_tick;
     hipGraph_t g = nullptr;
     HIPCHK(hipStreamBeginCapture(s, hipStreamCaptureModeRelaxed));
     rc = run_batch(h, b, s);
@@ -1177,26 +1209,36 @@ int mimo_rx_process_batch(mimo_rx *h, const mimo_batch *b, void *hip_stream) {
       hipGraphExec_t ex = nullptr;
       const bool inst = hipGraphInstantiate(&ex, g, nullptr, nullptr, 0) == hipSuccess;
       (void)hipGraphDestroy(g);
-      if (inst && h->g_sig == ws_signature(h)) {
-        h->g_exec = ex;
-        HIPCHK(hipGraphLaunch(h->g_exec, s));
+      if (inst && hit->sig == ws_signature(h)) {
+        hit->exec = ex;
+        HIPCHK(hipGraphLaunch(hit->exec, s));
       } else {
         if (inst) (void)hipGraphExecDestroy(ex);
-        h->g_valid = false;
+        *hit = mimo_rx::GraphEntry{};
         rc = run_batch(h, b, s);
       }
     } else {
       if (g) (void)hipGraphDestroy(g);
       (void)hipGetLastError();
+      *hit = mimo_rx::GraphEntry{};
       if (!rc) rc = run_batch(h, b, s);   // capture failed: run directly
     }
   } else {
-    if (h->g_exec) { (void)hipGraphExecDestroy(h->g_exec); h->g_exec = nullptr; }
     rc = run_batch(h, b, s);
-    h->g_key = *b;
-    h->g_stream = s;
-    h->g_sig = ws_signature(h);
-    h->g_valid = (rc == MIMO_OK);
+    // a workspace reallocation makes every earlier capture stale
+    const auto sig2 = ws_signature(h);
+    for (auto &g : h->graphs)
+      if (g.used && g.sig != sig2) drop_graph(h, g);
+    if (rc == MIMO_OK) {
+      mimo_rx::GraphEntry *slot = &h->graphs[0];   // an empty or the least recently used slot
+      for (auto &g : h->graphs)
+        if (g.used < slot->used) slot = &g;
+      drop_graph(h, *slot);
+      slot->key = *b;
+      slot->stream = s;
+      slot->sig = sig2;
+      slot->used = ++h->graph_tick;
+    }
   }
   if (rc) return rc;
   h->last_frames = b->n_frames * batch_fpc(b);
@@ -1272,6 +1314,12 @@ int mimo_rx_batch_W(mimo_rx *h, float *W, uint32_t F) {
 int mimo_rx_set_timing(mimo_rx *h, int enable) {
   if (!h) return fail(MIMO_ERR_ARG, "null handle");
   h->timer.on = enable != 0;
+  return MIMO_OK;
+}
+
+int mimo_rx_get_decode_path(const mimo_rx *h, int32_t *path) {
+  if (!h || !path) return fail(MIMO_ERR_ARG, "null argument");
+  *path = h->last_decode_path;
   return MIMO_OK;
 }
 

@@ -262,10 +262,12 @@ struct DecodeArgs {
   int expt;                        // diagnostics (RMIMO_DEC_EXPT): bit 0 IQ from one symbol,
                                    // bit 1 no output stores, bit 2 weights of subcarrier 0
 };
-// returns the number of EVM partial sets written per symbol (see EvmArgs::parts); sets
-// *per_frame_records when the streaming kernel wrote nrec[f] records per frame instead
+// returns the number of EVM partial sets written per symbol (see EvmArgs::parts), 0 when no
+// kernel takes the configuration (nothing launched: an sc16 batch the streaming kernel does not
+// take); sets *per_frame_records when the streaming kernel wrote nrec[f] records per frame
+// instead, and *path to the kernel family launched (MIMO_DECODE_*: 1 stream, 2 split, 3 symbol)
 uint32_t launch_decode(const DecodeArgs &a, int log2M, uint32_t n_frames, hipStream_t s,
-                       bool *per_frame_records);
+                       bool *per_frame_records, int *path);
 // decode_stream.hip: persistent streaming form (0 when the configuration is not handled)
 uint32_t launch_decode_stream(const DecodeArgs &a, int log2M, uint32_t n_frames, hipStream_t s);
 // true when launch_decode_stream takes this configuration (nrec aside): the sc16 wire input

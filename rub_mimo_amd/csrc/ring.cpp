@@ -37,6 +37,7 @@ struct mimo_ring {
   char *cap = nullptr;                  // bound capture (sc16)
   uint64_t stride = 0, capacity = 0, pos = 0;
   hipEvent_t last = nullptr;            // the latest commit's event (nullptr: none yet)
+  hipEvent_t consumed = nullptr;        // bind_after: the consumer's work on a rebound capture
 };
 
 #define RCHK(x, what)                                                                  \
@@ -50,6 +51,7 @@ static void ring_free(mimo_ring *r) {
   if (r->copy) (void)hipStreamSynchronize(r->copy);
   for (hipEvent_t e : r->done)
     if (e) (void)hipEventDestroy(e);
+  if (r->consumed) (void)hipEventDestroy(r->consumed);
   if (r->copy) (void)hipStreamDestroy(r->copy);
   if (r->host) (void)hipHostFree(r->host);
   delete r;
@@ -96,6 +98,21 @@ extern "C" int mimo_ring_bind(mimo_ring *r, void *d_capture, uint64_t stride, ui
   r->stride = stride;
   r->capacity = capacity;
   r->pos = 0;
+  return MIMO_OK;
+}
+
+// Write-after-read ordering for a rebound capture: the copy stream waits, on the device, for
+// everything enqueued on consumer_stream so far (e.g. the batch still reading the capture)
+// before the first upload of the new binding.
+extern "C" int mimo_ring_bind_after(mimo_ring *r, void *d_capture, uint64_t stride,
+                                    uint64_t capacity, void *consumer_stream) {
+  int rc = mimo_ring_bind(r, d_capture, stride, capacity);
+  if (rc) return rc;
+  std::lock_guard<std::mutex> lk(r->mu);
+  if (!r->consumed)
+    RCHK(hipEventCreateWithFlags(&r->consumed, hipEventDisableTiming), "mimo_ring_bind_after");
+  RCHK(hipEventRecord(r->consumed, (hipStream_t)consumer_stream), "mimo_ring_bind_after");
+  RCHK(hipStreamWaitEvent(r->copy, r->consumed, 0), "mimo_ring_bind_after");
   return MIMO_OK;
 }
 

@@ -1499,7 +1499,10 @@ MIMO_DEV int ring_slot(int64_t p, int64_t w0, int M, int RING) {
 }
 
 constexpr int kLocAmb = kScT / 2;   // near-threshold samples resolved per iteration pass
-constexpr int kResSpread = 1024;    // positions spanned by one exact-recompute window
+// positions spanned by one exact-recompute window: the tables hold M + kResSpread positions,
+// sized so that two workgroups fit a CU at M = 2048 (a plateau's two near-threshold edges,
+// ~cp + 115 positions apart, still share one window)
+constexpr int kResSpread = 512;
 
 // one (listed chunk, antenna): the item kernel's antenna pass over the iterations covering the
 // chunk's unproven range (and its cp+2 run history). Near-threshold samples are resolved in
@@ -1515,12 +1518,14 @@ void sc_exact_kernel(ScArgs a) {
   __shared__ double scan_ws[2][5][kScT / 64];
   __shared__ long long s_amb[kLocAmb], s_sorted[kLocAmb];
   __shared__ float s_rv[kLocAmb][3];
-  // exact-recompute tables after the ring: rtz[W] (0.5|x|^2), rtp[W] (-conj(x[k-M/2]) x[k])
+  // exact-recompute tables after the ring: rtz[i] = 0.5|x|^2 at table position i < W and
+  // rtp[i - M/2] = -conj(x[k-M/2]) x[k] for M/2 <= i < W (only those are summed)
   float *rtz = reinterpret_cast<float *>(sc_dyn + sizeof(float2) * ring_pad(RING));
   float2 *rtp = reinterpret_cast<float2 *>(rtz + ((M + kResSpread + 3) & ~3));
   __shared__ int s_namb, s_last;
-  __shared__ __attribute__((aligned(16))) uint16_t fwb[kMaxStreams * kScIters * kScT];
-  __shared__ uint16_t acond[kScIters][kScT];
+  // the plateau step's word copy and conditions alias the ring (dead after the iterations)
+  uint16_t *fwb = reinterpret_cast<uint16_t *>(sc_dyn);
+  uint16_t(*acond)[kScT] = reinterpret_cast<uint16_t(*)[kScT]>(fwb + kMaxStreams * kScIters * kScT);
   __shared__ long long run_ws[2][kScT / 64];
   __shared__ long long flo[kMaxStreams];
   __shared__ unsigned long long s_min;
@@ -1738,7 +1743,7 @@ void sc_exact_kernel(ScArgs a) {
           if (i >= RL) {
             const float2 dv = ring[ring_pad(ring_slot(q0 + i - RL, w0, M, RING))];
             const float2 pp = cj_mul(dv, vv);
-            rtp[i] = make_float2((-1.0f) * pp.x, (-1.0f) * pp.y);
+            rtp[i - RL] = make_float2((-1.0f) * pp.x, (-1.0f) * pp.y);
           }
         }
         __syncthreads();
@@ -1749,7 +1754,7 @@ void sc_exact_kernel(ScArgs a) {
             if (tid < kLocAmb) {
               s_rv[g][0] = seq_sum(rtz + r, M);
             } else {
-              const float2 P = seq_sum2(rtp + r + RL, RL);
+              const float2 P = seq_sum2(rtp + r, RL);
               s_rv[g][1] = P.x;
               s_rv[g][2] = P.y;
             }
@@ -1924,7 +1929,7 @@ void launch_sc_screen(const ScreenArgs &a, uint32_t n_frames, hipStream_t s) {
 void launch_sc_exact(const ScArgs &a, hipStream_t s) {
   const size_t shm = sc_table_bytes(a.M) +
                      sizeof(float) * (size_t)((a.M + kResSpread + 3) & ~3u) +
-                     sizeof(float2) * (size_t)(a.M + kResSpread);
+                     sizeof(float2) * (size_t)(a.M / 2 + kResSpread);
   static size_t set_shm[2] = {0, 0};
   const int v = a.sc16 ? 1 : 0;
   auto kern = a.sc16 ? sc_exact_kernel<true> : sc_exact_kernel<false>;

@@ -186,6 +186,12 @@ class Receiver:
                 osym = None if out_sym is None else _ptr(out_sym) + sl * slot_sym
                 oidx = None if out_idx is None else _ptr(out_idx) + sl * slot_idx
                 scratch = None
+                if rem == 1 and ref_mode == 1 and rs is None and refp is not None:
+                    # the scratch second slot reads reference row refp + 1, one past the last
+                    # capture's rows: give it a two-row copy
+                    ref2 = torch.zeros(2 * slot_idx, dtype=torch.uint8, device="cuda")
+                    _lib.memcpy_d2d(ref2.data_ptr(), refp, slot_idx)
+                    refp = ref2.data_ptr()
                 if rem == 1 and (osym or oidx):
                     scratch = torch.empty(2 * (slot_sym + slot_idx), dtype=torch.uint8,
                                           device="cuda")
@@ -265,6 +271,12 @@ class Receiver:
     def sc_exact_count(self):
         v = C.c_uint64()
         check(lib().mimo_rx_get_sc_exact_count(self._h, C.byref(v)), "sc_exact_count")
+        return v.value
+
+    def decode_path(self):
+        """Kernel family of the last decode launch (_lib.DECODE_STREAM / _SPLIT / _SYMBOL)."""
+        v = C.c_int32()
+        check(lib().mimo_rx_get_decode_path(self._h, C.byref(v)), "decode_path")
         return v.value
 
     def stage_times(self):

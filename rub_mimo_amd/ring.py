@@ -43,9 +43,12 @@ class CaptureRing:
         except Exception:
             pass
 
-    def bind(self, capture, stride=None, capacity=None):
+    def bind(self, capture, stride=None, capacity=None, after_stream=None):
         """Target of the following commits: a device sc16 capture. `capture` is a torch int16
-        tensor [n_ant][stride][2] (or a raw device pointer with stride/capacity given)."""
+        tensor [n_ant][stride][2] (or a raw device pointer with stride/capacity given).
+        after_stream (a hipStream_t handle, e.g. torch.cuda.current_stream().cuda_stream):
+        the uploads into this capture wait for the work enqueued there so far (a batch still
+        reading the capture); without it the caller synchronises before rebinding."""
         if hasattr(capture, "data_ptr"):
             ptr = capture.data_ptr()
             if stride is None:
@@ -54,7 +57,12 @@ class CaptureRing:
             ptr = int(capture)
         if capacity is None:
             capacity = stride
-        check(lib().mimo_ring_bind(self._h, C.c_void_p(ptr), stride, capacity), "mimo_ring_bind")
+        if after_stream is not None:
+            check(lib().mimo_ring_bind_after(self._h, C.c_void_p(ptr), stride, capacity,
+                                             C.c_void_p(after_stream)), "mimo_ring_bind_after")
+        else:
+            check(lib().mimo_ring_bind(self._h, C.c_void_p(ptr), stride, capacity),
+                  "mimo_ring_bind")
 
     def acquire(self):
         """The next chunk: one numpy int16 view [chunk_samples][2] of pinned memory per

@@ -103,6 +103,35 @@ def test_chunked_execute_equals_one_shot(path):
     assert evm_delta(np.stack(got), g["symbols"]) <= SYM_TOL
 
 
+def test_batch_then_reset_then_chunked_execute_on_one_handle():
+    """One handle runs a batch of 8 captures (its S&C records grow to F = 8 rows), then
+    reset(), then the chunked streaming execute: the streaming path keeps only frame 0's
+    records across record growth (engine.cpp ensure_workspace), so its results still equal
+    the golden fixture."""
+    import ctypes as C
+    g = load([p for p in GOLDEN if "m64_2x2_zf2" in p][0])
+    rx = g["rx"]
+    fs, got = gpu_framesync(g)
+    F = 8
+    buf, L = _upload_batch([rx] * F)
+    b = _lib.Batch(buf.addr, L, rx.shape[1], F, int(g["pid"]), None, None, 0, None, 0, 0, 1,
+                   0, None, 0, 1.0)
+    _lib.check(_lib.lib().mimo_rx_process_batch(fs._h, C.byref(b), None), "process_batch")
+    res = (_lib.FrameResult * F)()
+    _lib.check(_lib.lib().mimo_rx_batch_results(fs._h, res, F), "batch_results")
+    assert all(r.status == _lib.FRAME_OK and r.sync_index == int(g["sync_index"]) for r in res)
+    fs.reset()
+    got.clear()
+    pos = 0
+    rng = np.random.default_rng(11)
+    while pos < rx.shape[1]:
+        c = int(rng.integers(1, 2500))
+        fs.execute([r[pos:pos + c] for r in rx], min(c, rx.shape[1] - pos))
+        pos += c
+    assert_sync_equal(fs, g)
+    assert evm_delta(np.stack(got), g["symbols"]) <= SYM_TOL
+
+
 def test_incomplete_then_complete_and_mimo_semantics():
     g = load([p for p in GOLDEN if "m64_2x2_zf2" in p][0])
     M, cp, N, nac, pid = (int(g[k]) for k in ("M", "cp", "N", "nac", "pid"))
@@ -284,6 +313,35 @@ def test_repeated_batch_graph_replay_is_identical():
     assert [(r["status"], r["sync_index"]) for r in res2] == [t[:2] for t in outs[0][2][:F - 1]]
 
 
+def test_alternating_capture_buffers_replay_their_own_graphs():
+    """Double-buffered ingest alternates two capture buffers: each batch key keeps its own
+    captured graph (a small cache in engine.cpp), and every replay equals the direct launch
+    of the same buffer."""
+    import torch
+    M, cp, N, nac, pid, F = 256, 19, 4, 4, 24, 2
+    sp = SynthParams(M=M, cp_len=cp, num_streams=N, num_access_codes=nac, pid=pid,
+                     qam_order=16, seed=15, snr_db=30.0)
+    syn = Synthesizer(sp)
+    L = sp.max_frame_len()
+    bufs = [torch.empty((F, N, L), dtype=torch.complex64, device="cuda") for _ in range(2)]
+    syn.generate(bufs[0], L, L, F, frame_id0=0)
+    syn.generate(bufs[1], L, L, F, frame_id0=F)
+    rx = Receiver(RxParams(M=M, cp_len=cp, num_streams=N, num_access_codes=nac, pid_max=pid,
+                           detector=_lib.DET_MMSE, qam_order=16))
+    sym = torch.zeros((F, N, pid, M), dtype=torch.complex64, device="cuda")
+    seen = {0: [], 1: []}
+    for it in range(8):             # direct, direct, capture, capture, replays
+        k = it % 2
+        sym.zero_()
+        rx.process(bufs[k], L, L, F, max_out=pid, out_sym=sym, ref_mode=0)
+        torch.cuda.synchronize()
+        seen[k].append((sym.clone(), [(r["status"], r["sync_index"]) for r in rx.results()]))
+    for k in (0, 1):
+        for o in seen[k][1:]:
+            assert torch.equal(o[0], seen[k][0][0]) and o[1] == seen[k][0][1]
+    assert not torch.equal(seen[0][0][0], seen[1][0][0])
+
+
 def test_gpu_synth_matches_oracle_synth():
     M, cp, N, nac, pid, qam = 128, 16, 4, 3, 5, 64
     S = Synthesizer(SynthParams(M=M, cp_len=cp, num_streams=N, num_access_codes=nac, pid=pid,
@@ -329,7 +387,7 @@ def test_framegen_matches_oracle_tx():
 
 
 def _c_frame_parity(M, cp, N, nac, pid, qam, det, snr, seed, bias=True, max_delta=SYM_TOL,
-                    search_mode=0):
+                    search_mode=0, path=None, out_idx=False):
     S = Synthesizer(SynthParams(M=M, cp_len=cp, num_streams=N, num_access_codes=nac, pid=pid,
                                 qam_order=qam, seed=seed, snr_db=snr))
     L = S.frame_len(0)
@@ -342,9 +400,12 @@ def _c_frame_parity(M, cp, N, nac, pid, qam, det, snr, seed, bias=True, max_delt
                  detector=det, keep_identity_bias=bias, qam_order=qam)
     rxo = Receiver(P)
     osym = _lib.DeviceBuffer(N * pid * M * 8)
-    rxo.process(out, L, L, 1, max_out=pid, out_sym=osym, ref_mode=2, ref_seed=seed,
-                frame_id0=0)
+    oidx = _lib.DeviceBuffer(N * pid * M) if out_idx else None
+    rxo.process(out, L, L, 1, max_out=pid, out_sym=osym, out_idx=oidx, ref_mode=2,
+                ref_seed=seed, frame_id0=0)
     r = rxo.results()[0]
+    if path is not None:                 # the decode kernel family this geometry must take
+        assert rxo.decode_path() == path, (rxo.decode_path(), path)
     ci, si = rxo.corr()
     o = ref.FrameSyncRef(M, cp, N, nac, pid_max=pid, detector=det, keep_identity_bias=bias,
                          trace_corr=True, search_mode=search_mode)
@@ -367,10 +428,22 @@ def _c_frame_parity(M, cp, N, nac, pid, qam, det, snr, seed, bias=True, max_delt
     ours = osym.download(np.complex64, N * pid * M).reshape(N, pid, M).transpose(1, 0, 2)
     d = evm_delta(ours, syms_o)
     assert d <= max_delta, d
-    _, num, den, err = ref.demap_evm(syms_o, qam, txi)
+    dec_o, num, den, err = ref.demap_evm(syms_o, qam, txi)
     edb_gpu = 10 * np.log10(r["evm_num"] / r["evm_den"])
     edb_ref = 10 * np.log10(num / den)
     assert np.abs(edb_gpu - edb_ref).max() <= EVM_DB_TOL, (edb_gpu, edb_ref)
+    if out_idx:
+        # hard decisions equal the oracle's except where its symbol sits within 1e-3 of a
+        # decision boundary; the symbol-error counts likewise
+        got = oidx.download(np.uint8, N * pid * M).reshape(N, pid, M)
+        mism = got != dec_o
+        if mism.any():
+            y = syms_o.transpose(1, 0, 2)[mism]
+            Lq = int(np.sqrt(qam))
+            sc = np.sqrt(2 * (Lq * Lq - 1) / 3.0)
+            v = np.concatenate([(y.real * sc + Lq) / 2, (y.imag * sc + Lq) / 2])
+            assert np.min(np.abs(v - np.round(v))) < 1e-3
+        assert np.abs(r["errors"] - err.astype(np.int64)).max() <= int(mism.sum())
     return d, edb_gpu
 
 
@@ -387,13 +460,33 @@ def test_c2_2x2_zf_1024_16qam_full_frame():
 
 def test_c3_4x4_mmse_2048_64qam_full_frame():
     """BASELINE config C3 at full size (PID 1000): the oracle needs ~20 s of CPU."""
-    d, e = _c_frame_parity(2048, 152, 4, 20, 1000, 64, _lib.DET_MMSE, 30.0, seed=31)
+    d, e = _c_frame_parity(2048, 152, 4, 20, 1000, 64, _lib.DET_MMSE, 30.0, seed=31,
+                           path=_lib.DECODE_STREAM, out_idx=True)
     assert np.median(e) < -20
 
 
 def test_c4_8x8_mmse_4096_256qam_reduced_codes():
-    """C4 geometry with 2 access codes so the brute-force oracle stays within ~30 s."""
-    _c_frame_parity(4096, 304, 8, 2, 12, 256, _lib.DET_MMSE, 35.0, seed=41, bias=False)
+    """C4 geometry with 2 access codes so the brute-force oracle stays within ~30 s. PID 12 is
+    below M/64, so this takes the per-symbol decode_kernel<12, 8>."""
+    _c_frame_parity(4096, 304, 8, 2, 12, 256, _lib.DET_MMSE, 35.0, seed=41, bias=False,
+                    path=_lib.DECODE_SYMBOL)
+
+
+def test_c4_split_decode_matches_oracle():
+    """The production C4 decode: with max_out >= M/64 the 8x8 frame takes the split form
+    (spectra_kernel<12> writes every symbol's spectra, apply_split_kernel<8> applies W, demaps
+    and sums EVM per 64-subcarrier chunk; decode_stream.hip). PID 66 (not a multiple of the
+    apply's four symbols in flight, symbol ranges of 16/17) against the brute-force oracle
+    with 2 access codes: symbols within the EVM tolerance, indices, errors and EVM-dB."""
+    _c_frame_parity(4096, 304, 8, 2, 66, 256, _lib.DET_MMSE, 35.0, seed=48, bias=False,
+                    path=_lib.DECODE_SPLIT, out_idx=True)
+
+
+@pytest.mark.parametrize("det", [_lib.DET_ZF, _lib.DET_MMSE])
+def test_split_decode_m512_matches_oracle(det):
+    """spectra_kernel<9> + apply_split_kernel<8>: 8x8 at M = 512 with PID >= M/64."""
+    _c_frame_parity(512, 38, 8, 2, 21, 64, det, 35.0, seed=91 + det, bias=False,
+                    path=_lib.DECODE_SPLIT, out_idx=True)
 
 
 def test_two_phase_screen_finds_late_frames():
@@ -459,7 +552,7 @@ def test_c4_full_codes_against_parseval_oracle():
 def test_row_solve_8x8_matches_oracle(det):
     """8 streams take the 8-lane row solve (weights_row_kernel): reduced 8x8 frames checked
     against the oracle's Gauss-Jordan, symbols within the EVM tolerance."""
-    _c_frame_parity(256, 32, 8, 2, 12, 16, det, 35.0, seed=68 + det)
+    _c_frame_parity(256, 32, 8, 2, 12, 16, det, 35.0, seed=68 + det, path=_lib.DECODE_SYMBOL)
 
 
 def test_c4_batched_full_size_properties():
@@ -668,6 +761,19 @@ def test_cfo_batch_corrects_rotated_c3_frames(eps_true):
         assert e3 - e0 <= 0.5, (f, e0, e3)
         print("cfo frame %d: plain %.3f dB, corrected %.3f dB, raw %.3f dB" % (f, e0, e3, e2))
         assert e2 > e0 + 10.0, (f, e0, e2)
+
+
+def test_cfo_with_back_to_back_frames_is_refused():
+    """The opt-in CFO stages derotate each frame's window into a per-capture scratch, where
+    back-to-back frames' windows would overlap: frames_per_capture > 1 is refused loudly."""
+    import torch
+    M, cp, N, nac, pid = 256, 19, 2, 4, 16
+    rxo = Receiver(RxParams(M=M, cp_len=cp, num_streams=N, num_access_codes=nac, pid_max=pid,
+                            detector=_lib.DET_ZF2, qam_order=16, cfo_correct=True))
+    L = 40 * (M + cp)
+    iq = torch.zeros((1, N, L), dtype=torch.complex64, device="cuda")
+    with pytest.raises(_lib.MimoError, match="frames_per_capture"):
+        rxo.process(iq, L, L, 1, max_out=pid, frames_per_capture=2)
 
 
 def _sc16_capture(iq, amax):

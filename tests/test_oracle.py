@@ -359,3 +359,25 @@ def test_stream_numpy_model_agrees():
                             detector="zf2")
     assert [o for o, _ in out] == list(g["origin"])
     assert [d["sync_index"] for _, d in out] == list(g["sync_index"])
+
+
+def test_oracle_under_asan_ubsan():
+    """the CPU oracle (oracle/mimo_ref.c) built with AddressSanitizer and
+    UndefinedBehaviorSanitizer (oracle/Makefile target `sanitize`) and driven end to end by
+    oracle/sanitize_check.c -- synthesiser, chunked framesync (brute-force and Parseval search,
+    every detector, S&C and search traces), skip-to-sync, framegen, demap/EVM -- reports
+    nothing and exits 0."""
+    import shutil
+    import subprocess
+    if shutil.which("gcc") is None:
+        pytest.skip("gcc not available")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    subprocess.check_call(["make", "-s", "-C", os.path.join(root, "oracle"), "sanitize"])
+    # (verify_asan_link_order=0: a preloaded library of the environment may precede ASan)
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:verify_asan_link_order=0",
+               UBSAN_OPTIONS="print_stacktrace=1")
+    p = subprocess.run([os.path.join(root, "oracle", "_build", "sanitize_check")],
+                       capture_output=True, text=True, env=env, timeout=300)
+    assert p.returncode == 0, p.stderr[-4000:]
+    assert "runtime error" not in p.stderr and "AddressSanitizer" not in p.stderr, p.stderr
+    assert "sanitize_check OK" in p.stdout
