@@ -204,6 +204,11 @@ int mimo_rx_get_sc_exact_count(mimo_rx *h, uint64_t *out);
 enum { MIMO_DECODE_NONE = 0, MIMO_DECODE_STREAM = 1, MIMO_DECODE_SPLIT = 2,
        MIMO_DECODE_SYMBOL = 3 };
 int mimo_rx_get_decode_path(const mimo_rx *h, int32_t *path);
+/* streaming execute: the device capture's capacity and the samples it holds per antenna
+ * (diagnostic). While seeking, only the samples a later trigger can still reach are kept
+ * (the reference's bounded window ring, framing.cc:387-388), so the capture stays near the
+ * window size however long an unsynchronised stream runs. */
+int mimo_rx_get_stream_capacity(const mimo_rx *h, uint64_t *capacity, uint64_t *held);
 
 /* ---------------- transmitter: framegen (framing.h:42-103) ---------------- */
 typedef struct mimo_tx mimo_tx;

@@ -102,7 +102,8 @@ __global__ __launch_bounds__(kCfoThreads) void cfo_batch_est_kernel(CfoBatchArgs
   const bool live = STAGE == 1 ? cfo_live(I) : I.status == 0;
   double re = 0.0, im = 0.0;
   const int64_t L = (int64_t)a.frame_len;
-  const float2 *src = STAGE == 1 ? a.iq : a.out;
+  // folded path: no scratch, stage 2 reads the raw samples (below)
+  const float2 *src = (STAGE == 1 || a.fold) ? a.iq : a.out;
   if (live) {
     for (uint32_t r = 0; r < a.N; r++) {
       const float2 *row = src + ((uint64_t)I.cap * a.N + r) * a.stride;
@@ -143,9 +144,21 @@ __global__ __launch_bounds__(kCfoThreads) void cfo_batch_est_kernel(CfoBatchArgs
     __syncthreads();
   }
   if (threadIdx.x == 0) {
+    double re0 = sre[0], im0 = sim[0];
+    if (STAGE == 2 && a.fold && live) {
+      // on the raw samples conj(x[k]) x[k + M] lacks the stage-1 derotation's constant factor
+      // exp(-j 2 pi eps0): applied to the block's partial (the sum is linear in it)
+      double ph = -2.0 * cfo_stage_eps(a.part, f, 1);   // units of pi
+      ph -= 2.0 * rint(ph * 0.5);
+      double sn, cs;
+      sincospi(ph, &sn, &cs);
+      const double r2 = re0 * cs - im0 * sn, i2 = re0 * sn + im0 * cs;
+      re0 = r2;
+      im0 = i2;
+    }
     double *p = a.part + (((uint64_t)f * 2 + (STAGE - 1)) * kCfoBlocks + b) * 2;
-    p[0] = sre[0];
-    p[1] = sim[0];
+    p[0] = re0;
+    p[1] = im0;
   }
 }
 
@@ -190,7 +203,7 @@ void launch_cfo_batch(const CfoBatchArgs &a, uint32_t n_frames, int stage, hipSt
       (uint32_t)std::min<uint64_t>((a.len + kCfoThreads - 1) / kCfoThreads, 2048);
   if (stage == 1) {
     cfo_batch_est_kernel<1><<<dim3(kCfoBlocks, n_frames), kCfoThreads, 0, s>>>(a);
-    cfo_batch_rot_kernel<1><<<dim3(blocks, a.N, n_frames), kCfoThreads, 0, s>>>(a);
+    if (!a.fold) cfo_batch_rot_kernel<1><<<dim3(blocks, a.N, n_frames), kCfoThreads, 0, s>>>(a);
   } else {
     cfo_batch_est_kernel<2><<<dim3(kCfoBlocks, n_frames), kCfoThreads, 0, s>>>(a);
     if (a.rot_window)

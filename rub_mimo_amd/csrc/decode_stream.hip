@@ -187,6 +187,12 @@ MIMO_DEV void wave_passes(v2f *buf, v2f *v, const v2f *twl, uint32_t s) {
   }
 }
 
+// a wave-uniform complex value held in SGPRs
+MIMO_DEV v2f uni(v2f v) {
+  return v2f{__int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v.x))),
+             __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v.y)))};
+}
+
 MIMO_DEV uint32_t cvt_u32_sat(float x) {   // v_cvt_u32_f32: NaN and negatives -> 0, saturating
   uint32_t r;
   asm("v_cvt_u32_f32 %0, %1" : "=v"(r) : "v"(x));
@@ -525,7 +531,37 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
 
   v2f rot = v2f{1.0f, 0.0f};                          // CPE: current phase correction
   bool cpe_valid = false;                             // cpe_part holds this frame's last symbol
+  // folded CFO (a.cpe == 2): the frame's estimate nu = (eps0 + delta) / M cycles per sample
+  // about its window base, split into the part inside a symbol body (time domain, before the
+  // transform: sample j of the body turns by exp(-j 2 pi nu j), the thread's j = t0 % W8 + r W8)
+  // and the body start's phase (a constant per symbol, applied to the outputs with the CPE
+  // rotation) -- the derotation the scratch passes of the unfolded path applied
+  // (the body start's phasor rides in rot: set at each frame segment's first symbol, advanced
+  // by cfo_e per symbol, corrected by the CPE as before)
+  v2f cfo_ct = v2f{1.0f, 0.0f}, cfo_w = v2f{1.0f, 0.0f};   // exp(-j2pi nu t0%W8), exp(-j2pi nu W8)
+  v2f cfo_e = v2f{1.0f, 0.0f};                              // exp(-j2pi nu SL)
+  auto cfo_frame = [&](uint32_t ff, uint32_t ss) {
+    if constexpr (CPE) {
+      if (a.cpe == 2) {
+        // (eps0 + delta, written by ls_combine_q_kernel; phases reduced in fp64, then fp32)
+        const FrameInfo &J = a.info[ff];
+        const double nu = (double)J.cfo_eps / (double)M;
+        auto ph = [](double cyc) {
+          double p = -2.0 * cyc;
+          p -= 2.0 * rint(p * 0.5);
+          float sn, cs;
+          sincospif((float)p, &sn, &cs);
+          return v2f{cs, sn};
+        };
+        cfo_ct = ph(nu * (double)(opq(tid) % W8));
+        cfo_w = uni(ph(nu * (double)W8));
+        cfo_e = uni(ph(nu * (double)a.SL));
+        rot = uni(ph(nu * (double)((int64_t)J.i0 + a.cp + (int64_t)ss * a.SL)));
+      }
+    }
+  };
   load_w(f);
+  cfo_frame(f, s);
   uint32_t odd = fetch(f, s);
   // the first symbol's staging (issued after the weight loads: the counted wait in the loop
   // assumes only stores behind the DMA)
@@ -585,6 +621,16 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
             const int e = t * S + q;
             cref[e / 4] |= (uint32_t)rstg[t * M + t0 + q * T] << (8 * (e % 4));
           }
+      }
+    }
+    if constexpr (CPE) {
+      if (a.cpe == 2) {   // folded CFO: the in-body part of the derotation
+        v2f c = cfo_ct;
+#pragma unroll
+        for (int r = 0; r < 8; r++) {
+          v[r] = cmul_pk(v[r], c);
+          c = cmul_pk(c, cfo_w);
+        }
       }
     }
     MARK(";@@B pass0");
@@ -753,6 +799,8 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
     }
     MARK(";@@F tail");
     const bool last = (i + 1 == i_end);
+    if constexpr (CPE)
+      if (a.cpe == 2) rot = uni(cmul_pk(rot, cfo_e));   // the next symbol's body start
     if (last || fn != f) {
       if constexpr (CPE) {
         rot = v2f{1.0f, 0.0f};
@@ -762,6 +810,7 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
       if (!last) {
         n_out_f = n_out_n;
         load_w(fn);
+        cfo_frame(fn, sn);
       }
     }
     MARK(";@@G next");
@@ -781,40 +830,44 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
 //      its 64 subcarriers in registers (wave h: outputs 2h and 2h+1, 32 VGPRs) and streams
 //      the range's symbols through the 8x8 apply, demap, EVM and stores.
 // Weights are read once per (chunk, range) instead of once per symbol (the per-symbol kernel
-// reads 2 MB of W from L2 for every 256 KB symbol); the spectra make one extra HBM round
-// trip (2 x 256 KB per symbol). EVM records: chunk x range per frame (nrec), NA/2 per record.
+// reads 2 MB of W from L2 for every 256 KB symbol). The two kernels alternate over groups of
+// kSplitGroup symbols (a.sym0 .. + a.sym_cap) through one scratch of that many symbols per
+// frame (67 MB at C4 x 8): the spectra a group writes are read back by its apply while they
+// are still in the 256 MB Infinity Cache, and the next group overwrites the same lines, so
+// the round trip need not reach HBM. EVM records: symbol group x chunk x range per frame
+// (nrec), NA/2 per record.
 constexpr uint32_t kSplitSets = 16;   // EVM partial sets per record (<= kMaxEvmParts)
 
-template <int LOG2M, int T>
+template <int LOG2M, int T, bool SC16>
 __global__ __launch_bounds__(T) void spectra_kernel(DecodeArgs a) {
   constexpr int M = 1 << LOG2M, NCH = M / 64;
   extern __shared__ __attribute__((aligned(16))) float2 lds_sp[];
-  const uint32_t f = blockIdx.y, s = blockIdx.x, r = blockIdx.z;
+  const uint32_t f = blockIdx.y, sl = blockIdx.x, r = blockIdx.z;
+  const uint32_t s = a.sym0 + sl;                     // symbol; sl its scratch slot
   const FrameInfo &I = a.info[f];
   const uint32_t n_out = (I.status == 0) ? min(I.n_sym, a.max_out) : 0u;
   if (s >= n_out) return;                             // uniform
   const int64_t abs0 = I.base + (int64_t)I.i0 + (int64_t)s * a.SL + a.cp;
   const int64_t L = (int64_t)a.frame_len;
-  const float2 *x = a.iq + ((uint64_t)I.cap * a.N + r) * a.stride;
+  const auto xs = iq_row<SC16>(a.iq, a.iq_scale, ((uint64_t)I.cap * a.N + r) * a.stride);
   const int tid = threadIdx.x;
-  if (abs0 >= 0 && abs0 + M <= L && ((uintptr_t)(x + abs0) & 15u) == 0) {
-    const float4 *x4 = reinterpret_cast<const float4 *>(x + abs0);
+  if (abs0 >= 0 && abs0 + M <= L && xs.pair_ok() && (abs0 & 1) == 0) {
 #pragma unroll
     for (int i = tid; i < M / 2; i += T) {
-      const float4 v = x4[i];
+      const float4 v = xs.pair(abs0 + 2 * i);
       lds_sp[lds_pad(2 * i)] = make_float2(v.x, v.y);
       lds_sp[lds_pad(2 * i + 1)] = make_float2(v.z, v.w);
     }
   } else {
     for (int i = tid; i < M; i += T) {
       const int64_t n = abs0 + i;
-      lds_sp[lds_pad(i)] = (n >= 0 && n < L) ? x[n] : make_float2(0.0f, 0.0f);
+      lds_sp[lds_pad(i)] = (n >= 0 && n < L) ? xs.at(n) : make_float2(0.0f, 0.0f);
     }
   }
   __syncthreads();
   fft_lds<LOG2M, T, 1, false>(lds_sp, a.tw);
-  float2 *o = a.spec + (((uint64_t)f * NCH * a.max_out + s) * a.N + r) * 64;
-  const uint64_t cstep = (uint64_t)a.max_out * a.N * 64;
+  float2 *o = a.spec + (((uint64_t)f * NCH * a.sym_cap + sl) * a.N + r) * 64;
+  const uint64_t cstep = (uint64_t)a.sym_cap * a.N * 64;
 #pragma unroll
   for (int k = tid; k < M; k += T) o[(uint64_t)(k >> 6) * cstep + (k & 63)] = lds_sp[lds_pad(k)];
 }
@@ -837,9 +890,13 @@ __global__ __launch_bounds__(32 * NA) void apply_split_kernel(DecodeArgs a) {
   }
   const FrameInfo &I = a.info[f];
   const uint32_t n_out = (I.status == 0) ? min(I.n_sym, a.max_out) : 0u;
-  if (c == 0 && part == 0 && tid == 0) a.nrec[f] = NCH * P * (T / 64) / kSplitSets;
-  const uint32_t s0 = (uint32_t)((uint64_t)n_out * part / P);
-  const uint32_t s1 = (uint32_t)((uint64_t)n_out * (part + 1) / P);
+  const uint32_t grp = a.sym0 / a.sym_cap;            // this launch's symbol group
+  if (grp == 0 && c == 0 && part == 0 && tid == 0)
+    a.nrec[f] = a.sym_groups * NCH * P * (T / 64) / kSplitSets;
+  // the group's symbols of this frame, split in P ranges
+  const uint32_t ng = n_out > a.sym0 ? min(n_out - a.sym0, a.sym_cap) : 0u;
+  const uint32_t s0 = a.sym0 + (uint32_t)((uint64_t)ng * part / P);
+  const uint32_t s1 = a.sym0 + (uint32_t)((uint64_t)ng * (part + 1) / P);
   const uint32_t M = a.M, k = c * 64 + lane;
   v2f Wr[2][NA];
   {
@@ -856,10 +913,10 @@ __global__ __launch_bounds__(32 * NA) void apply_split_kernel(DecodeArgs a) {
   const v2f Lf = v2f{(float)a.qam.L, (float)a.qam.L};
   const uint32_t Lm1 = a.qam.L - 1;
   const uint64_t frame_id = a.frame_id0 + I.ref;
-  // symbol s of this chunk: 4 KB at spec4 + s * 256 (16 B per thread), reference indices of
-  // stream t at ref + (t * max_out + s) * M_occ (16 B per thread for tid < 32)
+  // symbol s of this chunk: 4 KB at spec4 + (s - sym0) * 256 (16 B per thread), reference
+  // indices of stream t at ref + (t * max_out + s) * M_occ (16 B per thread for tid < 32)
   const float4 *spec4 = reinterpret_cast<const float4 *>(a.spec) +
-                        ((uint64_t)f * NCH + c) * a.max_out * (NA * 64 / 2) + tid;
+                        ((uint64_t)f * NCH + c) * a.sym_cap * (NA * 64 / 2) + tid;
   const uint8_t *refb = (REF == 1) ? a.ref_idx + ((uint64_t)I.ref * NA + (tid >> 2)) * a.max_out * a.M_occ +
                                          c * 64 + (tid & 3) * 16
                                    : nullptr;
@@ -870,7 +927,7 @@ __global__ __launch_bounds__(32 * NA) void apply_split_kernel(DecodeArgs a) {
   uint4 pr0, pr1, pr2, pr3;
   auto load_sym = [&](float4 &x, uint4 &r, uint32_t s) {
     const uint32_t sc = min(s, slast);
-    x = spec4[(uint64_t)sc * (NA * 64 / 2)];
+    x = spec4[(uint64_t)(sc - a.sym0) * (NA * 64 / 2)];
     if constexpr (REF == 1)
       if (tid < 32) r = *reinterpret_cast<const uint4 *>(refb + (uint64_t)sc * a.M_occ);
   };
@@ -931,8 +988,8 @@ __global__ __launch_bounds__(32 * NA) void apply_split_kernel(DecodeArgs a) {
       e_num[tt] += __shfl_xor(e_num[tt], off);
       e_den[tt] += __shfl_xor(e_den[tt], off);
     }
-  // partial set (c * P + part) * waves + h: this wave's two streams, zeros elsewhere
-  const uint64_t set = ((uint64_t)c * P + part) * (T / 64) + h;
+  // partial set ((grp * NCH + c) * P + part) * waves + h: this wave's two streams, zeros elsewhere
+  const uint64_t set = (((uint64_t)grp * NCH + c) * P + part) * (T / 64) + h;
   double *ep = a.evm_part + ((uint64_t)f * a.max_out * kSplitSets + set) * NA * 3;
   if (lane < NA * 3) {
     const uint32_t t = lane / 3, comp = lane % 3;
@@ -944,30 +1001,53 @@ __global__ __launch_bounds__(32 * NA) void apply_split_kernel(DecodeArgs a) {
   }
 }
 
+bool decode_split_accepts(const DecodeArgs &a, int log2M) {
+  // (the apply reads 16 bytes of reference indices per lane)
+  return a.N == 8 && a.detector != 3 && a.all_occ && log2M >= 9 && log2M <= 12 &&
+         a.max_out >= (1u << log2M) / 64 && a.qam.L * a.qam.L <= kStreamMaxQam &&
+         (a.ref_mode != 1 || ((uintptr_t)a.ref_idx & 15u) == 0);
+}
+
+uint32_t split_group_symbols(uint32_t max_out) { return std::min(kSplitGroup, max_out); }
+
 // 8x8 split decode; returns the partial sets per record (0: not handled)
 uint32_t launch_decode_split(const DecodeArgs &a, int log2M, uint32_t n_frames, hipStream_t s) {
-  if (!a.spec || !a.nrec || a.sc16 || a.N != 8 || a.detector == 3 || !a.all_occ ||
-      log2M < 9 || log2M > 12 || a.qam.L * a.qam.L > kStreamMaxQam)
-    return 0;
+  if (!a.spec || !a.nrec || !decode_split_accepts(a, log2M)) return 0;
   const uint32_t NCH = a.M / 64;
-  // symbol ranges per chunk: many short workgroups (no tail round), records
-  // NCH * P * 4 / kSplitSets <= max_out, whole records
-  uint32_t P = std::min<uint32_t>(16, a.max_out * kSplitSets / (NCH * 4));
-  while (P > 0 && (NCH * P * 4) % kSplitSets) P--;
+  const uint32_t cap = split_group_symbols(a.max_out);
+  const uint32_t groups = (a.max_out + cap - 1) / cap;
+  // symbol ranges per (group, chunk): many short workgroups (no tail round); records
+  // groups * NCH * P * 4 / kSplitSets <= max_out (the EVM partial space), whole records
+  uint32_t P = 16;
+  while (P > 0 && ((uint64_t)groups * NCH * P * 4 > (uint64_t)a.max_out * kSplitSets ||
+                   (groups * NCH * P * 4) % kSplitSets))
+    P--;
   if (P == 0) return 0;
   constexpr int T1 = 512;
   const size_t shm = sizeof(float2) * lds_padded_len(1 << log2M);
-  const dim3 g1(a.max_out, n_frames, a.N);
-  switch (log2M) {
-    case 9: hipLaunchKernelGGL((spectra_kernel<9, T1>), g1, dim3(T1), shm, s, a); break;
-    case 10: hipLaunchKernelGGL((spectra_kernel<10, T1>), g1, dim3(T1), shm, s, a); break;
-    case 11: hipLaunchKernelGGL((spectra_kernel<11, T1>), g1, dim3(T1), shm, s, a); break;
-    default: hipLaunchKernelGGL((spectra_kernel<12, T1>), g1, dim3(T1), shm, s, a); break;
-  }
+  DecodeArgs g = a;
+  g.sym_cap = cap;
+  g.sym_groups = groups;
   const dim3 g2(NCH, n_frames, P);
-  if (a.ref_mode == 1) hipLaunchKernelGGL((apply_split_kernel<8, 1>), g2, dim3(256), 0, s, a);
-  else if (a.ref_mode == 2) hipLaunchKernelGGL((apply_split_kernel<8, 2>), g2, dim3(256), 0, s, a);
-  else hipLaunchKernelGGL((apply_split_kernel<8, 0>), g2, dim3(256), 0, s, a);
+  for (uint32_t k = 0; k < groups; k++) {
+    g.sym0 = k * cap;
+    const dim3 g1(std::min(cap, a.max_out - g.sym0), n_frames, a.N);
+#define SPECTRA(L2)                                                                      \
+  do {                                                                                   \
+    if (a.sc16) hipLaunchKernelGGL((spectra_kernel<L2, T1, true>), g1, dim3(T1), shm, s, g); \
+    else hipLaunchKernelGGL((spectra_kernel<L2, T1, false>), g1, dim3(T1), shm, s, g);       \
+  } while (0)
+    switch (log2M) {
+      case 9: SPECTRA(9); break;
+      case 10: SPECTRA(10); break;
+      case 11: SPECTRA(11); break;
+      default: SPECTRA(12); break;
+    }
+#undef SPECTRA
+    if (a.ref_mode == 1) hipLaunchKernelGGL((apply_split_kernel<8, 1>), g2, dim3(256), 0, s, g);
+    else if (a.ref_mode == 2) hipLaunchKernelGGL((apply_split_kernel<8, 2>), g2, dim3(256), 0, s, g);
+    else hipLaunchKernelGGL((apply_split_kernel<8, 0>), g2, dim3(256), 0, s, g);
+  }
   return kSplitSets;
 }
 

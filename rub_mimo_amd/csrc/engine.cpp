@@ -143,6 +143,7 @@ struct StageTimer {
 struct Codes {
   DevBuf<float2> code_time;   // [n_slots][M]
   DevBuf<float2> codespec;    // [n_slots][F]
+  DevBuf<float2> codespec_w;  // [n_slots][F], the wave-local search's bin order
 };
 
 int build_codes(Codes &c, uint32_t M, uint32_t N, uint32_t nac, const uint8_t *p,
@@ -166,6 +167,7 @@ int build_codes(Codes &c, uint32_t M, uint32_t N, uint32_t nac, const uint8_t *p
   HIPCHK(c.code_time.ensure((size_t)n_slots * M));
   const uint32_t F = 1u << log2F;
   if (spectra) HIPCHK(c.codespec.ensure((size_t)n_slots * F));
+  if (spectra && F >= 1024) HIPCHK(c.codespec_w.ensure((size_t)n_slots * F));
   CodesArgs a{};
   a.M = M; a.N = N; a.nac = nac; a.n_slots = n_slots;
   a.p = dp.p; a.s0_bits = d0.p; a.s1_bits = d1.p;
@@ -173,6 +175,7 @@ int build_codes(Codes &c, uint32_t M, uint32_t N, uint32_t nac, const uint8_t *p
   a.dn_s1 = (float)std::sqrt(1.0 / (double)(float)M);      // framing.cc:1228
   a.code_time = c.code_time.p;
   a.codespec = spectra ? c.codespec.p : nullptr;
+  a.codespec_w = (spectra && F >= 1024) ? c.codespec_w.p : nullptr;
   int rc2 = get_twiddles(const_cast<float2 **>(&a.tw));
   if (rc2) return rc2;
   launch_codes(a, ilog2(M), log2F, s);
@@ -243,9 +246,11 @@ struct mimo_rx {
   DevBuf<unsigned long long> sc_prof;   // RMIMO_SC_PROF=1 cycle counters
   uint32_t last_frames = 0, last_max_out = 0;
   int last_decode_path = MIMO_DECODE_NONE;   // kernel family of the last decode launch
-  // streaming state (facade)
+  // streaming state (facade). The device capture holds samples [origin, origin + total) of
+  // the stream since construction/reset (positions inside it are capture-relative).
   DevBuf<float2> capbuf;
-  uint64_t cap_len = 0, total = 0;
+  uint64_t cap_len = 0, total = 0, origin = 0;
+  DevBuf<uint32_t> probe;               // trim probe: per antenna, a proven metric zero
   int state = MIMO_STATE_SEEK_PLATEAU;
   uint64_t nsp = 0;
   bool have_sync = false, have_est = false;
@@ -529,6 +534,7 @@ int run_estimate(mimo_rx *h, const float2 *iq, uint64_t stride, uint32_t F, uint
   sa.N = h->N; sa.M = h->M; sa.SL = h->SL; sa.n_slots = h->n_slots;
   sa.lagc = h->lagc; sa.n_lagc = h->n_lagc;
   sa.codespec = h->codes.codespec.p; sa.vscale = h->vscale.p;
+  sa.codespec_w = h->codes.codespec_w.p;
   sa.info = h->info.p; sa.keys = h->keys.p; sa.tw = h->tw;
   LsArgs la{};
   la.iq = iq; la.stride = stride; la.frame_len = frame_len;
@@ -542,6 +548,7 @@ int run_estimate(mimo_rx *h, const float2 *iq, uint64_t stride, uint32_t F, uint
     // search of slot pairs with the LS terms fused in, then the fixed-order LS combine
     HIPCHK(h->lsq.ensure((size_t)F * h->N * h->N * h->nac * h->M));
     sa.s1sign = h->s1sign.p; sa.lsq = h->lsq.p; sa.nac = h->nac;
+    sa.cfo_part = (cfo && cfo->fold) ? cfo->part : nullptr;   // folded CFO: derotating loads
     static const bool xcd = [] { const char *e = getenv("RMIMO_SEARCH_XCD"); return !(e && e[0] == '0'); }();
     sa.xcd_order = xcd ? 1u : 0u;
     la.lsq = h->lsq.p;
@@ -604,7 +611,7 @@ int decode_expt() {
 int run_decode(mimo_rx *h, const float2 *iq, uint64_t stride, uint32_t F, uint64_t frame_len,
                uint32_t max_out, float2 *out_sym, uint8_t *out_idx, int ref_mode,
                const uint8_t *ref_idx, uint64_t ref_seed, uint64_t frame_id0, hipStream_t s,
-               uint32_t n_caps = 0) {
+               uint32_t n_caps = 0, const double *cfo_fold_part = nullptr) {
   int rc = ensure_workspace(h, F, 0, (uint64_t)F * max_out * h->N * 3 * kMaxEvmParts);
   if (rc) return rc;
   if (max_out == 0) return MIMO_OK;
@@ -629,11 +636,12 @@ int run_decode(mimo_rx *h, const float2 *iq, uint64_t stride, uint32_t F, uint64
   }
   hipEvent_t e = h->timer.begin(s);
   d.nrec = h->nrec.p;
-  d.cpe = h->cfo ? 1 : 0;
+  d.cpe = h->cfo ? (cfo_fold_part ? 2 : 1) : 0;
+  d.cfo_part = cfo_fold_part;
   static const bool no_split = [] { const char *e = getenv("RMIMO_DECODE_SPLIT"); return e && e[0] == '0'; }();
-  if (h->N == 8 && d.all_occ && h->det != 3 && max_out >= h->M / 64 && !no_split) {
-    // [F][M/64][max_out][N][64] complex64 spectra of the 8x8 split decode
-    if (h->spec.ensure((size_t)F * max_out * h->N * h->M) != hipSuccess)
+  if (!no_split && decode_split_accepts(d, h->log2M)) {
+    // [F][M/64][group][N][64] complex64 spectra of the 8x8 split decode (one symbol group)
+    if (h->spec.ensure((size_t)F * split_group_symbols(max_out) * h->N * h->M) != hipSuccess)
       return fail(MIMO_ERR_NOMEM, "split decode scratch");
     d.spec = h->spec.p;
   }
@@ -853,6 +861,11 @@ static int grow_capture(mimo_rx *h, uint64_t need) {
 static int finish_estimate(mimo_rx *h) {
   // channel estimate + replay decode of the complete window; callbacks per OFDM symbol
   const float2 *iq = h->capbuf.p;
+  // the window is complete: the device frame record says so (the plateau kernel saw it
+  // incomplete when the trigger fired)
+  h->sinfo.status = MIMO_FRAME_OK;
+  HIPCHK(hipMemcpyAsync(h->info.p, &h->sinfo, sizeof(FrameInfo), hipMemcpyHostToDevice,
+                        h->stream));
   int rc = run_estimate(h, iq, h->cap_len, 1, h->total, h->stream);
   if (rc) return rc;
   HIPCHK(hipMemcpyAsync(&h->sinfo, h->info.p, sizeof(FrameInfo), hipMemcpyDeviceToHost,
@@ -887,6 +900,127 @@ static int finish_estimate(mimo_rx *h) {
   return MIMO_OK;
 }
 
+// Bounded streaming memory. The reference holds a window ring of ACB + TX samples
+// (framing.cc:387-388, 639-651) and constant-size S&C filter state, so an unsynchronised stream
+// costs it nothing. Here the device capture keeps, while seeking, only what a later trigger can
+// still reach: the S&C history of the next chunk's work item (its halo and M samples of
+// filter history) and, in front of it, room for a plateau run and the window's leading SL.
+// Samples before a drop point D (a multiple of the chunk length, so the chunk grid stays
+// aligned) are dropped only when every antenna has a proven metric zero (y <= threshold in
+// the oracle's fp32, certified in fp64 with the decision band) in [D + SL + M, next item): no
+// plateau run then reaches back past it, so every run start, sync index and window start of
+// a later trigger lie inside the kept samples. A run that never ends (pathological input)
+// postpones the drop and the capture grows, as before.
+__global__ void trim_probe_kernel(const float2 *x, uint64_t stride, uint32_t M, int64_t lo,
+                                  int64_t hi, double thr, double band, uint32_t *ok) {
+  const uint32_t s = blockIdx.x, lane = threadIdx.x;
+  const float2 *r = x + (uint64_t)s * stride;
+  const int64_t span = hi - lo;
+  bool zero = false;
+  if (span > 0) {
+    const int64_t q = hi - 1 - (span * (int64_t)lane) / 64;   // 64 positions spread over [lo, hi)
+    double pr = 0.0, pi = 0.0, z = 0.0;
+    const int64_t h = M / 2;
+    for (int64_t k = q - (int64_t)M + 1; k <= q; k++) {
+      const float2 v = r[k];
+      z += (double)v.x * v.x + (double)v.y * v.y;
+      if (k > q - h) {
+        const float2 d = r[k - h];
+        pr += (double)d.x * v.x + (double)d.y * v.y;
+        pi += (double)d.x * v.y - (double)d.y * v.x;
+      }
+    }
+    const double R = 0.5 * z;
+    // the fp64 metric clears the threshold by more than the fp32 error band: the oracle's y
+    // is not above the threshold either
+    zero = R > 0.0 && pr * pr + pi * pi < (thr - band) * R * R;
+  }
+  const unsigned long long b = __ballot(zero);
+  if (lane == 0) ok[s] = b ? 1u : 0u;
+}
+
+static int maybe_trim(mimo_rx *h) {
+  const uint64_t K = sc_chunk_len(h->cp);
+  const uint64_t H = kScSpan - K;                     // halo of an S&C item
+  const uint64_t c_lo = h->total / K;                 // the next S&C starts at this chunk
+  const uint64_t need = H + 2 * (uint64_t)h->SL + 2 * (uint64_t)h->M + K;
+  if (c_lo * K < need + 4 * K) return MIMO_OK;        // not worth a move yet
+  const uint64_t D = (c_lo * K - need) / K * K;
+  const int64_t lo = (int64_t)(D + h->SL + h->M), hi = (int64_t)(c_lo * K - H);
+  if (hi - lo < (int64_t)K / 2) return MIMO_OK;
+  HIPCHK(h->probe.ensure(h->N));
+  hipLaunchKernelGGL(trim_probe_kernel, dim3(h->N), dim3(64), 0, h->stream, h->capbuf.p,
+                     h->cap_len, h->M, lo, hi, h->thr, sc_band(h->M), h->probe.p);
+  HIPCHK(hipGetLastError());
+  std::vector<uint32_t> ok(h->N);
+  HIPCHK(hipMemcpyAsync(ok.data(), h->probe.p, sizeof(uint32_t) * h->N, hipMemcpyDeviceToHost,
+                        h->stream));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  for (uint32_t a = 0; a < h->N; a++)
+    if (!ok[a]) return MIMO_OK;                       // a run may reach back: keep everything
+  // move [D, total) to the front in pieces of D samples (each piece's source is read before
+  // any later piece writes over it: copies on one stream run in order)
+  const uint64_t keep = h->total - D;
+  for (uint64_t o = 0; o < keep; o += D) {
+    const uint64_t m = std::min<uint64_t>(D, keep - o);
+    HIPCHK(hipMemcpy2DAsync(h->capbuf.p + o, sizeof(float2) * h->cap_len,
+                            h->capbuf.p + D + o, sizeof(float2) * h->cap_len,
+                            sizeof(float2) * m, h->N, hipMemcpyDeviceToDevice, h->stream));
+  }
+  h->origin += D;
+  h->total = keep;
+  return MIMO_OK;
+}
+
+// one piece of an execute call (at most a window's worth of samples)
+static int execute_piece(mimo_rx *h, const float *const *iq, uint64_t off, uint64_t n,
+                         uint64_t call_end) {
+  if (h->state == MIMO_STATE_SEEK_PLATEAU && h->total) {
+    int rc = maybe_trim(h);
+    if (rc) return rc;
+  }
+  const uint64_t old_total = h->total;
+  int rc = grow_capture(h, old_total + n);
+  if (rc) return rc;
+  for (uint32_t s = 0; s < h->N; s++)
+    HIPCHK(hipMemcpyAsync(h->capbuf.p + (size_t)s * h->cap_len + old_total,
+                          reinterpret_cast<const float2 *>(iq[s]) + off, sizeof(float2) * n,
+                          hipMemcpyHostToDevice, h->stream));
+  h->total = old_total + n;
+  if (h->state == MIMO_STATE_SEEK_PLATEAU) {
+    const uint64_t K = sc_chunk_len(h->cp);
+    rc = ensure_workspace(h, 1, (h->total + K - 1) / K, 0);
+    if (rc) return rc;
+    if (old_total == 0 && h->origin == 0)
+      HIPCHK(hipMemsetAsync(h->trig.p, 0xFF, sizeof(unsigned long long), h->stream));
+    // re-run the partially filled chunk; earlier chunks are final (y[n] uses x[<=n] only)
+    rc = run_sync(h, h->capbuf.p, h->cap_len, 1, h->total, old_total / K, false, h->stream);
+    if (rc) return rc;
+    HIPCHK(hipMemcpyAsync(&h->sinfo, h->info.p, sizeof(FrameInfo), hipMemcpyDeviceToHost,
+                          h->stream));
+    HIPCHK(hipStreamSynchronize(h->stream));
+    if (h->sinfo.status == MIMO_FRAME_NO_SYNC) {
+      h->nsp = h->origin + h->total;
+      return MIMO_OK;
+    }
+    h->have_sync = true;
+    h->state = MIMO_STATE_SAVE_ACCESS_CODES;
+  }
+  // SAVE_ACCESS_CODES (framing.cc:639-651): estimate_channel runs at window sample n_e =
+  // base + ACB + TX; a call that continues past it consumes one more sample in STATE_MIMO
+  // (framing.cc:494-503)
+  const uint64_t n_e = (uint64_t)h->sinfo.base + h->win_len;   // capture-relative
+  if (n_e < h->total) {
+    h->nsp = h->origin + n_e + ((h->origin + n_e + 1 < call_end) ? 2 : 1);
+    rc = finish_estimate(h);
+    if (rc) return rc;
+    h->state = MIMO_STATE_MIMO;
+  } else {
+    h->nsp = h->origin + h->total;
+  }
+  return MIMO_OK;
+}
+
 int mimo_rx_execute(mimo_rx *h, const float *const *iq, uint32_t n_ant, uint64_t n,
                     int32_t *state_out) {
   if (!h || (!iq && n)) return fail(MIMO_ERR_ARG, "null argument");
@@ -896,54 +1030,13 @@ int mimo_rx_execute(mimo_rx *h, const float *const *iq, uint32_t n_ant, uint64_t
     if (state_out) *state_out = h->state;
     return MIMO_OK;
   }
-  if (n == 0) {
-    if (state_out) *state_out = h->state;
-    return MIMO_OK;
-  }
-  const uint64_t old_total = h->total;
-  int rc = grow_capture(h, old_total + n);
-  if (rc) return rc;
-  for (uint32_t s = 0; s < h->N; s++)
-    HIPCHK(hipMemcpyAsync(h->capbuf.p + (size_t)s * h->cap_len + old_total, iq[s],
-                          sizeof(float2) * n, hipMemcpyHostToDevice, h->stream));
-  h->total = old_total + n;
-  if (h->state == MIMO_STATE_SEEK_PLATEAU) {
-    if (old_total == 0) {
-      const uint64_t K = sc_chunk_len(h->cp);
-      rc = ensure_workspace(h, 1, (h->total + K - 1) / K, 0);
-      if (rc) return rc;
-      HIPCHK(hipMemsetAsync(h->trig.p, 0xFF, sizeof(unsigned long long), h->stream));
-    }
-    // re-run the partially filled chunk; earlier chunks are final (y[n] uses x[<=n] only)
-    rc = run_sync(h, h->capbuf.p, h->cap_len, 1, h->total, old_total / sc_chunk_len(h->cp), false,
-                  h->stream);
+  // long calls are taken a window at a time, so the capture stays bounded whatever the
+  // caller's chunking (results are those of one call: the S&C is chunk-exact)
+  const uint64_t call_end = h->origin + h->total + n;
+  const uint64_t piece = std::max<uint64_t>(h->win_len, 4 * sc_chunk_len(h->cp));
+  for (uint64_t off = 0; off < n && h->state != MIMO_STATE_MIMO; off += piece) {
+    const int rc = execute_piece(h, iq, off, std::min<uint64_t>(piece, n - off), call_end);
     if (rc) return rc;
-    HIPCHK(hipMemcpyAsync(&h->sinfo, h->info.p, sizeof(FrameInfo), hipMemcpyDeviceToHost,
-                          h->stream));
-    HIPCHK(hipStreamSynchronize(h->stream));
-    if (h->sinfo.status == MIMO_FRAME_NO_SYNC) {
-      h->nsp = h->total;
-    } else {
-      h->have_sync = true;
-      h->state = MIMO_STATE_SAVE_ACCESS_CODES;
-    }
-  } else {
-    // SAVE: refresh completeness against the longer capture
-    rc = run_sync(h, h->capbuf.p, h->cap_len, 1, h->total, ~0ull, false, h->stream);
-    if (rc) return rc;
-    HIPCHK(hipMemcpyAsync(&h->sinfo, h->info.p, sizeof(FrameInfo), hipMemcpyDeviceToHost,
-                          h->stream));
-    HIPCHK(hipStreamSynchronize(h->stream));
-  }
-  if (h->state == MIMO_STATE_SAVE_ACCESS_CODES) {
-    if (h->sinfo.status == MIMO_FRAME_OK) {
-      h->nsp = h->sinfo.nsp;
-      rc = finish_estimate(h);
-      if (rc) return rc;
-      h->state = MIMO_STATE_MIMO;
-    } else {
-      h->nsp = h->total;
-    }
   }
   if (state_out) *state_out = h->state;
   return MIMO_OK;
@@ -957,6 +1050,8 @@ int mimo_rx_reset(mimo_rx *h) {
   HIPCHK(hipStreamSynchronize(h->stream));
   h->state = MIMO_STATE_SEEK_PLATEAU;
   h->total = 0;
+  h->origin = 0;
+  h->nsp = 0;
   h->have_sync = false;
   h->have_est = false;
   return MIMO_OK;
@@ -970,7 +1065,7 @@ int mimo_rx_get_state(const mimo_rx *h, int32_t *st) {
 
 int mimo_rx_get_sync_index(const mimo_rx *h, uint64_t *out) {
   if (!h || !out) return fail(MIMO_ERR_ARG, "null argument");
-  *out = h->have_sync ? h->sinfo.sync_index : 0;
+  *out = h->have_sync ? h->origin + h->sinfo.sync_index : 0;
   return MIMO_OK;
 }
 
@@ -982,8 +1077,8 @@ int mimo_rx_get_num_samples_processed(const mimo_rx *h, uint64_t *out) {
 
 int mimo_rx_get_plateau(const mimo_rx *h, uint32_t s, uint64_t *start, uint64_t *end) {
   if (!h || s >= h->N) return fail(MIMO_ERR_ARG, "bad stream");
-  if (start) *start = h->have_sync ? h->sinfo.plateau_start[s] : 0;
-  if (end) *end = h->have_sync ? h->sinfo.plateau_end[s] : 0;
+  if (start) *start = h->have_sync ? h->origin + h->sinfo.plateau_start[s] : 0;
+  if (end) *end = h->have_sync ? h->origin + h->sinfo.plateau_end[s] : 0;
   return MIMO_OK;
 }
 
@@ -1078,6 +1173,26 @@ static uint32_t batch_fpc(const mimo_batch *b) {
   return b->frames_per_capture > 1 ? b->frames_per_capture : 1u;
 }
 
+// The opt-in CFO folds into the loads (no scratch passes) where the fused search + LS (wave
+// form) and the streaming decode's CPE variant run: fc32 input (read in place or widened),
+// reference indices from HBM, both or neither output. Elsewhere the scratch passes remain.
+static bool cfo_folds(const mimo_rx *h, const mimo_batch *b, bool widened) {
+  if (!h->cfo || !h->search_ls || !h->codes.codespec_w.p || !search_ls_wave_enabled())
+    return false;
+  if (b->sample_format == MIMO_SAMPLE_SC16 && !widened) return false;
+  static const bool off = [] { const char *e = getenv("RMIMO_CFO_FOLD"); return e && e[0] == '0'; }();
+  if (off || b->ref_mode != 1 || (!b->d_out_sym) != (!b->d_out_idx)) return false;
+  DecodeArgs probe{};
+  probe.N = h->N; probe.detector = h->det;
+  probe.all_occ = (h->M_occ == h->M && !decode_grid_only()) ? 1 : 0;
+  probe.n_caps = b->n_frames; probe.n_refs = b->n_frames * batch_fpc(b); probe.qam = h->qam;
+  probe.ref_mode = b->ref_mode; probe.ref_idx = reinterpret_cast<const uint8_t *>(b->d_ref_idx);
+  probe.stride = b->stride; probe.max_out = b->max_out_syms; probe.M_occ = h->M_occ;
+  probe.out_sym = reinterpret_cast<float2 *>(b->d_out_sym);
+  probe.out_idx = reinterpret_cast<uint8_t *>(b->d_out_idx);
+  return decode_expt() == 0 && decode_stream_accepts(probe, h->log2M, b->n_frames * batch_fpc(b));
+}
+
 static int run_batch(mimo_rx *h, const mimo_batch *b, hipStream_t s) {
   const float2 *iq = reinterpret_cast<const float2 *>(b->d_iq);
   const uint32_t fpc = batch_fpc(b), slots = b->n_frames * fpc;
@@ -1095,8 +1210,10 @@ static int run_batch(mimo_rx *h, const mimo_batch *b, hipStream_t s) {
     probe.out_sym = reinterpret_cast<float2 *>(b->d_out_sym);
     probe.out_idx = reinterpret_cast<uint8_t *>(b->d_out_idx);
     probe.sc16 = 1;
+    static const bool no_split = [] { const char *e = getenv("RMIMO_DECODE_SPLIT"); return e && e[0] == '0'; }();
     const bool fused = sc_screen_ok(h->M) && h->search_ls && !h->cfo && decode_expt() == 0 &&
-                       decode_stream_accepts(probe, h->log2M, slots);
+                       (decode_stream_accepts(probe, h->log2M, slots) ||
+                        (!no_split && decode_split_accepts(probe, h->log2M)));
     if (fused) {
       h->cur_sc16 = 1;
       h->cur_scale = b->sc16_scale;
@@ -1116,7 +1233,19 @@ static int run_batch(mimo_rx *h, const mimo_batch *b, hipStream_t s) {
   int rc = run_sync(h, iq, b->stride, b->n_frames, b->frame_len, 0, true, s, fpc,
                     fpc > 1 ? b->d_ref_starts : nullptr, b->ref_stride, true);
   CfoBatchArgs ca{};
-  if (!rc && h->cfo) {
+  const bool fold = cfo_folds(h, b, iq != reinterpret_cast<const float2 *>(b->d_iq));
+  if (!rc && fold) {
+    // opt-in CFO, folded: estimates only (stage 1 here, stage 2 after the search); the
+    // search + LS loads and the decode derotate by them, no scratch capture
+    if (h->cfo_eps.ensure(cfo_batch_part_doubles(slots)) != hipSuccess)
+      return fail(MIMO_ERR_NOMEM, "cfo estimate allocation failed");
+    ca.iq = iq; ca.out = nullptr; ca.stride = b->stride; ca.frame_len = b->frame_len;
+    ca.len = h->win_len + 64; ca.N = h->N; ca.M = h->M; ca.cp = h->cp; ca.SL = h->SL;
+    ca.n_codes = h->N * h->nac; ca.n_data = h->pid + 2; ca.info = h->info.p;
+    ca.part = h->cfo_eps.p;
+    ca.fold = 1;
+    launch_cfo_batch(ca, slots, 1, s);
+  } else if (!rc && h->cfo) {
     // opt-in CFO, stage 1: coarse estimate per synced frame at its trigger, window derotated
     // into a scratch capture that search, LS, weights and decode read (S&C ran on the raw
     // samples: |P| and R do not depend on a frequency offset)
@@ -1133,14 +1262,14 @@ static int run_batch(mimo_rx *h, const mimo_batch *b, hipStream_t s) {
   }
   if (!rc) rc = run_estimate(h, iq, b->stride, slots, b->frame_len, s, true,
                              h->cfo ? &ca : nullptr);
-  if (!rc && h->cfo && h->search_ls)   // stage 2's data-region derotation (fused LS path)
+  if (!rc && h->cfo && !fold && h->search_ls)   // stage 2's data-region derotation
     launch_cfo_batch_rot2(ca, slots, s);
   if (!rc)
     rc = run_decode(h, iq, b->stride, slots, b->frame_len, b->max_out_syms,
                     reinterpret_cast<float2 *>(b->d_out_sym),
                     reinterpret_cast<uint8_t *>(b->d_out_idx), b->ref_mode,
                     reinterpret_cast<const uint8_t *>(b->d_ref_idx), b->ref_seed, b->frame_id0,
-                    s, b->n_frames);
+                    s, b->n_frames, fold ? ca.part : nullptr);
   h->cur_sc16 = 0;
   h->cur_scale = 1.0f;
   return rc;
@@ -1176,10 +1305,12 @@ int mimo_rx_process_batch(mimo_rx *h, const mimo_batch *b, void *hip_stream) {
   if (b->ref_mode == 1 && !b->d_ref_idx) return fail(MIMO_ERR_ARG, "ref_mode 1 needs d_ref_idx");
   if (batch_fpc(b) > 64)
     return fail(MIMO_ERR_ARG, "frames_per_capture must be at most 64");
-  // the opt-in CFO stages derotate each frame's window into one scratch capture per capture:
-  // back-to-back frames' windows overlap there, so the combination is refused
-  if (h->cfo && batch_fpc(b) > 1)
-    return fail(MIMO_ERR_UNSUPPORTED, "cfo_correct needs frames_per_capture <= 1");
+  // the unfolded CFO stages derotate each frame's window into one scratch capture per
+  // capture: back-to-back frames' windows overlap there, so that combination is refused (the
+  // folded form has no scratch)
+  if (h->cfo && batch_fpc(b) > 1 && !cfo_folds(h, b, b->sample_format == MIMO_SAMPLE_SC16))
+    return fail(MIMO_ERR_UNSUPPORTED, "cfo_correct with frames_per_capture > 1 needs the folded "
+                                      "CFO path (fc32 C2/C3-type geometry, ref_mode 1)");
   hipStream_t s = hip_stream ? (hipStream_t)hip_stream : h->stream;
   static const bool no_graph = [] {
     const char *e = getenv("RMIMO_NO_GRAPH");
@@ -1314,6 +1445,13 @@ int mimo_rx_batch_W(mimo_rx *h, float *W, uint32_t F) {
 int mimo_rx_set_timing(mimo_rx *h, int enable) {
   if (!h) return fail(MIMO_ERR_ARG, "null handle");
   h->timer.on = enable != 0;
+  return MIMO_OK;
+}
+
+int mimo_rx_get_stream_capacity(const mimo_rx *h, uint64_t *samples, uint64_t *held) {
+  if (!h) return fail(MIMO_ERR_ARG, "null handle");
+  if (samples) *samples = h->capbuf.p ? h->cap_len : 0;
+  if (held) *held = h->total;
   return MIMO_OK;
 }
 

@@ -56,6 +56,13 @@ __global__ __launch_bounds__(kEstT) void codes_kernel(CodesArgs a) {
   __syncthreads();
   fft_lds<LOG2F, kEstT, 1, false>(buf, a.tw);
   for (int i = tid; i < F; i += kEstT) a.codespec[(size_t)slot * F + i] = buf[lds_pad(i)];
+  if constexpr (F >= 1024) {
+    // the wave-local search's order: bin B k + q at q * 1024 + k (B = F / 1024)
+    constexpr int B = F / 1024;
+    if (a.codespec_w)
+      for (int i = tid; i < F; i += kEstT)
+        a.codespec_w[(size_t)slot * F + (i % B) * 1024 + i / B] = buf[lds_pad(i)];
+  }
 }
 
 // ------------------------------------------------------------------------------------
@@ -187,6 +194,16 @@ void search_reg_kernel(SearchArgs a) {
   __syncthreads();
   if (tid == 0 && s_key)
     atomicMax(&a.keys[((uint64_t)f * a.N + r) * a.n_slots + slot], s_key);
+}
+
+// exp(-j 2 pi cyc) for a phase in cycles given in fp64 (reduced to [-1/2, 1/2] first, so
+// long offsets keep their accuracy), as an fp32 phasor
+MIMO_DEV v2f phasor_cycles(double cyc) {
+  double ph = -2.0 * cyc;                             // units of pi
+  ph -= 2.0 * rint(ph * 0.5);
+  double sn, cs;
+  sincospi(ph, &sn, &cs);
+  return v2f{(float)cs, (float)sn};
 }
 
 MIMO_DEV uint32_t key_index(unsigned long long k) {
@@ -379,6 +396,250 @@ void search_ls_kernel(SearchArgs a) {
   }
 }
 
+// The same search + LS with the FFT_F split into one workgroup-wide radix-B pass and B
+// wave-local 1024-point transforms (F = 1024 B, one wave per sub-transform, T = 64 B):
+//   forward  X[B k + q] = DFT_1024( c_q )[k],   c_q[n] = W_F^{nq} sum_r x[n + 1024 r] W_B^{rq}
+//   inverse  y[m' + 1024 p] = sum_q W_B^{-pq} W_F^{-m'q} Y_q[m'],  Y_q = IDFT_1024( Z[B k + q] )
+// The radix-B pass runs on 16/B butterflies per thread straight from the segment loads; one
+// workgroup exchange hands c_q to wave q, whose 1024-point transform (RegPlan<10, 16>: radix
+// 16, 4, 16) exchanges only through its own LDS region (wave-local order, no barrier) and
+// leaves X[B (l + 64 s) + q] in lane l, slot s -- the inverse's first-pass input order, so the
+// product with conj(code spectrum) (stored permuted, codespec_w[slot][q][k]) and the inverse
+// run on in registers. One exchange back gathers Y_q[m'] over q for the final radix-B pass.
+// Three workgroup exchanges per slot pair instead of nine.
+// CFO (opt-in, folded): every loaded sample n is derotated by the frame's coarse estimate,
+// x[n] exp(-j 2 pi eps0 (n - base) / M) -- what the scratch pass of the unfolded path wrote --
+// as a per-thread phasor (fp64 phase) times per-frame step phasors.
+template <int LOG2F, int LOG2M, bool SC16 = false, bool CFO = false>
+__global__ __launch_bounds__((1 << LOG2F) / 16) __attribute__((amdgpu_waves_per_eu(4)))
+void search_ls_wave_kernel(SearchArgs a) {
+  constexpr int F = 1 << LOG2F, T = F / 16, M = 1 << LOG2M;
+  constexpr int B = F / 1024;                          // waves = sub-transforms = block radix
+  constexpr int NB = 16 / B;                           // block butterflies per thread
+  constexpr int RB = lds_padded_len(1024);             // region stride (entries)
+  using PW = RegPlan<10, 16>;
+  static_assert(B >= 1 && B <= 16 && T == 64 * B, "F = 1024 B, one wave per sub-transform");
+  extern __shared__ __attribute__((aligned(16))) float2 lds_raw[];
+  v2f *buf = reinterpret_cast<v2f *>(lds_raw);
+  __shared__ unsigned long long s_key[2];
+  uint32_t f = blockIdx.y, bx = blockIdx.x;
+  if (a.xcd_order) {   // as search_ls_kernel: slot pair slowest within each XCD's range
+    const uint32_t G = gridDim.x * gridDim.y, b = blockIdx.y * gridDim.x + blockIdx.x;
+    const uint32_t x = b % 8, q = G / 8, rem = G % 8;
+    const uint32_t lid = x * q + min(x, rem) + b / 8;
+    const uint32_t nf = gridDim.y, nrx = a.N;
+    bx = (lid / (nrx * nf)) * nrx + lid % nrx;
+    f = (lid / nrx) % nf;
+  }
+  const FrameInfo &I = a.info[f];
+  if (I.status != 0) return;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const uint32_t wq = __builtin_amdgcn_readfirstlane((uint32_t)tid >> 6);   // this wave's q
+  const uint32_t r = bx % a.N;
+  const uint32_t s0 = 2 * (bx / a.N);
+  const uint32_t ns = min(2u, a.n_slots - s0);
+  const int64_t abs0 = I.base + (int64_t)a.SL * s0;
+  const int64_t L = (int64_t)a.frame_len;
+  const auto xs = iq_row<SC16>(a.iq, a.iq_scale, ((uint64_t)I.cap * a.N + r) * a.stride);
+  const bool inb = abs0 >= 0 && abs0 + F <= L;
+  v2f v[16], X[16];
+  // segment loads in the block pass's order: v[i B + rr] = x[n_i + 1024 rr], n_i = tid + T i
+#pragma unroll
+  for (int i = 0; i < NB; i++)
+#pragma unroll
+    for (int rr = 0; rr < B; rr++) {
+      const int64_t n = abs0 + tid + T * i + 1024 * rr;
+      const float2 t = xs.at(inb ? n : (n < 0 ? 0 : (n >= L ? L - 1 : n)));
+      v[i * B + rr] = v2f{t.x, t.y};
+    }
+  if (!inb) {
+#pragma unroll
+    for (int i = 0; i < NB; i++)
+#pragma unroll
+      for (int rr = 0; rr < B; rr++) {
+        const int64_t n = abs0 + tid + T * i + 1024 * rr;
+        if (n < 0 || n >= L) v[i * B + rr] = v2f{0.0f, 0.0f};
+      }
+  }
+  double nu = 0.0;                                    // CFO: eps0 / M, cycles per sample
+  if constexpr (CFO) {
+    nu = cfo_stage_eps(a.cfo_part, f, 1) / (double)M;
+    // sample n_i + 1024 rr, n_i = tid + T i, relative to base: SL s0 + n_i + 1024 rr
+    v2f ri = phasor_cycles(nu * (double)((int64_t)a.SL * s0 + tid));
+    const v2f sa = phasor_cycles(nu * (double)T), sb = phasor_cycles(nu * 1024.0);
+#pragma unroll
+    for (int i = 0; i < NB; i++) {
+      v2f rb = ri;
+#pragma unroll
+      for (int rr = 0; rr < B; rr++) {
+        v[i * B + rr] = vmul(v[i * B + rr], rb);
+        rb = vmul(rb, sb);
+      }
+      ri = vmul(ri, sa);
+    }
+  }
+  v2f w1[PW::NTW > 0 ? PW::NTW : 1];
+  reg_twiddles<10, 16>(w1, a.tw, lane);
+  if (tid == 0) { s_key[0] = 0ull; s_key[1] = 0ull; }
+  // radix-B block pass (forward): DFT_B over rr, twiddle W_F^{nq}, c_q[n] -> region q
+  v2f *rg = buf + wq * RB;                             // this wave's region
+  if constexpr (B > 1) {
+#pragma unroll
+    for (int i = 0; i < NB; i++) {
+      dft_small<B, false>(v + i * B);
+      const int n = tid + T * i;
+#pragma unroll
+      for (int q = 1; q < B; q++)
+        v[i * B + q] = vmul(v[i * B + q], twiddle<false>(a.tw, ((n * q) & (F - 1)) * (kTwN / F)));
+#pragma unroll
+      for (int q = 0; q < B; q++) buf[q * RB + lds_pad(n)] = v[i * B + q];
+    }
+    __syncthreads();                                   // every c_q complete
+#pragma unroll
+    for (int e = 0; e < 16; e++) v[e] = rg[lds_pad(reg_index<10, 16>(lane, e))];
+  }
+  // wave-local 1024-point forward transform of c_q: X[B k + q], k = lane + 64 e, in v[e]
+  reg_compute<10, 16, 0, false>(v, w1);
+  reg_rest_wave<10, 16, 1, false>(rg, v, w1, lane);
+#pragma unroll
+  for (int e = 0; e < 16; e++) X[e] = v[e];
+  for (uint32_t u = 0; u < ns; u++) {                 // uniform
+    const uint32_t slot = s0 + u;
+    const v2f *__restrict__ csp =
+        reinterpret_cast<const v2f *>(a.codespec_w + (size_t)slot * F) + wq * 1024 + lane;
+#pragma unroll
+    for (int e = 0; e < 16; e++) v[e] = vmulc(X[e], csp[64 * e]);
+    reg_compute<10, 16, 0, true>(v, w1);
+    reg_rest_wave<10, 16, 1, true>(rg, v, w1, lane);
+    // Y_q[m'] (m' = lane + 64 e) -> region q; then the radix-B pass over q per m'
+    if constexpr (B > 1) {
+#pragma unroll
+      for (int e = 0; e < 16; e++) rg[lds_pad(reg_index<10, 16>(lane, e))] = v[e];
+      __syncthreads();
+#pragma unroll
+      for (int i = 0; i < NB; i++) {
+        // an opaque copy per use: the twiddle reads are issued here, not hoisted out of the
+        // slot loop and held in registers across it
+        int n = tid + T * i;
+        asm volatile("" : "+v"(n));
+#pragma unroll
+        for (int q = 0; q < B; q++) v[i * B + q] = buf[q * RB + lds_pad(n)];
+#pragma unroll
+        for (int q = 1; q < B; q++)
+          v[i * B + q] = vmul(v[i * B + q], twiddle<true>(a.tw, ((n * q) & (F - 1)) * (kTwN / F)));
+        dft_small<B, true>(v + i * B);
+      }
+    }
+    // lag index of v[i B + p]: m = n_i + 1024 p (B > 1), or lane + 64 e (B = 1)
+    const float vs = a.vscale[slot];
+    const int off = (int)(u * a.SL);
+    const uint32_t ws = a.SL * slot;                  // window index of lag 0
+    unsigned long long best = 0ull;
+#pragma unroll
+    for (int e = 0; e < 16; e++) {
+      const int m = (B > 1) ? tid + T * (e / B) + 1024 * (e % B) : reg_index<10, 16>(lane, e);
+      const int i = m - off;
+      const float val = (v[e].x * v[e].x + v[e].y * v[e].y) * vs;
+      if (i >= 0 && i < (int)a.SL && val > 0.0f) {
+        const unsigned long long key = ((unsigned long long)__float_as_uint(val) << 32) |
+                                       (unsigned long long)(0xFFFFFFFFu - (ws + (uint32_t)i));
+        best = key > best ? key : best;
+      }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const unsigned long long q = __shfl_xor(best, o);
+      best = q > best ? q : best;
+    }
+    if (lane == 0 && best) atomicMax(&s_key[u], best);
+    __syncthreads();                                  // key final; every reader of buf is done
+    if (tid == 0) a.keys[((uint64_t)f * a.N + r) * a.n_slots + slot] = s_key[u];
+  }
+  // LS terms of the pair's access codes, as search_ls_kernel (register-resident form where
+  // the workgroup holds two M-point windows of M/8 threads, else batched through LDS)
+  constexpr int PBM = lds_padded_len(M), NL = 2 * M / T;
+  static_assert(2 * M % T == 0, "whole windows per thread");
+  const bool valid0 = s0 != 0, valid1 = ns > 1;
+  if (!valid0 && !valid1) return;                     // uniform
+  const int64_t w0 = I.base + (int64_t)key_index(s_key[0]);
+  const int64_t w1v = I.base + (int64_t)key_index(s_key[1]);
+  constexpr bool LSREG = 2 * (M / 8) == T && LOG2M >= 9;
+  if constexpr (LSREG) {
+    using PM = RegPlan<LOG2M, 8>;
+    const uint32_t u = (uint32_t)tid / PM::T, lt = (uint32_t)tid % PM::T;   // u uniform per wave
+    const bool valid = u ? valid1 : valid0;
+    const int64_t wb = u ? w1v : w0;
+    v2f xw[8];
+#pragma unroll
+    for (int e = 0; e < 8; e++) {
+      const int64_t n = wb + reg_index<LOG2M, 8>((int)lt, e);
+      const bool ok = valid && n >= 0 && n < L;
+      const float2 t = xs.at(n < 0 ? 0 : (n >= L ? L - 1 : n));
+      xw[e] = ok ? v2f{t.x, t.y} : v2f{0.0f, 0.0f};
+    }
+    if constexpr (CFO) {   // window sample lt + e M/8, relative to base: wb - base + ...
+      v2f rb = phasor_cycles(nu * (double)(wb - I.base + (int64_t)lt));
+      const v2f st = phasor_cycles(nu * (double)(M / 8));
+#pragma unroll
+      for (int e = 0; e < 8; e++) {
+        xw[e] = vmul(xw[e], rb);
+        rb = vmul(rb, st);
+      }
+    }
+    v2f wm[PM::NTW > 0 ? PM::NTW : 1];
+    reg_twiddles<LOG2M, 8>(wm, a.tw, (int)lt);
+    reg_compute<LOG2M, 8, 0, false>(xw, wm);
+    reg_rest<LOG2M, 8, 1, false>(buf + u * PBM, xw, wm, (int)lt);
+    if (!valid) return;                               // uniform per wave
+    const uint32_t ac = s0 + u - 1, code = ac / a.N, tx = ac % a.N;
+    const int8_t *sg = a.s1sign + ((size_t)tx * a.nac + code) * M;
+    float2 *q = a.lsq + ((((uint64_t)f * a.N + r) * a.N + tx) * a.nac + code) * M;
+#pragma unroll
+    for (int e = 0; e < 8; e++) {
+      const int k = reg_index<LOG2M, 8>((int)lt, e);
+      const int sgn = sg[k];
+      const float2 Xk = make_float2(xw[e].x, xw[e].y);
+      q[k] = sgn > 0 ? Xk : (sgn < 0 ? cneg(Xk) : make_float2(0.0f, 0.0f));
+    }
+    return;
+  } else {
+    float2 *twm = reinterpret_cast<float2 *>(lds_raw) + lds_padded_len(F);
+    fill_twiddles_lds<LOG2M, T>(twm, a.tw);
+    float2 win[NL];
+#pragma unroll
+    for (int e = 0; e < NL; e++) {
+      const int i = tid + e * T, uu = i / M, j = i % M;
+      const int64_t n = (uu ? w1v : w0) + j;
+      const bool ok = (uu ? valid1 : valid0) && n >= 0 && n < L;
+      win[e] = ok ? xs.at(n) : make_float2(0.0f, 0.0f);
+      if constexpr (CFO) {
+        const v2f ph = phasor_cycles(nu * (double)(n - I.base));
+        const v2f w = vmul(v2f{win[e].x, win[e].y}, ph);
+        win[e] = make_float2(w.x, w.y);
+      }
+    }
+    float2 *lb = reinterpret_cast<float2 *>(buf);
+#pragma unroll
+    for (int e = 0; e < NL; e++) {
+      const int i = tid + e * T, uu = i / M, j = i % M;
+      lb[uu * PBM + lds_pad(j)] = win[e];
+    }
+    __syncthreads();
+    fft_lds_twl<LOG2M, T, 2, false>(lb, twm, tid);
+#pragma unroll
+    for (int e = 0; e < NL; e++) {
+      const int i = tid + e * T, uu = i / M, k = i % M;
+      if (!(uu ? valid1 : valid0)) continue;
+      const uint32_t ac = s0 + uu - 1, code = ac / a.N, tx = ac % a.N;
+      const int8_t *sg = a.s1sign + ((size_t)tx * a.nac + code) * M;
+      float2 *q = a.lsq + ((((uint64_t)f * a.N + r) * a.N + tx) * a.nac + code) * M;
+      const float2 Xk = lb[uu * PBM + lds_pad(k)];
+      const int sgn = sg[k];
+      q[k] = sgn > 0 ? Xk : (sgn < 0 ? cneg(Xk) : make_float2(0.0f, 0.0f));
+    }
+  }
+}
+
 // one thread per (frame, subcarrier, rx-tx pair): the codes' X/S1 of lsq in code order, G and
 // this block's share of the residual variance (as ls_combine_kernel)
 __global__ __launch_bounds__(256) void ls_combine_q_kernel(LsArgs a) {
@@ -395,6 +656,8 @@ __global__ __launch_bounds__(256) void ls_combine_q_kernel(LsArgs a) {
     double sr = 0.0, si = 0.0, s2 = 0.0;
     const uint32_t r_ = rt / N, t_ = rt % N;
     const double nu = a.cfo_part ? cfo_stage_eps(a.cfo_part, f, 2) / (double)M : 0.0;
+    if (a.cfo_part && k == 0 && rt == 0)   // the frame's total estimate (stage 1 + stage 2)
+      const_cast<FrameInfo &>(I).cfo_eps = (float)(cfo_stage_eps(a.cfo_part, f, 1) + nu * M);
     // the codes' terms in batches of CB loads in flight (one latency per batch instead of per
     // code), summed in code order as before
     constexpr uint32_t CB = 8;
@@ -921,8 +1184,18 @@ static bool search_ls_try(const SearchArgs &a, int log2F, int log2M, uint32_t nf
         if (nf) {
           // the segment image, then the LS transform's M/2 twiddles
           const size_t shm = sizeof(float2) * (lds_padded_len(1 << LOG2F) + (1 << LOG2M) / 2);
-          auto kern = a.sc16 ? search_ls_kernel<LOG2F, LOG2M, true>
-                             : search_ls_kernel<LOG2F, LOG2M, false>;
+          // wave-local sub-transforms (F = 1024 B) unless RMIMO_SEARCH_WAVE=0 (A/B)
+          void (*kern)(SearchArgs) = nullptr;
+          if constexpr (LOG2F >= 10) {
+            if (search_ls_wave_enabled() && a.codespec_w)
+              kern = a.cfo_part ? (a.sc16 ? search_ls_wave_kernel<LOG2F, LOG2M, true, true>
+                                          : search_ls_wave_kernel<LOG2F, LOG2M, false, true>)
+                                : (a.sc16 ? search_ls_wave_kernel<LOG2F, LOG2M, true>
+                                          : search_ls_wave_kernel<LOG2F, LOG2M, false>);
+          }
+          if (!kern)
+            kern = a.sc16 ? search_ls_kernel<LOG2F, LOG2M, true>
+                          : search_ls_kernel<LOG2F, LOG2M, false>;
           (void)hipFuncSetAttribute((const void *)kern,
                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
           dim3 grid(((a.n_slots + 1) / 2) * a.N, nf);
@@ -936,6 +1209,11 @@ static bool search_ls_try(const SearchArgs &a, int log2F, int log2M, uint32_t nf
     }
   }
   return false;
+}
+
+bool search_ls_wave_enabled() {
+  static const bool off = [] { const char *e = getenv("RMIMO_SEARCH_WAVE"); return e && e[0] == '0'; }();
+  return !off;
 }
 
 bool search_ls_supported(int log2F, int log2M) {

@@ -160,6 +160,31 @@ MIMO_DEV void reg_rest(v2f *buf, v2f *v, const v2f *w1, int tid) {
   }
 }
 
+// LDS writes of this wave visible to its own reads; no code motion across
+MIMO_DEV void wave_lds_sync() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_wave_barrier();
+}
+
+// passes P .. NP-1 of a transform held by ONE wave (T = 64 lanes) through that wave's own LDS
+// region: no workgroup barrier, only the wave's own store -> load ordering. (A pass's loads are
+// consumed by its butterflies before the next store is issued, so the region needs no sync
+// ahead of a store.)
+template <int LOG2N, int PTS, int P, bool INV>
+MIMO_DEV void reg_rest_wave(v2f *buf, v2f *v, const v2f *w1, int lane) {
+  using PL = RegPlan<LOG2N, PTS>;
+  static_assert(PL::T == 64, "one wave per transform");
+  if constexpr (P < PL::NP) {
+    int t = lane;
+    asm volatile("" : "+v"(t));
+    reg_store<LOG2N, PTS, P - 1>(buf, v, t);
+    wave_lds_sync();
+    reg_load<LOG2N, PTS, P>(buf, v, t);
+    reg_compute<LOG2N, PTS, P, INV>(v, w1);
+    reg_rest_wave<LOG2N, PTS, P + 1, INV>(buf, v, w1, lane);
+  }
+}
+
 // element index held in v[s] after the last pass (and read by pass 0): j + r*N/R, R the main
 // radix (the first and the last pass)
 template <int LOG2N, int PTS>

@@ -149,6 +149,7 @@ struct SearchArgs {
   uint32_t N, M, SL, n_slots;      // n_slots = N*nac + 1 (slot 0 = S0)
   uint32_t lagc, n_lagc;           // lags per transform, transforms per slot
   const float2 *codespec;          // [n_slots][F]
+  const float2 *codespec_w;        // [n_slots][F], bin B k + q at q 1024 + k (B = F/1024), or null
   const float *vscale;             // [n_slots]
   const FrameInfo *info;
   unsigned long long *keys;        // [F][N][n_slots] packed (value, ~index)
@@ -158,11 +159,14 @@ struct SearchArgs {
   float2 *lsq;                     // [F][N][N][nac][M] X/S1 per access code
   uint32_t nac;
   uint32_t xcd_order;              // search_ls_kernel: slot pair slowest within each XCD
+  const double *cfo_part;          // opt-in CFO, folded: derotate the loads by stage 1 (or null)
 };
 void launch_search(const SearchArgs &a, int log2F, uint32_t n_frames, hipStream_t s);
 // true when (log2F, log2M) has a search_ls_kernel instance (it then ran)
 bool launch_search_ls(const SearchArgs &a, int log2F, int log2M, uint32_t n_frames, hipStream_t s);
 bool search_ls_supported(int log2F, int log2M);
+// the wave-local form of search_ls_kernel (F >= 1024) is on (RMIMO_SEARCH_WAVE=0: off)
+bool search_ls_wave_enabled();
 
 // LS estimate, framing.cc:797-824 (+ training residual noise variance)
 struct LsArgs {
@@ -217,6 +221,7 @@ struct CfoBatchArgs {
   uint32_t n_data;                 // data symbols in a window (PID + 2)
   uint32_t n_slots;
   int rot_window;                  // stage 2 derotates the whole window (LS not yet run)
+  int fold;                        // the search, LS and decode loads derotate: estimates only
   FrameInfo *info;
   const unsigned long long *keys;  // search keys (stage 2 timing)
   double *part;                    // [F][2 stages][blocks][2] partial correlations
@@ -257,8 +262,11 @@ struct DecodeArgs {
   uint32_t n_cu;                   // compute units (persistent grid size)
   unsigned long long *prof;        // diagnostics: [items, load, fft, apply, reduce] cycles
   uint32_t *nrec;                  // [F] EVM records per frame (decode_stream_kernel) or null
-  float2 *spec;                    // split decode (8x8) spectra scratch [F][M/64][max_out][N][64]
-  int cpe;                         // opt-in CFO: decision-directed common-phase tracking
+  float2 *spec;                    // split decode (8x8) spectra scratch [F][M/64][sym_cap][N][64]
+  uint32_t sym0, sym_cap, sym_groups;   // split decode: this launch's symbol group (set inside)
+  int cpe;                         // opt-in CFO: decision-directed common-phase tracking; 2 =
+                                   // folded: the kernel also derotates by the frame's estimate
+  const double *cfo_part;          // folded CFO: the stage partials (cfo_stage_eps)
   int expt;                        // diagnostics (RMIMO_DEC_EXPT): bit 0 IQ from one symbol,
                                    // bit 1 no output stores, bit 2 weights of subcarrier 0
 };
@@ -273,9 +281,13 @@ uint32_t launch_decode_stream(const DecodeArgs &a, int log2M, uint32_t n_frames,
 // true when launch_decode_stream takes this configuration (nrec aside): the sc16 wire input
 // is decoded only there
 bool decode_stream_accepts(const DecodeArgs &a, int log2M, uint32_t n_frames);
-// decode_stream.hip: 8x8 split form (spectra to a scratch, then a chunked apply); 0 when the
-// configuration is not handled or a.spec is null
+// decode_stream.hip: 8x8 split form (spectra to a scratch, then a chunked apply, alternating
+// over groups of kSplitGroup symbols); 0 when the configuration is not handled or a.spec is
+// null. The scratch holds split_group_symbols(max_out) symbols per frame.
+constexpr uint32_t kSplitGroup = 32;
 uint32_t launch_decode_split(const DecodeArgs &a, int log2M, uint32_t n_frames, hipStream_t s);
+bool decode_split_accepts(const DecodeArgs &a, int log2M);
+uint32_t split_group_symbols(uint32_t max_out);
 constexpr uint32_t kMaxEvmParts = 16;
 
 struct EvmArgs {
@@ -300,6 +312,7 @@ struct CodesArgs {
   float dn_s0, dn_s1;
   float2 *code_time;               // [n_slots][M]
   float2 *codespec;                // [n_slots][F] (null: skip)
+  float2 *codespec_w;              // [n_slots][F] permuted for the wave-local search (or null)
   const float2 *tw;
 };
 void launch_codes(const CodesArgs &a, int log2M, int log2F, hipStream_t s);

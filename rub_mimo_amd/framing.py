@@ -282,6 +282,14 @@ class framesync:
     def reset(self):
         check(lib().mimo_rx_reset(self._h), "reset")
 
+    def stream_capacity(self):
+        """(device capture capacity, samples held) per antenna of the streaming execute
+        (mimo_rx_get_stream_capacity; diagnostic)."""
+        cap, held = C.c_uint64(), C.c_uint64()
+        check(lib().mimo_rx_get_stream_capacity(self._h, C.byref(cap), C.byref(held)),
+              "stream_capacity")
+        return cap.value, held.value
+
     def set_siso_tx(self, tx):
         self._siso = (tx, getattr(self, "_siso", (0, 0))[1])
         check(lib().mimo_rx_set_siso(self._h, *self._siso), "set_siso_tx")

@@ -132,6 +132,43 @@ def test_batch_then_reset_then_chunked_execute_on_one_handle():
     assert evm_delta(np.stack(got), g["symbols"]) <= SYM_TOL
 
 
+def test_streaming_execute_memory_is_bounded_by_the_window():
+    """A live stream that stays unsynchronised for a long time: a noise lead of more than 20
+    reference windows (ACB + TX, framing.cc:387-388) before a frame, fed to the streaming
+    execute in random chunks. The device capture stays within 2x the window (the reference
+    holds one window ring; here only what a later trigger can reach is kept while seeking),
+    and sync, plateau, samples processed and symbols equal the oracle's on the whole stream."""
+    M, cp, N, nac, pid, qam = 1024, 76, 2, 4, 40, 16
+    SL = M + cp
+    win = SL * (nac * N + 4) + pid * SL                   # ACB + TX
+    rx, txo, _ = ref.synth_frame(M, cp, N, nac, pid, qam, seed=5, frame=0, offset=-1,
+                                 snr_db=25.0)
+    rng = np.random.default_rng(17)
+    lead_len = 21 * win
+    nstd = np.sqrt(0.0625 * 10 ** (-25.0 / 10) / 2)
+    lead = (rng.standard_normal((N, lead_len)) + 1j * rng.standard_normal((N, lead_len))) * nstd
+    stream = np.concatenate([lead.astype(np.complex64), rx], axis=1)
+    o = ref.FrameSyncRef(M, cp, N, nac, pid_max=pid, detector=_lib.DET_ZF2)
+    assert o.execute(stream) == ref.STATE_MIMO
+    got = []
+    ms0, ms1 = new_codes(N)
+    fs = fr.framesync(M, cp, N, nac, fr.ofdmframe_init_default_sctype(M), ms0, ms1,
+                      callback=lambda xs, m: got.append(np.stack([x.copy() for x in xs])),
+                      pid_max=pid, detector=_lib.DET_ZF2, qam_order=qam)
+    pos, peak = 0, 0
+    while pos < stream.shape[1]:
+        c = int(rng.integers(1, 40000))
+        fs.execute([r[pos:pos + c] for r in stream], min(c, stream.shape[1] - pos))
+        pos += c
+        peak = max(peak, fs.stream_capacity()[0])
+    assert peak <= 2 * win, (peak, win)
+    assert fs.get_sync_index() == o.get_sync_index()
+    assert fs.get_num_samples_processed() == o.get_num_samples_processed()
+    assert [fs.get_plateau_start(s) for s in range(N)] == [o.get_plateau_start(s)
+                                                          for s in range(N)]
+    assert evm_delta(np.stack(got)[:pid], o.symbols()[:pid]) <= SYM_TOL
+
+
 def test_incomplete_then_complete_and_mimo_semantics():
     g = load([p for p in GOLDEN if "m64_2x2_zf2" in p][0])
     M, cp, N, nac, pid = (int(g[k]) for k in ("M", "cp", "N", "nac", "pid"))
@@ -705,8 +742,8 @@ def test_cfo_estimate_and_derotate(M, eps_true):
     assert np.all(back[:, n:] == 0)                                   # nothing past n
 
 
-@pytest.mark.parametrize("eps_true", [0.3, -0.62])
-def test_cfo_batch_corrects_rotated_c3_frames(eps_true):
+@pytest.mark.parametrize("eps_true,mode", [(0.3, "fold"), (-0.62, "fold"), (0.3, "scratch")])
+def test_cfo_batch_corrects_rotated_c3_frames(eps_true, mode):
     """Opt-in CFO on the batched path (mimo_rx_config.cfo_correct; the reference has a FIXME at
     framing.cc:486 and no CFO step, so parity is unpinned). C3 captures rotated by eps_true
     subcarrier spacings:
@@ -719,7 +756,9 @@ def test_cfo_batch_corrects_rotated_c3_frames(eps_true):
       subcarrier spacings at 30 dB) would cost the cleanest (-32 dB) frames ~2.4 dB of drift
       over 1000 symbols; the decode's decision-directed common-phase tracking takes that to
       ~0.3 dB (the first symbol of each decode workgroup's range is not yet tracked);
-    - without the correction the rotated frames collapse (> 10 dB worse)."""
+    - without the correction the rotated frames collapse (> 10 dB worse).
+    mode "fold" (reference indices from HBM): the search + LS loads and the streaming decode
+    derotate in place; "scratch" (ref_mode 2): the estimate-and-derotate scratch passes."""
     import torch
     from rub_mimo_amd.receiver import cfo_derotate
     M, cp, N, nac, pid, qam, F = 2048, 152, 4, 20, 1000, 64, 4
@@ -735,7 +774,10 @@ def test_cfo_batch_corrects_rotated_c3_frames(eps_true):
         rxo = Receiver(RxParams(M=M, cp_len=cp, num_streams=N, num_access_codes=nac,
                                 pid_max=pid, detector=_lib.DET_MMSE, qam_order=qam,
                                 cfo_correct=cfo))
-        rxo.process(x, L, L, F, max_out=pid, ref_mode=1, ref_idx=tx)
+        if mode == "fold":
+            rxo.process(x, L, L, F, max_out=pid, ref_mode=1, ref_idx=tx)
+        else:
+            rxo.process(x, L, L, F, max_out=pid, ref_mode=2, ref_seed=812, frame_id0=0)
         return rxo.results()
 
     def evm(r):
@@ -763,9 +805,10 @@ def test_cfo_batch_corrects_rotated_c3_frames(eps_true):
         assert e2 > e0 + 10.0, (f, e0, e2)
 
 
-def test_cfo_with_back_to_back_frames_is_refused():
-    """The opt-in CFO stages derotate each frame's window into a per-capture scratch, where
-    back-to-back frames' windows would overlap: frames_per_capture > 1 is refused loudly."""
+def test_cfo_with_back_to_back_frames_is_refused_unfolded():
+    """The unfolded CFO stages derotate each frame's window into a per-capture scratch, where
+    back-to-back frames' windows would overlap: frames_per_capture > 1 is refused loudly
+    outside the folded path (here M = 256: no fused search + streaming decode)."""
     import torch
     M, cp, N, nac, pid = 256, 19, 2, 4, 16
     rxo = Receiver(RxParams(M=M, cp_len=cp, num_streams=N, num_access_codes=nac, pid_max=pid,
@@ -776,6 +819,51 @@ def test_cfo_with_back_to_back_frames_is_refused():
         rxo.process(iq, L, L, 1, max_out=pid, frames_per_capture=2)
 
 
+def test_cfo_folded_on_back_to_back_frames():
+    """Folded CFO (no scratch) on streams of back-to-back C3 frames with tight gaps: the
+    captures rotated by eps sync and re-arm exactly as the unrotated ones (S&C is
+    offset-invariant), every decoded frame's estimate is within 2e-5 of eps, and its EVM is
+    within 0.5 dB of the unrotated frame decoded without correction."""
+    import torch
+    from rub_mimo_amd.receiver import cfo_derotate
+    M, cp, N, nac, pid, qam = 2048, 152, 4, 20, 200, 64
+    eps = 0.27
+    sp = SynthParams(M=M, cp_len=cp, num_streams=N, num_access_codes=nac, pid=pid,
+                     qam_order=qam, seed=611, snr_db=30.0)
+    S = Synthesizer(sp)
+    F, J, K = 2, 3, 4
+    lens, L = S.stream_layout(F, J)
+    iq = torch.zeros((F, N, L), dtype=torch.complex64, device="cuda")
+    tx = torch.zeros((F * K, N, pid, M), dtype=torch.uint8, device="cuda")
+    starts, _ = S.generate_streams(iq, L, F, J, K, tx_idx=tx)
+    rs = torch.from_numpy(starts.view(np.int64).copy()).cuda()
+    rot = iq.clone()
+    cfo_derotate(rot, L, F * N, L, 0, -eps, M)              # a CFO of +eps
+
+    def run(x, cfo):
+        rxo = Receiver(RxParams(M=M, cp_len=cp, num_streams=N, num_access_codes=nac,
+                                pid_max=pid, detector=_lib.DET_MMSE, qam_order=qam,
+                                cfo_correct=cfo))
+        rxo.process(x, L, L, F, max_out=pid, ref_mode=1, ref_idx=tx, frames_per_capture=K,
+                    ref_starts=rs)
+        torch.cuda.synchronize()
+        return rxo.results(F * K)
+
+    plain, corr = run(iq, False), run(rot, True)
+    ok = 0
+    for a_, b_ in zip(plain, corr):
+        assert a_["status"] == b_["status"] and a_["sync_index"] == b_["sync_index"]
+        assert a_["origin"] == b_["origin"]
+        if a_["status"] != _lib.FRAME_OK:
+            continue
+        ok += 1
+        assert abs(b_["cfo_eps"] - eps) < 2e-5, b_["cfo_eps"]
+        e0 = 10 * np.log10(np.sum(a_["evm_num"]) / np.sum(a_["evm_den"]))
+        e1 = 10 * np.log10(np.sum(b_["evm_num"]) / np.sum(b_["evm_den"]))
+        assert e1 - e0 <= 0.5, (e0, e1)
+    assert ok >= 2
+
+
 def _sc16_capture(iq, amax):
     """Quantise complex64 captures [F][N][L] to the sc16 wire format (int16 I/Q) at full scale
     amax, as a radio's ADC path would; returns the int16 tensor [F][N][L][2] and the scale."""
@@ -784,18 +872,20 @@ def _sc16_capture(iq, amax):
     return q.round_().clamp_(-32768, 32767).to(torch.int16).contiguous(), amax / 32767.0
 
 
-@pytest.mark.parametrize("geom", ["c3", "c3_streams", "c2", "m512"])
+@pytest.mark.parametrize("geom", ["c3", "c3_streams", "c2", "m512", "m512x8"])
 def test_sc16_batch_equals_widened_batch(geom):
     """mimo_batch.sample_format = SC16 (UHD wire samples read in place by the S&C, fused search
-    + LS and streaming decode kernels; other geometries widen internally) gives bit-identical
-    results to widening with mimo_ingest_sc16 first and running the complex64 path: sync,
-    corr indices, symbols, indices and EVM sums."""
+    + LS, streaming decode and 8x8 split decode kernels; other geometries widen internally)
+    gives bit-identical results to widening with mimo_ingest_sc16 first and running the
+    complex64 path: sync, corr indices, symbols, indices and EVM sums."""
     import torch
     from rub_mimo_amd.receiver import ingest_sc16
     if geom == "c2":
         M, cp, N, nac, pid, qam, det, F, K = 1024, 76, 2, 20, 200, 16, _lib.DET_ZF2, 4, 1
     elif geom == "m512":
         M, cp, N, nac, pid, qam, det, F, K = 512, 38, 2, 8, 100, 16, _lib.DET_ZF2, 4, 1
+    elif geom == "m512x8":     # 8x8 split decode (spectra_kernel<9> reads the wire samples)
+        M, cp, N, nac, pid, qam, det, F, K = 512, 38, 8, 4, 40, 64, _lib.DET_MMSE, 5, 1
     else:
         M, cp, N, nac, pid, qam, det, F, K = 2048, 152, 4, 20, 300, 64, _lib.DET_MMSE, 4, 1
     sp = SynthParams(M=M, cp_len=cp, num_streams=N, num_access_codes=nac, pid=pid,
