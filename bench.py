@@ -132,10 +132,14 @@ def spawn_ranks(args):
     return rc
 
 
-def decode_kernel_name(M, N, args):
-    """The decode kernel launch_decode picks for this configuration (decode_stream.hip /
-    decode_kernels.hip dispatch rules; all-carrier allocation, 16-byte aligned buffers)."""
+def decode_kernel_name(M, N, args, path=None):
+    """The decode kernel family launch_decode ran (mimo_rx_get_decode_path), named as rocprof
+    shows it; for the per-symbol family the dispatch rules of decode_kernels.hip pick it."""
     lg = M.bit_length() - 1
+    if path == 1:
+        return "decode_stream_kernel<%d,%d>" % (lg, N)
+    if path == 2:
+        return "spectra_kernel<%d>|apply_split_kernel<8>" % lg
     stream_ok = (os.environ.get("RMIMO_DECODE_STREAM", "1") != "0" and args.detector != "siso"
                  and args.qam <= 256 and (N, lg) in ((4, 11), (4, 10), (2, 12), (2, 11), (2, 10)))
     if stream_ok:
@@ -493,7 +497,7 @@ def main():
     dec_avg_s = dec_ms / max(dec_n, 1) / 1e3
     # per decoded symbol: N bodies read, N x M_occ complex64 + uint8 written (+ the uint8
     # transmitted index read when the EVM reference comes from HBM)
-    kname = decode_kernel_name(M, N, args)
+    kname = decode_kernel_name(M, N, args, rx.decode_path())
     # (sc16 is read in place by the streaming decode; other decode kernels read the widened copy)
     dec_in = in_bytes if kname.startswith("decode_stream") else 8
     per_sym = N * M * dec_in + N * m_occ * 9 + (N * m_occ if args.ref_mode == 1 else 0)

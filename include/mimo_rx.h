@@ -209,6 +209,15 @@ int mimo_rx_get_decode_path(const mimo_rx *h, int32_t *path);
  * (the reference's bounded window ring, framing.cc:387-388), so the capture stays near the
  * window size however long an unsynchronised stream runs. */
 int mimo_rx_get_stream_capacity(const mimo_rx *h, uint64_t *capacity, uint64_t *held);
+/* DEBUG_LOG (mimo/config.h:84-86, off by default here): the streaming execute writes the
+ * reference's debug traces into directory `dir` (NULL or "" turns them off):
+ *   f_sc_<k>.dat     float32 Schmidl-Cox metric y of every sample processed while seeking,
+ *                    antenna k from 1, appended per call (framing.cc:390-402, 598-600);
+ *   corr_<k>_<ac>.dat  float32 search metric over window indices [0, ACB - M), ac from 1, and
+ *                    corr_<k>_0.dat for S0 (framing.cc:675-696, 716-737, 873-883).
+ * The files mimo/apps/plot.py reads. Opening happens here (the reference opens them in its
+ * constructor); they are closed by the next call or mimo_rx_destroy. */
+int mimo_rx_set_debug_log(mimo_rx *h, const char *dir);
 
 /* ---------------- transmitter: framegen (framing.h:42-103) ---------------- */
 typedef struct mimo_tx mimo_tx;

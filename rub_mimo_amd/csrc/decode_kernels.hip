@@ -708,7 +708,7 @@ __global__ __launch_bounds__(256) void evm_kernel(EvmArgs a) {
   const uint64_t n = recs * a.parts;                // (record, part) entries, fixed order
   const uint64_t lo = n * ch / kEvmChunks, hi = n * (ch + 1) / kEvmChunks;
   const uint32_t g = tid / per, c = tid % per;
-  const double *src = a.evm_part + (uint64_t)f * a.max_out * a.parts * per;
+  const double *src = a.evm_part + (uint64_t)f * a.rec_stride * a.parts * per;
   double v = 0.0;
   if (g < G)
     for (uint64_t e = lo + g; e < hi; e += G) v += src[e * per + c];

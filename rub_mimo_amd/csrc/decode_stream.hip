@@ -301,7 +301,7 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
   constexpr int MS = WP::MS, LG = WP::LG, QS = WP::QS, GS = WP::GS;
   // subcarriers of a thread in the apply: k = S tid + q (adjacent: one S*8-byte symbol store and
   // one S-byte index store per stream) on the wave-FFT layout, else k = tid + q T
-  constexpr bool KADJ = WF && S == 2 && !CPE;
+  constexpr bool KADJ = WF && S == 2;
   constexpr int SPS = KADJ ? NA : NA * S;          // store instructions per output kind
   constexpr int NSTORE = ((OUTS & 1) ? SPS : 0) + ((OUTS & 2) ? SPS : 0);
   extern __shared__ __attribute__((aligned(16))) float2 lds_raw[];
@@ -624,13 +624,19 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
       }
     }
     if constexpr (CPE) {
-      if (a.cpe == 2) {   // folded CFO: the in-body part of the derotation
-        v2f c = cfo_ct;
+      // the symbol's phase correction, applied to its time samples (a constant rotation of
+      // the body turns every output by it, and costs one multiply per sample instead of one
+      // per output); folded CFO: times the in-body part of the derotation
+      if (a.cpe == 2) {
+        v2f c = cmul_pk(cfo_ct, rot);
 #pragma unroll
         for (int r = 0; r < 8; r++) {
           v[r] = cmul_pk(v[r], c);
           c = cmul_pk(c, cfo_w);
         }
+      } else {
+#pragma unroll
+        for (int r = 0; r < 8; r++) v[r] = cmul_pk(v[r], rot);
       }
     }
     MARK(";@@B pass0");
@@ -712,9 +718,11 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
 #ifdef DS_ABL_NODEMAP   // timing ablation: no demap / EVM
       return 0u;
 #endif
-      if constexpr (CPE) acc = cmul_pk(acc, rot);
       const uint32_t d = gidx[qam_level_pair_pk(acc, inv_sc, Lf, Lm1, a.qam.L)];
-      if constexpr (CPE) cpe_acc = cmac_pk(cpe_acc, v2f{ptab[d].x, -ptab[d].y}, acc);
+      // (the residual phase from the thread's first subcarrier of every stream: a quarter of the
+      // symbol's outputs at 4x4 measure it to far below the drift it tracks)
+      if constexpr (CPE)
+        if (q == 0) cpe_acc = cmac_pk(cpe_acc, v2f{ptab[d].x, -ptab[d].y}, acc);
       uint32_t refi;
       if constexpr (REF == 1) refi = (cref[(t * S + q) / 4] >> (8 * ((t * S + q) % 4))) & 0xFFu;
       else if constexpr (REF == 2)
@@ -830,12 +838,11 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
 //      its 64 subcarriers in registers (wave h: outputs 2h and 2h+1, 32 VGPRs) and streams
 //      the range's symbols through the 8x8 apply, demap, EVM and stores.
 // Weights are read once per (chunk, range) instead of once per symbol (the per-symbol kernel
-// reads 2 MB of W from L2 for every 256 KB symbol). The two kernels alternate over groups of
-// kSplitGroup symbols (a.sym0 .. + a.sym_cap) through one scratch of that many symbols per
-// frame (67 MB at C4 x 8): the spectra a group writes are read back by its apply while they
-// are still in the 256 MB Infinity Cache, and the next group overwrites the same lines, so
-// the round trip need not reach HBM. EVM records: symbol group x chunk x range per frame
-// (nrec), NA/2 per record.
+// reads 2 MB of W from L2 for every 256 KB symbol). The two kernels can alternate over groups
+// of symbols (a.sym0 .. + a.sym_cap) through one scratch of that many symbols per frame, so
+// that a group's spectra are read back while still in the 256 MB Infinity Cache
+// (RMIMO_SPLIT_GROUP, off by default: see split_group_symbols). EVM records: symbol group x
+// chunk x range per frame (nrec), NA/2 per record.
 constexpr uint32_t kSplitSets = 16;   // EVM partial sets per record (<= kMaxEvmParts)
 
 template <int LOG2M, int T, bool SC16>
@@ -990,7 +997,7 @@ __global__ __launch_bounds__(32 * NA) void apply_split_kernel(DecodeArgs a) {
     }
   // partial set ((grp * NCH + c) * P + part) * waves + h: this wave's two streams, zeros elsewhere
   const uint64_t set = (((uint64_t)grp * NCH + c) * P + part) * (T / 64) + h;
-  double *ep = a.evm_part + ((uint64_t)f * a.max_out * kSplitSets + set) * NA * 3;
+  double *ep = a.evm_part + ((uint64_t)f * a.rec_stride * kSplitSets + set) * NA * 3;
   if (lane < NA * 3) {
     const uint32_t t = lane / 3, comp = lane % 3;
     float v = 0.0f;
@@ -1008,21 +1015,36 @@ bool decode_split_accepts(const DecodeArgs &a, int log2M) {
          (a.ref_mode != 1 || ((uintptr_t)a.ref_idx & 15u) == 0);
 }
 
-uint32_t split_group_symbols(uint32_t max_out) { return std::min(kSplitGroup, max_out); }
+// symbols per group: every symbol in one group (the spectra of the whole batch in the
+// scratch) unless RMIMO_SPLIT_GROUP = G > 0 (the Infinity-Cache-sized groups, e.g. 32: measured
+// slower at C4 x 8 -- 2.10 vs 1.58 ms per decode -- because each group's apply re-reads its
+// chunk's weights, 16x the weight traffic, and each launch is a quarter of the chip)
+uint32_t split_group_symbols(uint32_t max_out) {
+  static const int env = [] { const char *e = getenv("RMIMO_SPLIT_GROUP"); return e ? atoi(e) : 0; }();
+  const uint32_t g = env <= 0 ? max_out : (uint32_t)env;
+  return std::max(1u, std::min(g, max_out));
+}
+
+// symbol groups, ranges per (group, chunk) and the EVM records per frame of the split decode:
+// ranges of ~8 symbols (four in flight per workgroup) so that each apply launch has enough
+// workgroups; records = groups * chunks * ranges * 4 waves / kSplitSets
+uint32_t split_plan(uint32_t max_out, int log2M, uint32_t *groups_out, uint32_t *P_out) {
+  const uint32_t NCH = (1u << log2M) / 64, cap = split_group_symbols(max_out);
+  const uint32_t groups = (max_out + cap - 1) / cap;
+  uint32_t P = std::max(1u, std::min(16u, cap / 8));
+  while ((groups * NCH * P * 4) % kSplitSets) P++;    // whole records (NCH * 4 >= 32: P as is)
+  if (groups_out) *groups_out = groups;
+  if (P_out) *P_out = P;
+  return groups * NCH * P * 4 / kSplitSets;
+}
 
 // 8x8 split decode; returns the partial sets per record (0: not handled)
 uint32_t launch_decode_split(const DecodeArgs &a, int log2M, uint32_t n_frames, hipStream_t s) {
   if (!a.spec || !a.nrec || !decode_split_accepts(a, log2M)) return 0;
   const uint32_t NCH = a.M / 64;
   const uint32_t cap = split_group_symbols(a.max_out);
-  const uint32_t groups = (a.max_out + cap - 1) / cap;
-  // symbol ranges per (group, chunk): many short workgroups (no tail round); records
-  // groups * NCH * P * 4 / kSplitSets <= max_out (the EVM partial space), whole records
-  uint32_t P = 16;
-  while (P > 0 && ((uint64_t)groups * NCH * P * 4 > (uint64_t)a.max_out * kSplitSets ||
-                   (groups * NCH * P * 4) % kSplitSets))
-    P--;
-  if (P == 0) return 0;
+  uint32_t groups = 0, P = 0;
+  if (split_plan(a.max_out, log2M, &groups, &P) > a.rec_stride) return 0;   // EVM space
   constexpr int T1 = 512;
   const size_t shm = sizeof(float2) * lds_padded_len(1 << log2M);
   DecodeArgs g = a;

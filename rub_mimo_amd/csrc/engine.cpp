@@ -251,6 +251,11 @@ struct mimo_rx {
   DevBuf<float2> capbuf;
   uint64_t cap_len = 0, total = 0, origin = 0;
   DevBuf<uint32_t> probe;               // trim probe: per antenna, a proven metric zero
+  // DEBUG_LOG files of the streaming execute (framing.cc:390-402, 598-600, 675-696, 873-883)
+  std::string dbg_dir;
+  std::vector<FILE *> dbg_fsc;
+  DevBuf<float> dbg_y, dbg_corr;
+  float *cur_corr_trace = nullptr;
   int state = MIMO_STATE_SEEK_PLATEAU;
   uint64_t nsp = 0;
   bool have_sync = false, have_est = false;
@@ -378,6 +383,8 @@ int run_sync(mimo_rx *h, const float2 *iq, uint64_t stride, uint32_t F, uint64_t
     a.band = band_env >= 0.0 ? band_env : sc_band(h->M);
     static const int diag_env = [] { const char *e = getenv("RMIMO_SC_DIAG"); return e ? atoi(e) : 0; }();
     a.diag = (uint32_t)diag_env;
+    static const bool split_env = [] { const char *e = getenv("RMIMO_SC_SPLIT"); return e && e[0] == '1'; }();
+    a.split_iters = split_env ? 1u : 0u;
     a.chunk_len = K; a.chunk_lo = chunk_lo; a.chunk_hi = nchunks;
     a.trig = h->trig.p; a.rec = h->rec.p; a.rec_stride = h->cap_chunks;
     a.cand = stream ? h->cand.p : nullptr;
@@ -536,6 +543,7 @@ int run_estimate(mimo_rx *h, const float2 *iq, uint64_t stride, uint32_t F, uint
   sa.codespec = h->codes.codespec.p; sa.vscale = h->vscale.p;
   sa.codespec_w = h->codes.codespec_w.p;
   sa.info = h->info.p; sa.keys = h->keys.p; sa.tw = h->tw;
+  sa.corr_trace = h->cur_corr_trace;
   LsArgs la{};
   la.iq = iq; la.stride = stride; la.frame_len = frame_len;
   la.N = h->N; la.M = h->M; la.nac = h->nac; la.n_slots = h->n_slots;
@@ -612,9 +620,10 @@ int run_decode(mimo_rx *h, const float2 *iq, uint64_t stride, uint32_t F, uint64
                uint32_t max_out, float2 *out_sym, uint8_t *out_idx, int ref_mode,
                const uint8_t *ref_idx, uint64_t ref_seed, uint64_t frame_id0, hipStream_t s,
                uint32_t n_caps = 0, const double *cfo_fold_part = nullptr) {
-  int rc = ensure_workspace(h, F, 0, (uint64_t)F * max_out * h->N * 3 * kMaxEvmParts);
-  if (rc) return rc;
-  if (max_out == 0) return MIMO_OK;
+  if (max_out == 0) {
+    int rc0 = ensure_workspace(h, F, 0, 0);
+    return rc0;
+  }
   DecodeArgs d{};
   d.iq = iq; d.stride = stride; d.frame_len = frame_len;
   d.sc16 = h->cur_sc16; d.iq_scale = h->cur_scale;
@@ -639,12 +648,19 @@ int run_decode(mimo_rx *h, const float2 *iq, uint64_t stride, uint32_t F, uint64
   d.cpe = h->cfo ? (cfo_fold_part ? 2 : 1) : 0;
   d.cfo_part = cfo_fold_part;
   static const bool no_split = [] { const char *e = getenv("RMIMO_DECODE_SPLIT"); return e && e[0] == '0'; }();
+  d.rec_stride = max_out;
   if (!no_split && decode_split_accepts(d, h->log2M)) {
     // [F][M/64][group][N][64] complex64 spectra of the 8x8 split decode (one symbol group)
     if (h->spec.ensure((size_t)F * split_group_symbols(max_out) * h->N * h->M) != hipSuccess)
       return fail(MIMO_ERR_NOMEM, "split decode scratch");
     d.spec = h->spec.p;
+    d.rec_stride = std::max(max_out, split_plan(max_out, h->log2M, nullptr, nullptr));
   }
+  {
+    const int rc0 = ensure_workspace(h, F, 0, (uint64_t)F * d.rec_stride * h->N * 3 * kMaxEvmParts);
+    if (rc0) return rc0;
+  }
+  d.evm_part = h->evm_part.p;
   bool per_frame = false;
   int path = MIMO_DECODE_NONE;
   const uint32_t parts = launch_decode(d, h->log2M, F, s, &per_frame, &path);
@@ -663,6 +679,7 @@ int run_decode(mimo_rx *h, const float2 *iq, uint64_t stride, uint32_t F, uint64
   EvmArgs ea{};
   ea.N = h->N; ea.max_out = max_out; ea.parts = parts; ea.info = h->info.p;
   ea.evm_part = h->evm_part.p;
+  ea.rec_stride = d.rec_stride;
   ea.evm_out = h->evm_out.p;
   ea.chunk_part = h->evm_chunk.p;
   ea.counter = h->evm_cnt.p;
@@ -684,6 +701,12 @@ extern "C" {
 
 const char *mimo_last_error(void) { return g_err.c_str(); }
 const char *mimo_version(void) { return "rub_mimo_amd 0.1.0 (gfx950)"; }
+
+static void close_debug_files(mimo_rx *h) {
+  for (FILE *f : h->dbg_fsc)
+    if (f) fclose(f);
+  h->dbg_fsc.clear();
+}
 
 int mimo_rx_create(const mimo_rx_config *cfg, void *hip_stream, mimo_rx **out) {
   if (!cfg || !out || !cfg->p || !cfg->s0_bits || !cfg->s1_bits)
@@ -798,6 +821,7 @@ int mimo_rx_create(const mimo_rx_config *cfg, void *hip_stream, mimo_rx **out) {
 int mimo_rx_destroy(mimo_rx *h) {
   if (!h) return MIMO_OK;
   if (h->stream) (void)hipStreamSynchronize(h->stream);
+  close_debug_files(h);
   for (auto &e : h->timer.ev) {
     (void)hipEventDestroy(e.second.first);
     (void)hipEventDestroy(e.second.second);
@@ -842,8 +866,10 @@ int mimo_rx_set_siso(mimo_rx *h, uint32_t tx, uint32_t rx) {
 // ---------------- streaming framesync::execute ----------------
 static int grow_capture(mimo_rx *h, uint64_t need) {
   if (need <= h->cap_len && h->capbuf.p) return MIMO_OK;
-  uint64_t nc = std::max<uint64_t>(need, h->cap_len * 2);
-  nc = std::max<uint64_t>(nc, 1 << 16);
+  // 1.5x growth in 16 K steps (the streaming capture is trimmed while seeking, so its size
+  // follows what is held plus one piece, not the stream length)
+  uint64_t nc = std::max<uint64_t>(need, h->cap_len + h->cap_len / 2);
+  nc = std::max<uint64_t>((nc + 16383) / 16384 * 16384, 1 << 16);
   float2 *np = nullptr;
   HIPCHK(hipMalloc(&np, sizeof(float2) * nc * h->N));
   if (h->capbuf.p && h->total) {
@@ -858,6 +884,31 @@ static int grow_capture(mimo_rx *h, uint64_t need) {
   return MIMO_OK;
 }
 
+// DEBUG_LOG: the search metric of every lag as the reference's corr_<rx>_<ac>.dat files, one
+// float per window index over [0, ACB - M): S0's lags at [0, SL) (corr_<rx>_0), access code
+// ac's at SL (ac + 1) + [0, SL) (framing.cc:716-737), zeros elsewhere
+static int write_corr_logs(mimo_rx *h) {
+  const size_t per = (size_t)h->n_slots * h->SL;
+  std::vector<float> tr((size_t)h->N * per);
+  HIPCHK(hipMemcpy(tr.data(), h->dbg_corr.p, sizeof(float) * tr.size(), hipMemcpyDeviceToHost));
+  const size_t len = h->acb - h->M;
+  std::vector<float> out(len);
+  for (uint32_t ch = 0; ch < h->N; ch++)
+    for (uint32_t slot = 0; slot < h->n_slots; slot++) {
+      std::fill(out.begin(), out.end(), 0.0f);
+      const size_t at = (size_t)h->SL * slot;
+      for (uint32_t i = 0; i < h->SL && at + i < len; i++) out[at + i] = tr[ch * per + (size_t)slot * h->SL + i];
+      const std::string fn = h->dbg_dir + "/corr_" + std::to_string(ch + 1) + "_" +
+                             std::to_string(slot) + ".dat";
+      FILE *fp = fopen(fn.c_str(), "wb");
+      if (!fp) return fail(MIMO_ERR_ARG, "cannot open " + fn);
+      const size_t w = fwrite(out.data(), sizeof(float), len, fp);
+      fclose(fp);
+      if (w != len) return fail(MIMO_ERR_ARG, "short write " + fn);
+    }
+  return MIMO_OK;
+}
+
 static int finish_estimate(mimo_rx *h) {
   // channel estimate + replay decode of the complete window; callbacks per OFDM symbol
   const float2 *iq = h->capbuf.p;
@@ -866,11 +917,18 @@ static int finish_estimate(mimo_rx *h) {
   h->sinfo.status = MIMO_FRAME_OK;
   HIPCHK(hipMemcpyAsync(h->info.p, &h->sinfo, sizeof(FrameInfo), hipMemcpyHostToDevice,
                         h->stream));
+  if (!h->dbg_dir.empty()) {
+    HIPCHK(h->dbg_corr.ensure((size_t)h->N * h->n_slots * h->SL));
+    HIPCHK(hipMemsetAsync(h->dbg_corr.p, 0, sizeof(float) * h->N * h->n_slots * h->SL, h->stream));
+    h->cur_corr_trace = h->dbg_corr.p;
+  }
   int rc = run_estimate(h, iq, h->cap_len, 1, h->total, h->stream);
+  h->cur_corr_trace = nullptr;
   if (rc) return rc;
   HIPCHK(hipMemcpyAsync(&h->sinfo, h->info.p, sizeof(FrameInfo), hipMemcpyDeviceToHost,
                         h->stream));
   HIPCHK(hipStreamSynchronize(h->stream));
+  if (!h->dbg_dir.empty() && (rc = write_corr_logs(h))) return rc;
   const uint32_t n_sym = h->sinfo.n_sym;
   const size_t per = (size_t)h->N * h->M_occ;
   if (n_sym) {
@@ -944,7 +1002,7 @@ static int maybe_trim(mimo_rx *h) {
   const uint64_t H = kScSpan - K;                     // halo of an S&C item
   const uint64_t c_lo = h->total / K;                 // the next S&C starts at this chunk
   const uint64_t need = H + 2 * (uint64_t)h->SL + 2 * (uint64_t)h->M + K;
-  if (c_lo * K < need + 4 * K) return MIMO_OK;        // not worth a move yet
+  if (c_lo * K < need + K) return MIMO_OK;            // nothing to drop yet
   const uint64_t D = (c_lo * K - need) / K * K;
   const int64_t lo = (int64_t)(D + h->SL + h->M), hi = (int64_t)(c_lo * K - H);
   if (hi - lo < (int64_t)K / 2) return MIMO_OK;
@@ -972,9 +1030,41 @@ static int maybe_trim(mimo_rx *h) {
   return MIMO_OK;
 }
 
+// At the trigger: nothing before the window start (base) is read again -- the S&C is done and
+// the search, LS and decode read [base, base + ACB + TX) -- so the capture is re-based there
+// into a buffer sized for the window (positions of the frame record shift with it).
+static int rebase_to_window(mimo_rx *h, uint64_t piece) {
+  const int64_t D = h->sinfo.base;
+  if (D <= 0) return MIMO_OK;
+  const uint64_t keep = h->total - (uint64_t)D;
+  uint64_t nc = std::max<uint64_t>(keep, h->win_len + piece + 64);
+  nc = (nc + 16383) / 16384 * 16384;
+  float2 *np = nullptr;
+  HIPCHK(hipMalloc(&np, sizeof(float2) * nc * h->N));
+  if (keep)
+    HIPCHK(hipMemcpy2DAsync(np, sizeof(float2) * nc, h->capbuf.p + D, sizeof(float2) * h->cap_len,
+                            sizeof(float2) * keep, h->N, hipMemcpyDeviceToDevice, h->stream));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  h->capbuf.release();
+  h->capbuf.p = np;
+  h->capbuf.n = nc * h->N;
+  h->cap_len = nc;
+  h->origin += (uint64_t)D;
+  h->total = keep;
+  FrameInfo &I = h->sinfo;   // (unsigned fields wrap consistently: getters add origin back)
+  I.base -= D;
+  I.trigger -= (uint64_t)D;
+  I.sync_index -= (uint64_t)D;
+  for (uint32_t a = 0; a < h->N; a++) {
+    I.plateau_start[a] -= (uint64_t)D;
+    I.plateau_end[a] -= (uint64_t)D;
+  }
+  return MIMO_OK;
+}
+
 // one piece of an execute call (at most a window's worth of samples)
 static int execute_piece(mimo_rx *h, const float *const *iq, uint64_t off, uint64_t n,
-                         uint64_t call_end) {
+                         uint64_t call_end, uint64_t piece) {
   if (h->state == MIMO_STATE_SEEK_PLATEAU && h->total) {
     int rc = maybe_trim(h);
     if (rc) return rc;
@@ -999,12 +1089,32 @@ static int execute_piece(mimo_rx *h, const float *const *iq, uint64_t off, uint6
     HIPCHK(hipMemcpyAsync(&h->sinfo, h->info.p, sizeof(FrameInfo), hipMemcpyDeviceToHost,
                           h->stream));
     HIPCHK(hipStreamSynchronize(h->stream));
+    if (!h->dbg_fsc.empty()) {
+      // DEBUG_LOG: y of every sample this piece processed while seeking, through the trigger
+      const uint64_t hi = h->sinfo.status == MIMO_FRAME_NO_SYNC ? h->total : h->sinfo.trigger + 1;
+      if (hi > old_total) {
+        const uint64_t cnt = hi - old_total;
+        HIPCHK(h->dbg_y.ensure(cnt * h->N));
+        launch_sc_trace(h->capbuf.p, h->cap_len, h->N, h->M, (int64_t)old_total, (int64_t)hi,
+                        h->dbg_y.p, h->stream);
+        HIPCHK(hipGetLastError());
+        std::vector<float> y(cnt * h->N);
+        HIPCHK(hipMemcpyAsync(y.data(), h->dbg_y.p, sizeof(float) * y.size(),
+                              hipMemcpyDeviceToHost, h->stream));
+        HIPCHK(hipStreamSynchronize(h->stream));
+        for (uint32_t a = 0; a < h->N; a++)
+          if (fwrite(y.data() + (size_t)a * cnt, sizeof(float), cnt, h->dbg_fsc[a]) != cnt)
+            return fail(MIMO_ERR_ARG, "short write of an f_sc debug file");
+      }
+    }
     if (h->sinfo.status == MIMO_FRAME_NO_SYNC) {
       h->nsp = h->origin + h->total;
       return MIMO_OK;
     }
     h->have_sync = true;
     h->state = MIMO_STATE_SAVE_ACCESS_CODES;
+    rc = rebase_to_window(h, piece);
+    if (rc) return rc;
   }
   // SAVE_ACCESS_CODES (framing.cc:639-651): estimate_channel runs at window sample n_e =
   // base + ACB + TX; a call that continues past it consumes one more sample in STATE_MIMO
@@ -1033,9 +1143,9 @@ int mimo_rx_execute(mimo_rx *h, const float *const *iq, uint32_t n_ant, uint64_t
   // long calls are taken a window at a time, so the capture stays bounded whatever the
   // caller's chunking (results are those of one call: the S&C is chunk-exact)
   const uint64_t call_end = h->origin + h->total + n;
-  const uint64_t piece = std::max<uint64_t>(h->win_len, 4 * sc_chunk_len(h->cp));
+  const uint64_t piece = std::max<uint64_t>(h->win_len / 2, 2 * sc_chunk_len(h->cp));
   for (uint64_t off = 0; off < n && h->state != MIMO_STATE_MIMO; off += piece) {
-    const int rc = execute_piece(h, iq, off, std::min<uint64_t>(piece, n - off), call_end);
+    const int rc = execute_piece(h, iq, off, std::min<uint64_t>(piece, n - off), call_end, piece);
     if (rc) return rc;
   }
   if (state_out) *state_out = h->state;
@@ -1177,8 +1287,7 @@ static uint32_t batch_fpc(const mimo_batch *b) {
 // form) and the streaming decode's CPE variant run: fc32 input (read in place or widened),
 // reference indices from HBM, both or neither output. Elsewhere the scratch passes remain.
 static bool cfo_folds(const mimo_rx *h, const mimo_batch *b, bool widened) {
-  if (!h->cfo || !h->search_ls || !h->codes.codespec_w.p || !search_ls_wave_enabled())
-    return false;
+  if (!h->cfo || !h->search_ls) return false;
   if (b->sample_format == MIMO_SAMPLE_SC16 && !widened) return false;
   static const bool off = [] { const char *e = getenv("RMIMO_CFO_FOLD"); return e && e[0] == '0'; }();
   if (off || b->ref_mode != 1 || (!b->d_out_sym) != (!b->d_out_idx)) return false;
@@ -1445,6 +1554,25 @@ int mimo_rx_batch_W(mimo_rx *h, float *W, uint32_t F) {
 int mimo_rx_set_timing(mimo_rx *h, int enable) {
   if (!h) return fail(MIMO_ERR_ARG, "null handle");
   h->timer.on = enable != 0;
+  return MIMO_OK;
+}
+
+int mimo_rx_set_debug_log(mimo_rx *h, const char *dir) {
+  if (!h) return fail(MIMO_ERR_ARG, "null handle");
+  close_debug_files(h);
+  h->dbg_dir.clear();
+  if (!dir || !dir[0]) return MIMO_OK;
+  h->dbg_dir = dir;
+  for (uint32_t a = 0; a < h->N; a++) {   // framing.cc:390-402: f_sc_<k>.dat, k from 1
+    const std::string fn = h->dbg_dir + "/f_sc_" + std::to_string(a + 1) + ".dat";
+    FILE *f = fopen(fn.c_str(), "wb");
+    if (!f) {
+      close_debug_files(h);
+      h->dbg_dir.clear();
+      return fail(MIMO_ERR_ARG, "cannot open " + fn);
+    }
+    h->dbg_fsc.push_back(f);
+  }
   return MIMO_OK;
 }
 

@@ -65,6 +65,13 @@ __global__ __launch_bounds__(kEstT) void codes_kernel(CodesArgs a) {
   }
 }
 
+// DEBUG_LOG trace (framing.cc:675-696, 873-883, opt-in): every lag's metric of (frame, rx, slot)
+MIMO_DEV void corr_trace_put(const SearchArgs &a, uint32_t f, uint32_t r, uint32_t slot,
+                             int64_t lag, float v) {
+  if (a.corr_trace && lag >= 0 && lag < (int64_t)a.SL)
+    a.corr_trace[(((uint64_t)f * a.N + r) * a.n_slots + slot) * a.SL + lag] = v;
+}
+
 // ------------------------------------------------------------------------------------
 template <int LOG2F>
 __global__ __launch_bounds__(kEstT) void search_kernel(SearchArgs a) {
@@ -99,6 +106,7 @@ __global__ __launch_bounds__(kEstT) void search_kernel(SearchArgs a) {
   unsigned long long best = 0ull;
   for (int i = tid; i < nl; i += kEstT) {
     const float v = cabs2(lds[lds_pad(i)]) * vs;
+    corr_trace_put(a, f, r, slot, lag0 + i, v);
     if (v > 0.0f) {
       const unsigned long long key =
           ((unsigned long long)__float_as_uint(v) << 32) |
@@ -179,6 +187,7 @@ void search_reg_kernel(SearchArgs a) {
   for (int e = 0; e < PTS; e++) {
     const int i = reg_index<LOG2F, PTS>(tid, e);
     const float val = (v[e].x * v[e].x + v[e].y * v[e].y) * vs;
+    if (i < nl) corr_trace_put(a, f, r, slot, lag0 + i, val);
     if (i < nl && val > 0.0f) {
       const unsigned long long key = ((unsigned long long)__float_as_uint(val) << 32) |
                                      (unsigned long long)(0xFFFFFFFFu - (uint32_t)(ws + i));
@@ -220,7 +229,7 @@ MIMO_DEV uint32_t key_index(unsigned long long k) {
 // (X / S1, S1 = +-1, framing.cc:811), stored per code in lsq[f][rx][tx][code][M] for
 // ls_combine_q_kernel's fixed-order sum. The separate LS pass re-read and re-transformed the
 // same windows; here the window is still in L2 from the segment load.
-template <int LOG2F, int LOG2M, bool SC16 = false>
+template <int LOG2F, int LOG2M, bool SC16 = false, bool CFO = false>
 __global__ __launch_bounds__((1 << LOG2F) / 16) __attribute__((amdgpu_waves_per_eu(4)))
 void search_ls_kernel(SearchArgs a) {
   constexpr int PTS = 16;
@@ -273,6 +282,19 @@ void search_ls_kernel(SearchArgs a) {
       if (n < 0 || n >= L) v[e] = v2f{0.0f, 0.0f};
     }
   }
+  double nu = 0.0;                                    // folded CFO: eps0 / M cycles per sample
+  if constexpr (CFO) {
+    // sample tid + e F/16 of the segment, relative to base: SL s0 + tid + e F/16
+    static_assert(PTS == 16 && PL::RM == 16, "reg_index = tid + e F/16");
+    nu = cfo_stage_eps(a.cfo_part, f, 1) / (double)M;
+    v2f rb = phasor_cycles(nu * (double)((int64_t)a.SL * s0 + tid));
+    const v2f st = phasor_cycles(nu * (double)(F / 16));
+#pragma unroll
+    for (int e = 0; e < PTS; e++) {
+      v[e] = vmul(v[e], rb);
+      rb = vmul(rb, st);
+    }
+  }
   v2f w1[PL::NTW > 0 ? PL::NTW : 1];
   reg_twiddles<LOG2F, PTS>(w1, a.tw, tid);
   // LS transform: register-resident (M/8 threads and 8 points per window, one window per half
@@ -309,6 +331,7 @@ void search_ls_kernel(SearchArgs a) {
     for (int e = 0; e < PTS; e++) {
       const int i = reg_index<LOG2F, PTS>(tid, e) - off;
       const float val = (v[e].x * v[e].x + v[e].y * v[e].y) * vs;
+      corr_trace_put(a, f, r, slot, i, val);
       if (i >= 0 && i < (int)a.SL && val > 0.0f) {
         const unsigned long long key = ((unsigned long long)__float_as_uint(val) << 32) |
                                        (unsigned long long)(0xFFFFFFFFu - (ws + (uint32_t)i));
@@ -350,6 +373,15 @@ void search_ls_kernel(SearchArgs a) {
       const float2 t = xs.at(n < 0 ? 0 : (n >= L ? L - 1 : n));   // clamped, masked below
       xw[e] = ok ? v2f{t.x, t.y} : v2f{0.0f, 0.0f};
     }
+    if constexpr (CFO) {   // window sample lt + e M/8, relative to base
+      v2f rb = phasor_cycles(nu * (double)(wb - I.base + (int64_t)lt));
+      const v2f st = phasor_cycles(nu * (double)(M / 8));
+#pragma unroll
+      for (int e = 0; e < 8; e++) {
+        xw[e] = vmul(xw[e], rb);
+        rb = vmul(rb, st);
+      }
+    }
     v2f wm[PM::NTW > 0 ? PM::NTW : 1];
     reg_twiddles<LOG2M, 8>(wm, a.tw, (int)lt);
     reg_compute<LOG2M, 8, 0, false>(xw, wm);
@@ -374,6 +406,10 @@ void search_ls_kernel(SearchArgs a) {
     const int64_t n = (u ? w1v : w0) + j;
     const bool ok = (u ? valid1 : valid0) && n >= 0 && n < L;
     win[e] = ok ? xs.at(n) : make_float2(0.0f, 0.0f);
+    if constexpr (CFO) {
+      const v2f w = vmul(v2f{win[e].x, win[e].y}, phasor_cycles(nu * (double)(n - I.base)));
+      win[e] = make_float2(w.x, w.y);
+    }
   }
   float2 *lb = reinterpret_cast<float2 *>(buf);
 #pragma unroll
@@ -393,6 +429,32 @@ void search_ls_kernel(SearchArgs a) {
     const float2 Xk = lb[u * PBM + lds_pad(k)];
     const int s = sg[k];
     q[k] = s > 0 ? Xk : (s < 0 ? cneg(Xk) : make_float2(0.0f, 0.0f));
+  }
+}
+
+// w[q] = w1^q for q < R (w[0] unused), at most three roundings deep (as reg_compute)
+template <int R>
+MIMO_DEV void twiddle_powers(v2f *w, v2f w1) {
+  w[1] = w1;
+  if constexpr (R >= 4) {
+    w[2] = vmul(w[1], w[1]);
+    w[3] = vmul(w[2], w[1]);
+  }
+  if constexpr (R >= 8) {
+    w[4] = vmul(w[2], w[2]);
+    w[5] = vmul(w[4], w[1]);
+    w[6] = vmul(w[3], w[3]);
+    w[7] = vmul(w[4], w[3]);
+  }
+  if constexpr (R == 16) {
+    w[8] = vmul(w[4], w[4]);
+    w[9] = vmul(w[8], w[1]);
+    w[10] = vmul(w[5], w[5]);
+    w[11] = vmul(w[8], w[3]);
+    w[12] = vmul(w[6], w[6]);
+    w[13] = vmul(w[8], w[5]);
+    w[14] = vmul(w[7], w[7]);
+    w[15] = vmul(w[8], w[7]);
   }
 }
 
@@ -488,9 +550,10 @@ void search_ls_wave_kernel(SearchArgs a) {
     for (int i = 0; i < NB; i++) {
       dft_small<B, false>(v + i * B);
       const int n = tid + T * i;
+      v2f w[B > 1 ? B : 2];
+      twiddle_powers<B>(w, twiddle<false>(a.tw, n * (kTwN / F)));
 #pragma unroll
-      for (int q = 1; q < B; q++)
-        v[i * B + q] = vmul(v[i * B + q], twiddle<false>(a.tw, ((n * q) & (F - 1)) * (kTwN / F)));
+      for (int q = 1; q < B; q++) v[i * B + q] = vmul(v[i * B + q], w[q]);
 #pragma unroll
       for (int q = 0; q < B; q++) buf[q * RB + lds_pad(n)] = v[i * B + q];
     }
@@ -524,9 +587,10 @@ void search_ls_wave_kernel(SearchArgs a) {
         asm volatile("" : "+v"(n));
 #pragma unroll
         for (int q = 0; q < B; q++) v[i * B + q] = buf[q * RB + lds_pad(n)];
+        v2f w[B > 1 ? B : 2];
+        twiddle_powers<B>(w, twiddle<true>(a.tw, n * (kTwN / F)));
 #pragma unroll
-        for (int q = 1; q < B; q++)
-          v[i * B + q] = vmul(v[i * B + q], twiddle<true>(a.tw, ((n * q) & (F - 1)) * (kTwN / F)));
+        for (int q = 1; q < B; q++) v[i * B + q] = vmul(v[i * B + q], w[q]);
         dft_small<B, true>(v + i * B);
       }
     }
@@ -540,6 +604,7 @@ void search_ls_wave_kernel(SearchArgs a) {
       const int m = (B > 1) ? tid + T * (e / B) + 1024 * (e % B) : reg_index<10, 16>(lane, e);
       const int i = m - off;
       const float val = (v[e].x * v[e].x + v[e].y * v[e].y) * vs;
+      corr_trace_put(a, f, r, slot, i, val);
       if (i >= 0 && i < (int)a.SL && val > 0.0f) {
         const unsigned long long key = ((unsigned long long)__float_as_uint(val) << 32) |
                                        (unsigned long long)(0xFFFFFFFFu - (ws + (uint32_t)i));
@@ -1194,8 +1259,10 @@ static bool search_ls_try(const SearchArgs &a, int log2F, int log2M, uint32_t nf
                                           : search_ls_wave_kernel<LOG2F, LOG2M, false>);
           }
           if (!kern)
-            kern = a.sc16 ? search_ls_kernel<LOG2F, LOG2M, true>
-                          : search_ls_kernel<LOG2F, LOG2M, false>;
+            kern = a.cfo_part ? (a.sc16 ? search_ls_kernel<LOG2F, LOG2M, true, true>
+                                        : search_ls_kernel<LOG2F, LOG2M, false, true>)
+                              : (a.sc16 ? search_ls_kernel<LOG2F, LOG2M, true>
+                                        : search_ls_kernel<LOG2F, LOG2M, false>);
           (void)hipFuncSetAttribute((const void *)kern,
                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
           dim3 grid(((a.n_slots + 1) / 2) * a.N, nf);
@@ -1211,9 +1278,9 @@ static bool search_ls_try(const SearchArgs &a, int log2F, int log2M, uint32_t nf
   return false;
 }
 
-bool search_ls_wave_enabled() {
-  static const bool off = [] { const char *e = getenv("RMIMO_SEARCH_WAVE"); return e && e[0] == '0'; }();
-  return !off;
+bool search_ls_wave_enabled() {   // RMIMO_SEARCH_WAVE=1 (measured slower at C2/C3: A/B only)
+  static const bool on = [] { const char *e = getenv("RMIMO_SEARCH_WAVE"); return e && e[0] == '1'; }();
+  return on;
 }
 
 bool search_ls_supported(int log2F, int log2M) {

@@ -68,6 +68,7 @@ struct ScArgs {
   unsigned long long *cand;
   int no_skip;
   uint32_t diag;            // diagnostics (RMIMO_SC_DIAG bits 8/16: skip in-place resolve/finalize)
+  uint32_t split_iters;     // sc_exact_kernel: one workgroup per (antenna, iteration) (else per antenna)
 };
 
 // S&C screen over antenna 0 (sc_screen_kernel): blocks of kScrB positions, kScrSpan positions
@@ -139,6 +140,10 @@ void launch_plateau(const PlateauArgs &a, uint32_t n_frames, hipStream_t s);
 // back-to-back frames per capture: the re-arm walk over the chunk candidates, the re-arm
 // certificates of frames k >= 1 and the chain fix-up (see sync_kernels.hip)
 void launch_stream_walk(const PlateauArgs &a, uint32_t n_caps, hipStream_t s);
+// DEBUG_LOG: the oracle-exact fp32 metric y of positions [lo, hi) of every antenna row
+// (framing.cc:598-600), out[row][i]
+void launch_sc_trace(const float2 *iq, uint64_t stride, uint32_t rows, uint32_t M, int64_t lo,
+                     int64_t hi, float *out, hipStream_t s);
 
 // access-code search, framing.cc:702-744 (est_kernels.hip)
 struct SearchArgs {
@@ -160,12 +165,13 @@ struct SearchArgs {
   uint32_t nac;
   uint32_t xcd_order;              // search_ls_kernel: slot pair slowest within each XCD
   const double *cfo_part;          // opt-in CFO, folded: derotate the loads by stage 1 (or null)
+  float *corr_trace;               // DEBUG_LOG: [F][N][n_slots][SL] every lag's metric (or null)
 };
 void launch_search(const SearchArgs &a, int log2F, uint32_t n_frames, hipStream_t s);
 // true when (log2F, log2M) has a search_ls_kernel instance (it then ran)
 bool launch_search_ls(const SearchArgs &a, int log2F, int log2M, uint32_t n_frames, hipStream_t s);
 bool search_ls_supported(int log2F, int log2M);
-// the wave-local form of search_ls_kernel (F >= 1024) is on (RMIMO_SEARCH_WAVE=0: off)
+// the wave-local form of search_ls_kernel (F >= 1024) is on (RMIMO_SEARCH_WAVE=1; off by default)
 bool search_ls_wave_enabled();
 
 // LS estimate, framing.cc:797-824 (+ training residual noise variance)
@@ -264,6 +270,7 @@ struct DecodeArgs {
   uint32_t *nrec;                  // [F] EVM records per frame (decode_stream_kernel) or null
   float2 *spec;                    // split decode (8x8) spectra scratch [F][M/64][sym_cap][N][64]
   uint32_t sym0, sym_cap, sym_groups;   // split decode: this launch's symbol group (set inside)
+  uint32_t rec_stride;             // EVM records per frame in evm_part (max_out, or the split's)
   int cpe;                         // opt-in CFO: decision-directed common-phase tracking; 2 =
                                    // folded: the kernel also derotates by the frame's estimate
   const double *cfo_part;          // folded CFO: the stage partials (cfo_stage_eps)
@@ -281,13 +288,14 @@ uint32_t launch_decode_stream(const DecodeArgs &a, int log2M, uint32_t n_frames,
 // true when launch_decode_stream takes this configuration (nrec aside): the sc16 wire input
 // is decoded only there
 bool decode_stream_accepts(const DecodeArgs &a, int log2M, uint32_t n_frames);
-// decode_stream.hip: 8x8 split form (spectra to a scratch, then a chunked apply, alternating
-// over groups of kSplitGroup symbols); 0 when the configuration is not handled or a.spec is
-// null. The scratch holds split_group_symbols(max_out) symbols per frame.
-constexpr uint32_t kSplitGroup = 32;
+// decode_stream.hip: 8x8 split form (spectra to a scratch, then a chunked apply, optionally
+// alternating over symbol groups); 0 when the configuration is not handled or a.spec is null.
+// The scratch holds split_group_symbols(max_out) symbols per frame.
 uint32_t launch_decode_split(const DecodeArgs &a, int log2M, uint32_t n_frames, hipStream_t s);
 bool decode_split_accepts(const DecodeArgs &a, int log2M);
 uint32_t split_group_symbols(uint32_t max_out);
+// the split decode's symbol groups, symbol ranges per (group, chunk) and EVM records per frame
+uint32_t split_plan(uint32_t max_out, int log2M, uint32_t *groups, uint32_t *P);
 constexpr uint32_t kMaxEvmParts = 16;
 
 struct EvmArgs {
@@ -299,6 +307,7 @@ struct EvmArgs {
   double *chunk_part;              // [F][kEvmChunks][N][3]
   uint32_t *counter;               // [F] chunks done, zero between launches (self-resetting)
   const uint32_t *nrec;            // [F] records per frame (streaming decode) or null: n_sym
+  uint32_t rec_stride;             // records per frame in evm_part (DecodeArgs::rec_stride)
 };
 constexpr uint32_t kEvmChunks = 16;
 void launch_evm(const EvmArgs &a, uint32_t n_frames, hipStream_t s);

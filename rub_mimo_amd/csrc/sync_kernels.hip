@@ -1531,8 +1531,14 @@ void sc_exact_kernel(ScArgs a) {
   __shared__ unsigned long long s_min;
   const uint32_t count = min(*a.hot_count, a.hot_cap);
   const uint32_t item0 = a.item_lo ? *a.item_lo : 0u;   // items of earlier screen phases: done
-  const uint32_t s = blockIdx.x;   // antenna fastest: an item's passes are dispatched together,
-                                   // ahead of the grid's empty tail
+  // one (antenna, iteration) of an item per workgroup, iteration fastest: an item's passes are
+  // dispatched together, ahead of the grid's empty tail. Each iteration starts from its own
+  // window sums (history of M samples), so an item's iterations run side by side instead of
+  // one after the other: the item's critical path is one iteration, not four.
+  // (a.split_iters = 0: one workgroup per antenna walks the item's iterations in turn)
+  const uint32_t IT = a.split_iters ? kScIters : 1u;
+  const uint32_t s = blockIdx.x / IT;
+  const int itw = (int)(blockIdx.x % IT);
   for (uint32_t slot = item0 + blockIdx.y; slot < count; slot += gridDim.y) {
   ScHot *hp = a.hot + slot;
   const int tid = threadIdx.x;
@@ -1550,11 +1556,19 @@ void sc_exact_kernel(ScArgs a) {
   int it_hi = (int)std::min<int64_t>(kScIters - 1, (fmax - w0) / kScIt);
   const auto x = iq_row<S>(a.iq, a.iq_scale, ((uint64_t)f * a.N + s) * a.stride);
   const bool vec = x.pair_ok();
-  const int64_t ib_lo = w0 + (int64_t)it_lo * kScIt;   // first evaluated position
-  if (tid == 0) hp->lo[s] = ib_lo;
-  for (int it = 0; it < kScIters; it++)
-    if (it < it_lo || it > it_hi) hp->wbits[((int)s * kScIters + it) * kScT + tid] = 0;
-  // history [ib_lo - M, ib_lo) -> its ring slots; the first block in flight behind it
+  if (tid == 0 && itw == 0) hp->lo[s] = w0 + (int64_t)it_lo * kScIt;   // first evaluated position
+  bool active = true;
+  if (a.split_iters) {
+    active = itw >= it_lo && itw <= it_hi;            // uniform
+    if (!active) hp->wbits[((int)s * kScIters + itw) * kScT + tid] = 0;
+    it_lo = it_hi = itw;                              // this workgroup's iteration
+  } else {
+    for (int it = 0; it < kScIters; it++)
+      if (it < it_lo || it > it_hi) hp->wbits[((int)s * kScIters + it) * kScT + tid] = 0;
+  }
+  const int64_t ib_lo = w0 + (int64_t)it_lo * kScIt;
+  if (active) {
+  // history [ib_lo - M, ib_lo) -> its ring slots; the block in flight behind it
   const int wb = (kScIt * it_lo) % RING;
   if (vec && ib_lo - M >= 0 && ib_lo <= L) {
     // all history pairs in flight together, then the ring writes
@@ -1782,6 +1796,7 @@ void sc_exact_kernel(ScArgs a) {
     hp->wbits[((int)s * kScIters + it) * kScT + tid] = (uint16_t)bits;
     __syncthreads();   // every lane's phase B reads of the ring precede the next block's writes
   }
+  }   // active
   // the item's last antenna pass: plateau rule over every antenna's words
   if (a.prof && tid == 0) {
     const unsigned long long t = (unsigned long long)wall_clock64();
@@ -1800,7 +1815,7 @@ void sc_exact_kernel(ScArgs a) {
   __syncthreads();
   if (tid == 0)
     s_last = (__hip_atomic_fetch_add(&hp->arrived, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) ==
-              hp->n_done - 1u) ? 1 : 0;
+              hp->n_done * IT - 1u) ? 1 : 0;
   __syncthreads();
   if (s_last && !(a.diag & 16)) {
     // the acquire of the arrival counter (agent scope) invalidated this CU's L1: plain 16-byte
@@ -1938,7 +1953,24 @@ void launch_sc_exact(const ScArgs &a, hipStream_t s) {
                               (int)shm);
     set_shm[v] = shm;
   }
-  hipLaunchKernelGGL(kern, dim3(a.N, std::min<uint32_t>(a.hot_cap, 256)), dim3(kScT), shm, s, a);
+  hipLaunchKernelGGL(kern, dim3(a.N * (a.split_iters ? kScIters : 1),
+                                 std::min<uint32_t>(a.hot_cap, 256)), dim3(kScT), shm, s, a);
+}
+
+__global__ __launch_bounds__(256) void sc_trace_kernel(const float2 *iq, uint64_t stride,
+                                                       uint32_t M, int64_t lo, int64_t n,
+                                                       float *out) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  out[(uint64_t)blockIdx.y * n + i] = sc_exact(iq + (uint64_t)blockIdx.y * stride, lo + i, M);
+}
+
+void launch_sc_trace(const float2 *iq, uint64_t stride, uint32_t rows, uint32_t M, int64_t lo,
+                     int64_t hi, float *out, hipStream_t s) {
+  if (hi <= lo || rows == 0) return;
+  const int64_t n = hi - lo;
+  hipLaunchKernelGGL(sc_trace_kernel, dim3((uint32_t)((n + 255) / 256), rows), dim3(256), 0, s,
+                     iq, stride, M, lo, n, out);
 }
 
 void launch_plateau(const PlateauArgs &a, uint32_t n_frames, hipStream_t s) {

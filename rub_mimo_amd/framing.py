@@ -282,6 +282,13 @@ class framesync:
     def reset(self):
         check(lib().mimo_rx_reset(self._h), "reset")
 
+    def set_debug_log(self, directory):
+        """DEBUG_LOG (mimo/config.h:84-86): write the reference's f_sc_<k>.dat and
+        corr_<k>_<ac>.dat traces into `directory` (None: off), the files mimo/apps/plot.py
+        reads (mimo_rx_set_debug_log)."""
+        d = None if directory is None else str(directory).encode()
+        check(lib().mimo_rx_set_debug_log(self._h, d), "set_debug_log")
+
     def stream_capacity(self):
         """(device capture capacity, samples held) per antenna of the streaming execute
         (mimo_rx_get_stream_capacity; diagnostic)."""
