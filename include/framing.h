@@ -221,6 +221,10 @@ class framesync {
     c.qam_order = 4;
     if (mimo_rx_create(&c, nullptr, &h_) != MIMO_OK) detail::die("framesync");
     mimo_rx_set_callback(h_, &framesync::bridge, this);
+    // DEBUG_LOG (config.h:84-86 writes /tmp/f_sc_*, /tmp/corr_*): off unless the environment
+    // names a directory, RMIMO_DEBUG_LOG=/tmp for the reference's behaviour
+    if (const char *d = std::getenv("RMIMO_DEBUG_LOG"))
+      if (d[0] && mimo_rx_set_debug_log(h_, d) != MIMO_OK) detail::die("framesync debug log");
   }
   ~framesync() { mimo_rx_destroy(h_); }
   framesync(const framesync &) = delete;

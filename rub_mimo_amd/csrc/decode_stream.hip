@@ -538,7 +538,10 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
   // rotation) -- the derotation the scratch passes of the unfolded path applied
   // (the body start's phasor rides in rot: set at each frame segment's first symbol, advanced
   // by cfo_e per symbol, corrected by the CPE as before)
-  v2f cfo_ct = v2f{1.0f, 0.0f}, cfo_w = v2f{1.0f, 0.0f};   // exp(-j2pi nu t0%W8), exp(-j2pi nu W8)
+  // (the thread's in-body phasor exp(-j2pi nu t0%W8) is recomputed per symbol from nu in an
+  // SGPR: fp32 is exact enough over one body, |nu t0%W8| < 1/8 cycle for |eps| < 1)
+  float cfo_nu = 0.0f;                                      // nu, cycles per sample
+  v2f cfo_w = v2f{1.0f, 0.0f};                              // exp(-j2pi nu W8)
   v2f cfo_e = v2f{1.0f, 0.0f};                              // exp(-j2pi nu SL)
   auto cfo_frame = [&](uint32_t ff, uint32_t ss) {
     if constexpr (CPE) {
@@ -553,7 +556,7 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
           sincospif((float)p, &sn, &cs);
           return v2f{cs, sn};
         };
-        cfo_ct = ph(nu * (double)(opq(tid) % W8));
+        cfo_nu = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int((float)nu)));
         cfo_w = uni(ph(nu * (double)W8));
         cfo_e = uni(ph(nu * (double)a.SL));
         rot = uni(ph(nu * (double)((int64_t)J.i0 + a.cp + (int64_t)ss * a.SL)));
@@ -581,7 +584,7 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
         if (m2 > 0.0f) {
           const float inv = 1.0f / sqrtf(m2);
           const v2f u = v2f{c.x * inv, -c.y * inv};
-          rot = v2f{rot.x * u.x - rot.y * u.y, rot.x * u.y + rot.y * u.x};
+          rot = uni(v2f{rot.x * u.x - rot.y * u.y, rot.x * u.y + rot.y * u.x});
         }
       }
     }
@@ -628,7 +631,9 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
       // the body turns every output by it, and costs one multiply per sample instead of one
       // per output); folded CFO: times the in-body part of the derotation
       if (a.cpe == 2) {
-        v2f c = cmul_pk(cfo_ct, rot);
+        float sn, cs;
+        sincospif(-2.0f * cfo_nu * (float)(opq(tid) % W8), &sn, &cs);
+        v2f c = cmul_pk(v2f{cs, sn}, rot);
 #pragma unroll
         for (int r = 0; r < 8; r++) {
           v[r] = cmul_pk(v[r], c);

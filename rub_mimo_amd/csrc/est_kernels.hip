@@ -1278,8 +1278,8 @@ static bool search_ls_try(const SearchArgs &a, int log2F, int log2M, uint32_t nf
   return false;
 }
 
-bool search_ls_wave_enabled() {   // RMIMO_SEARCH_WAVE=1 (measured slower at C2/C3: A/B only)
-  static const bool on = [] { const char *e = getenv("RMIMO_SEARCH_WAVE"); return e && e[0] == '1'; }();
+bool search_ls_wave_enabled() {   // on; RMIMO_SEARCH_WAVE=0 is the A/B switch back to the block form
+  static const bool on = [] { const char *e = getenv("RMIMO_SEARCH_WAVE"); return !(e && e[0] == '0'); }();
   return on;
 }
 

@@ -171,7 +171,7 @@ void launch_search(const SearchArgs &a, int log2F, uint32_t n_frames, hipStream_
 // true when (log2F, log2M) has a search_ls_kernel instance (it then ran)
 bool launch_search_ls(const SearchArgs &a, int log2F, int log2M, uint32_t n_frames, hipStream_t s);
 bool search_ls_supported(int log2F, int log2M);
-// the wave-local form of search_ls_kernel (F >= 1024) is on (RMIMO_SEARCH_WAVE=1; off by default)
+// the wave-local form of search_ls_kernel (F >= 1024) is on (default; RMIMO_SEARCH_WAVE=0 turns it off)
 bool search_ls_wave_enabled();
 
 // LS estimate, framing.cc:797-824 (+ training residual noise variance)

@@ -545,6 +545,26 @@ def test_c2_2x2_zf_1024_16qam_full_frame():
     assert np.all(e < -15)
 
 
+def test_block_search_form_matches_oracle():
+    """The wave-local search_ls_wave_kernel is the default for F >= 1024; the block-exchange
+    search_ls_kernel stays behind RMIMO_SEARCH_WAVE=0 (read once per process, so a child
+    interpreter runs the same C2/C3 parity cases with it)."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = ("import sys; sys.path.insert(0, %r); sys.path.insert(0, %r)\n"
+            "import test_gpu as t\nfrom rub_mimo_amd import _lib\n"
+            "t._c_frame_parity(1024, 76, 2, 20, 200, 16, _lib.DET_ZF2, 25.0, seed=21)\n"
+            "t._c_frame_parity(2048, 152, 4, 20, 60, 64, _lib.DET_MMSE, 30.0, seed=31,"
+            " path=_lib.DECODE_STREAM, out_idx=True)\nprint('block-search parity ok')\n"
+            % (root, os.path.join(root, "tests")))
+    env = dict(os.environ, RMIMO_SEARCH_WAVE="0")
+    out = subprocess.run([sys.executable, "-c", code], env=env, cwd=root, timeout=100,
+                         capture_output=True, text=True)
+    assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-4000:]
+    assert "block-search parity ok" in out.stdout
+
+
 def test_c3_4x4_mmse_2048_64qam_full_frame():
     """BASELINE config C3 at full size (PID 1000): the oracle needs ~20 s of CPU."""
     d, e = _c_frame_parity(2048, 152, 4, 20, 1000, 64, _lib.DET_MMSE, 30.0, seed=31,
