@@ -104,32 +104,48 @@ __global__ __launch_bounds__(kCfoThreads) void cfo_batch_est_kernel(CfoBatchArgs
   const int64_t L = (int64_t)a.frame_len;
   // folded path: no scratch, stage 2 reads the raw samples (below)
   const float2 *src = (STAGE == 1 || a.fold) ? a.iq : a.out;
-  if (live) {
+  if (live && STAGE == 1) {
     for (uint32_t r = 0; r < a.N; r++) {
       const float2 *row = src + ((uint64_t)I.cap * a.N + r) * a.stride;
-      if (STAGE == 1) {
-        const uint32_t half = a.M / 2;
-        const int64_t start = (int64_t)I.trigger - (int64_t)a.M + 1;
-        for (uint32_t n = b * kCfoThreads + threadIdx.x; n < half; n += kCfoBlocks * kCfoThreads) {
-          const int64_t k = start + n;
-          if (k < 0 || k + half >= L) continue;
-          const float2 u = row[k], v = row[k + half];
-          re += (double)u.x * v.x + (double)u.y * v.y;
-          im += (double)u.x * v.y - (double)u.y * v.x;
-        }
-      } else {
-        const uint32_t inner = a.cp > 2 * kCfoMargin ? a.cp - 2 * kCfoMargin : 0;
-        const int64_t d0 = I.base + cfo_i0(a, f);             // data symbol 0's prefix
-        for (uint32_t sym = b; sym < a.n_data; sym += kCfoBlocks) {
-          const int64_t c0 = d0 + (int64_t)sym * a.SL + kCfoMargin;
-          for (uint32_t n = threadIdx.x; n < inner; n += kCfoThreads) {
-            const int64_t k = c0 + n;
-            if (k < 0 || k + a.M >= L) continue;
-            const float2 u = row[k], v = row[k + a.M];
-            re += (double)u.x * v.x + (double)u.y * v.y;
-            im += (double)u.x * v.y - (double)u.y * v.x;
-          }
-        }
+      const uint32_t half = a.M / 2;
+      const int64_t start = (int64_t)I.trigger - (int64_t)a.M + 1;
+      for (uint32_t n = b * kCfoThreads + threadIdx.x; n < half; n += kCfoBlocks * kCfoThreads) {
+        const int64_t k = start + n;
+        if (k < 0 || k + half >= L) continue;
+        const float2 u = row[k], v = row[k + half];
+        re += (double)u.x * v.x + (double)u.y * v.y;
+        im += (double)u.x * v.y - (double)u.y * v.x;
+      }
+    }
+  } else if (live) {
+    // the block's symbols sym = b + kCfoBlocks j, every antenna, the prefix interiors: items
+    // (j, r, n) flattened (n fastest) and taken U at a time with all 2U loads issued before the
+    // sums (a symbol-by-symbol loop waited one memory latency per symbol and antenna)
+    const uint32_t inner = a.cp > 2 * kCfoMargin ? a.cp - 2 * kCfoMargin : 0;
+    const int64_t d0 = I.base + cfo_i0(a, f);               // data symbol 0's prefix
+    const uint32_t nsym = a.n_data > b ? (a.n_data - b + kCfoBlocks - 1) / kCfoBlocks : 0u;
+    const uint32_t per_sym = a.N * inner, total = nsym * per_sym;
+    const float2 *cap = src + (uint64_t)I.cap * a.N * a.stride;
+    constexpr int U = 8;
+    for (uint32_t j0 = threadIdx.x; j0 < total; j0 += U * kCfoThreads) {
+      float2 u[U], v[U];
+      bool ok[U];
+#pragma unroll
+      for (int e = 0; e < U; e++) {
+        const uint32_t j = j0 + (uint32_t)e * kCfoThreads;
+        const uint32_t js = j / per_sym, jr = j % per_sym, r = jr / inner, n = jr % inner;
+        const int64_t k = d0 + (int64_t)(b + js * kCfoBlocks) * a.SL + kCfoMargin + n;
+        ok[e] = j < total && k >= 0 && k + a.M < L;
+        const float2 *row = cap + (uint64_t)(ok[e] ? r : 0u) * a.stride;
+        const int64_t kk = ok[e] ? k : 0;
+        u[e] = row[kk];
+        v[e] = row[kk + (ok[e] ? a.M : 0)];
+      }
+#pragma unroll
+      for (int e = 0; e < U; e++) {
+        if (!ok[e]) continue;
+        re += (double)u[e].x * v[e].x + (double)u[e].y * v[e].y;
+        im += (double)u[e].x * v[e].y - (double)u[e].y * v[e].x;
       }
     }
   }

@@ -252,7 +252,7 @@ MIMO_DEV gptr<P> sgpr_ptr(P *p) {
   return (gptr<P>)(((uint64_t)hi << 32) | lo);
 }
 
-constexpr size_t kStreamStaticLds = 8192;   // pfx, fbody, fcr, ptab, gidx (+ slack)
+constexpr size_t kStreamStaticLds = 8192;   // pfx, fbody, fcr, ptab, gidx, cpe_part, cfo_tab (+ slack)
 
 // dynamic LDS of the kernel: FFT images, staging, reference staging, twiddle table
 template <int LOG2M, int NA>
@@ -280,9 +280,11 @@ constexpr bool stream_wave_fft() {
 // CPE (opt-in CFO path): decision-directed common-phase tracking. The residual frequency
 // offset left by the CFO estimate turns every symbol by a slowly growing angle; each symbol's
 // equalised outputs are rotated by the current estimate before the decision, and the sum of
-// conj(decided point) x rotated output over the symbol (all streams and subcarriers, reduced
-// through LDS at the next symbol's top barrier) corrects the estimate for the next symbol of
-// the same frame. Off (CPE = false) the kernel is unchanged.
+// conj(decided point) x rotated output over a group of kCpeEvery symbols (all streams, one
+// subcarrier slot per thread, reduced through LDS at the next symbol's top barrier) corrects
+// the estimate for the following symbols of the same frame. Off (CPE = false) the kernel is
+// unchanged.
+constexpr uint32_t kCpeEvery = 8;   // CPE: symbols per common-phase update
 template <int LOG2M, int NA, int REF, int OUTS, bool SC16 = false, bool CPE = false>
 __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(DecodeArgs a) {
   using PL = StreamPlan<LOG2M, NA>;
@@ -317,6 +319,8 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
   __shared__ v2f ptab[kStreamMaxQam];
   __shared__ uint8_t gidx[kStreamMaxQam];
   __shared__ v2f cpe_part[CPE ? T / 64 : 1];                       // per-wave phase sums
+  constexpr int CTN = W8 < 256 ? W8 : 256;
+  __shared__ v2f cfo_tab[CPE ? CTN : 1];                           // folded CFO, in-body phasors
   const int tid = threadIdx.x;
   const uint32_t wv = __builtin_amdgcn_readfirstlane((uint32_t)tid >> 6);
   for (uint32_t e = tid; e < a.qam.L * a.qam.L; e += T) {
@@ -530,7 +534,8 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
   };
 
   v2f rot = v2f{1.0f, 0.0f};                          // CPE: current phase correction
-  bool cpe_valid = false;                             // cpe_part holds this frame's last symbol
+  bool cpe_valid = false;                             // cpe_part holds this frame's last K symbols
+  v2f cpe_acc = v2f{0.0f, 0.0f};                      // this thread's residual-phase sum
   // folded CFO (a.cpe == 2): the frame's estimate nu = (eps0 + delta) / M cycles per sample
   // about its window base, split into the part inside a symbol body (time domain, before the
   // transform: sample j of the body turns by exp(-j 2 pi nu j), the thread's j = t0 % W8 + r W8)
@@ -538,9 +543,10 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
   // rotation) -- the derotation the scratch passes of the unfolded path applied
   // (the body start's phasor rides in rot: set at each frame segment's first symbol, advanced
   // by cfo_e per symbol, corrected by the CPE as before)
-  // (the thread's in-body phasor exp(-j2pi nu t0%W8) is recomputed per symbol from nu in an
-  // SGPR: fp32 is exact enough over one body, |nu t0%W8| < 1/8 cycle for |eps| < 1)
-  float cfo_nu = 0.0f;                                      // nu, cycles per sample
+  // (the thread's in-body phasor exp(-j2pi nu t0%W8) comes from an LDS table of the frame,
+  // cfo_tab[n] = exp(-j2pi nu n) for n < CTN, times a wave-uniform exp(-j2pi nu CTN hi) when
+  // W8 > CTN)
+  v2f cfo_hi = v2f{1.0f, 0.0f};
   v2f cfo_w = v2f{1.0f, 0.0f};                              // exp(-j2pi nu W8)
   v2f cfo_e = v2f{1.0f, 0.0f};                              // exp(-j2pi nu SL)
   auto cfo_frame = [&](uint32_t ff, uint32_t ss) {
@@ -556,7 +562,10 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
           sincospif((float)p, &sn, &cs);
           return v2f{cs, sn};
         };
-        cfo_nu = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int((float)nu)));
+        // (every reader of the previous frame's table passed this symbol's barriers; the next
+        // top barrier publishes the new one)
+        for (int e = tid; e < CTN; e += T) cfo_tab[e] = ph(nu * (double)e);
+        if constexpr (W8 > CTN) cfo_hi = uni(ph(nu * (double)((opq(tid) % W8) / CTN * CTN)));
         cfo_w = uni(ph(nu * (double)W8));
         cfo_e = uni(ph(nu * (double)a.SL));
         rot = uni(ph(nu * (double)((int64_t)J.i0 + a.cp + (int64_t)ss * a.SL)));
@@ -576,7 +585,8 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
     asm volatile("s_waitcnt vmcnt(%0)" :: "n"(NSTORE) : "memory");
     __syncthreads();
     if constexpr (CPE) {
-      if (cpe_valid) {   // the previous symbol's residual phase: rot *= conj(c) / |c|
+      if (cpe_valid) {   // the previous kCpeEvery symbols' residual phase: rot *= conj(c) / |c|
+        cpe_valid = false;
         v2f c = v2f{0.0f, 0.0f};
 #pragma unroll
         for (int w = 0; w < T / 64; w++) c += cpe_part[w];
@@ -631,9 +641,8 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
       // the body turns every output by it, and costs one multiply per sample instead of one
       // per output); folded CFO: times the in-body part of the derotation
       if (a.cpe == 2) {
-        float sn, cs;
-        sincospif(-2.0f * cfo_nu * (float)(opq(tid) % W8), &sn, &cs);
-        v2f c = cmul_pk(v2f{cs, sn}, rot);
+        v2f c = cmul_pk(cfo_tab[(opq(tid) % W8) % CTN], rot);
+        if constexpr (W8 > CTN) c = cmul_pk(c, cfo_hi);
 #pragma unroll
         for (int r = 0; r < 8; r++) {
           v[r] = cmul_pk(v[r], c);
@@ -714,7 +723,6 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
     const uint64_t frame_id = a.frame_id0 + (fcr[f] >> 16);
     // output row (f, t, s) = ob0 + t * max_out * M_occ: uniform, one 64-bit product per symbol
     const uint64_t ob0 = rfl64((((uint64_t)f * NA) * a.max_out + s) * a.M_occ);
-    v2f cpe_acc = v2f{0.0f, 0.0f};
     // one output (stream t, slot q, subcarrier k): apply, demap, EVM terms; returns the decision
     auto one_out = [&](int t, int q, uint32_t k, const v2f *X, v2f &acc) -> uint32_t {
       acc = v2f{0.0f, 0.0f};
@@ -801,14 +809,20 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
       }
     }
 
-    if constexpr (CPE) {   // this symbol's residual phase sum, per wave, read after the next barrier
+    if constexpr (CPE) {
+      // every kCpeEvery symbols of a frame: the residual phase sum, per wave, read after the
+      // next barrier (the estimate moves ~1e-4 rad per symbol; reducing once per group of
+      // symbols instead of per symbol saves the shuffles, the LDS round and the update)
+      if ((s + 1) % kCpeEvery == 0) {                 // uniform
 #pragma unroll
-      for (int off = 32; off > 0; off >>= 1) {
-        cpe_acc.x += __shfl_xor(cpe_acc.x, off);
-        cpe_acc.y += __shfl_xor(cpe_acc.y, off);
+        for (int off = 32; off > 0; off >>= 1) {
+          cpe_acc.x += __shfl_xor(cpe_acc.x, off);
+          cpe_acc.y += __shfl_xor(cpe_acc.y, off);
+        }
+        if ((tid & 63) == 0) cpe_part[wv] = cpe_acc;
+        cpe_acc = v2f{0.0f, 0.0f};
+        cpe_valid = true;
       }
-      if ((tid & 63) == 0) cpe_part[wv] = cpe_acc;
-      cpe_valid = true;
     }
     MARK(";@@F tail");
     const bool last = (i + 1 == i_end);
@@ -818,6 +832,7 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
       if constexpr (CPE) {
         rot = v2f{1.0f, 0.0f};
         cpe_valid = false;
+        cpe_acc = v2f{0.0f, 0.0f};
       }
       flush(f);
       if (!last) {

@@ -707,22 +707,47 @@ void search_ls_wave_kernel(SearchArgs a) {
 
 // one thread per (frame, subcarrier, rx-tx pair): the codes' X/S1 of lsq in code order, G and
 // this block's share of the residual variance (as ls_combine_kernel)
+constexpr int kLsRotCodes = 256;   // CFO code rotations tabled in LDS
 __global__ __launch_bounds__(256) void ls_combine_q_kernel(LsArgs a) {
   __shared__ double red[4];
+  __shared__ double s_nu;
+  __shared__ double2 s_rot[kLsRotCodes];
   const uint32_t rt = blockIdx.y, f = blockIdx.z;
   const FrameInfo &I = a.info[f];
   if (I.status != 0) return;
   const uint32_t M = a.M, N = a.N;
   const uint32_t k = blockIdx.x * 256 + threadIdx.x;
+  const uint32_t r_ = rt / N, t_ = rt % N;
+  // opt-in CFO: the residual's phase at each code's window (window-relative, about the frame's
+  // base), as the data region is derotated (cfo_kernels.hip stage 2) -- uniform over the
+  // workgroup, so tabled once per code instead of per subcarrier
+  const bool rot_tab = a.cfo_part && a.nac <= (uint32_t)kLsRotCodes;
+  if (a.cfo_part) {
+    if (threadIdx.x == 0) {
+      s_nu = cfo_stage_eps(a.cfo_part, f, 2) / (double)M;
+      if (blockIdx.x == 0 && rt == 0)   // the frame's total estimate (stage 1 + stage 2)
+        const_cast<FrameInfo &>(I).cfo_eps = (float)(cfo_stage_eps(a.cfo_part, f, 1) + s_nu * M);
+    }
+    __syncthreads();
+    if (rot_tab) {
+      for (uint32_t c = threadIdx.x; c < a.nac; c += 256) {
+        const unsigned long long key = a.keys[((uint64_t)f * N + r_) * a.n_slots + 1 + c * N + t_];
+        const double w = (double)key_index(key) + 0.5 * (double)M;
+        double ph = -2.0 * s_nu * w;
+        ph -= 2.0 * rint(ph * 0.5);
+        double sn, cs;
+        sincospi(ph, &sn, &cs);
+        s_rot[c] = make_double2(cs, sn);
+      }
+      __syncthreads();
+    }
+  }
   double nv = 0.0;
   if (k < M) {
     const bool occ = a.occ_index[k] >= 0;
     const float2 *q = a.lsq + ((uint64_t)f * N * N + rt) * a.nac * M + k;
     double sr = 0.0, si = 0.0, s2 = 0.0;
-    const uint32_t r_ = rt / N, t_ = rt % N;
-    const double nu = a.cfo_part ? cfo_stage_eps(a.cfo_part, f, 2) / (double)M : 0.0;
-    if (a.cfo_part && k == 0 && rt == 0)   // the frame's total estimate (stage 1 + stage 2)
-      const_cast<FrameInfo &>(I).cfo_eps = (float)(cfo_stage_eps(a.cfo_part, f, 1) + nu * M);
+    const double nu = a.cfo_part ? s_nu : 0.0;
     // the codes' terms in batches of CB loads in flight (one latency per batch instead of per
     // code), summed in code order as before
     constexpr uint32_t CB = 8;
@@ -737,15 +762,18 @@ __global__ __launch_bounds__(256) void ls_combine_q_kernel(LsArgs a) {
         if (c >= a.nac) break;
         float2 v = vb[j];
         if (a.cfo_part) {
-          // opt-in CFO: the residual's phase at this code's window (window-relative, about the
-          // frame's base), as the data region is derotated (cfo_kernels.hip stage 2)
-          const unsigned long long key =
-              a.keys[((uint64_t)f * N + r_) * a.n_slots + 1 + c * N + t_];
-          const double w = (double)key_index(key) + 0.5 * (double)M;
-          double ph = -2.0 * nu * w;
-          ph -= 2.0 * rint(ph * 0.5);
           double sn, cs;
-          sincospi(ph, &sn, &cs);
+          if (rot_tab) {
+            cs = s_rot[c].x;
+            sn = s_rot[c].y;
+          } else {   // (more codes than the table holds)
+            const unsigned long long key =
+                a.keys[((uint64_t)f * N + r_) * a.n_slots + 1 + c * N + t_];
+            const double w = (double)key_index(key) + 0.5 * (double)M;
+            double ph = -2.0 * nu * w;
+            ph -= 2.0 * rint(ph * 0.5);
+            sincospi(ph, &sn, &cs);
+          }
           v = make_float2((float)(v.x * cs - v.y * sn), (float)(v.x * sn + v.y * cs));
         }
         sr += (double)v.x;
