@@ -284,7 +284,10 @@ constexpr bool stream_wave_fft() {
 // subcarrier slot per thread, reduced through LDS at the next symbol's top barrier) corrects
 // the estimate for the following symbols of the same frame. Off (CPE = false) the kernel is
 // unchanged.
-constexpr uint32_t kCpeEvery = 8;   // CPE: symbols per common-phase update
+#ifndef MIMO_CPE_EVERY
+#define MIMO_CPE_EVERY 8
+#endif
+constexpr uint32_t kCpeEvery = MIMO_CPE_EVERY;   // CPE: symbols per common-phase update
 template <int LOG2M, int NA, int REF, int OUTS, bool SC16 = false, bool CPE = false>
 __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(DecodeArgs a) {
   using PL = StreamPlan<LOG2M, NA>;
@@ -536,6 +539,7 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
   v2f rot = v2f{1.0f, 0.0f};                          // CPE: current phase correction
   bool cpe_valid = false;                             // cpe_part holds this frame's last K symbols
   v2f cpe_acc = v2f{0.0f, 0.0f};                      // this thread's residual-phase sum
+  uint32_t cpe_k = 0;                                 // symbols of this frame segment so far
   // folded CFO (a.cpe == 2): the frame's estimate nu = (eps0 + delta) / M cycles per sample
   // about its window base, split into the part inside a symbol body (time domain, before the
   // transform: sample j of the body turns by exp(-j 2 pi nu j), the thread's j = t0 % W8 + r W8)
@@ -810,10 +814,12 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
     }
 
     if constexpr (CPE) {
-      // every kCpeEvery symbols of a frame: the residual phase sum, per wave, read after the
-      // next barrier (the estimate moves ~1e-4 rad per symbol; reducing once per group of
-      // symbols instead of per symbol saves the shuffles, the LDS round and the update)
-      if ((s + 1) % kCpeEvery == 0) {                 // uniform
+      // the residual phase sum, per wave, read after the next barrier: after each of a frame
+      // segment's first four symbols (a range that starts mid-frame opens with the estimate's
+      // accumulated error), then once per kCpeEvery symbols (the error then moves ~1e-4 rad
+      // per symbol; one reduction per group saves the shuffles, the LDS round and the update)
+      cpe_k++;
+      if (cpe_k <= 4 || cpe_k % kCpeEvery == 0) {    // uniform
 #pragma unroll
         for (int off = 32; off > 0; off >>= 1) {
           cpe_acc.x += __shfl_xor(cpe_acc.x, off);
@@ -833,6 +839,7 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
         rot = v2f{1.0f, 0.0f};
         cpe_valid = false;
         cpe_acc = v2f{0.0f, 0.0f};
+        cpe_k = 0;
       }
       flush(f);
       if (!last) {
