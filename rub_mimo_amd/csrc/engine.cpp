@@ -425,8 +425,8 @@ int run_sync(mimo_rx *h, const float2 *iq, uint64_t stride, uint32_t F, uint64_t
     launch_fill(fa, s);   // trigger words, queue heads and screen flags in one launch
     static const bool prof_env = [] { const char *e = getenv("RMIMO_SC_PROF"); return e && e[0] == '1'; }();
     if (prof_env) {
-      if (!h->sc_prof.p) HIPCHK(h->sc_prof.ensure(20));
-      HIPCHK(hipMemsetAsync(h->sc_prof.p, 0, 20 * sizeof(unsigned long long), s));
+      if (!h->sc_prof.p) HIPCHK(h->sc_prof.ensure(28));
+      HIPCHK(hipMemsetAsync(h->sc_prof.p, 0, 28 * sizeof(unsigned long long), s));
       HIPCHK(hipMemsetAsync(h->sc_prof.p + 8, 0xFF, sizeof(unsigned long long), s));
       if (screen) HIPCHK(hipMemsetAsync(h->sc_prof.p, 0xFF, sizeof(unsigned long long), s));
       a.prof = h->sc_prof.p;
@@ -482,7 +482,7 @@ int run_sync(mimo_rx *h, const float2 *iq, uint64_t stride, uint32_t F, uint64_t
     }
     h->timer.end(0, e, s);
     if (prof_env && screen) {   // diagnostics: exact-kernel timeline (wall clock, 100 MHz)
-      unsigned long long v[20];
+      unsigned long long v[28];
       HIPCHK(hipMemcpyAsync(v, h->sc_prof.p, sizeof(v), hipMemcpyDeviceToHost, s));
       HIPCHK(hipStreamSynchronize(s));
       fprintf(stderr, "exact_prof passes %llu last_pass_end %.2f us finalize_end %.2f us "
@@ -495,6 +495,13 @@ int run_sync(mimo_rx *h, const float2 *iq, uint64_t stride, uint32_t F, uint64_t
               v[12] ? (double)v[11] / v[12] / 100.0 : 0.0, v[12], (double)(v[13] >> 32) / 100.0,
               (v[13] >> 24) & 0xFF, (double)(v[13] & 0xFFFFFF) / 100.0, v[14] >> 32,
               v[14] & 0xFFFFFFFFull, v[15]);
+      const double np = v[4] ? (double)v[4] : 1.0;
+      fprintf(stderr, "exact_split record %.2f us setup %.2f us iterations %.2f us (%.2f per pass) "
+              "start offset avg %.2f max %.2f us | per iteration: ring %.2f scan %.2f walk %.2f us\n",
+              v[20] / np / 100.0, v[21] / np / 100.0,
+              v[22] / np / 100.0, v[23] / np, (v[26] / np - (double)v[0]) / 100.0,
+              (double)(v[25] - v[0]) / 100.0, v[23] ? v[16] / (double)v[23] / 100.0 : 0.0,
+              v[23] ? v[17] / (double)v[23] / 100.0 : 0.0, v[23] ? v[18] / (double)v[23] / 100.0 : 0.0);
     } else if (prof_env) {   // diagnostics: per-item cycle split of the S&C kernel
       unsigned long long v[20];
       HIPCHK(hipMemcpyAsync(v, h->sc_prof.p, sizeof(v), hipMemcpyDeviceToHost, s));
@@ -639,7 +646,7 @@ int run_decode(mimo_rx *h, const float2 *iq, uint64_t stride, uint32_t F, uint64
   d.expt = decode_expt();
   static const bool dprof = [] { const char *e = getenv("RMIMO_DEC_PROF"); return e && e[0] == '1'; }();
   if (dprof) {
-    if (!h->sc_prof.p) HIPCHK(h->sc_prof.ensure(20));
+    if (!h->sc_prof.p) HIPCHK(h->sc_prof.ensure(28));
     HIPCHK(hipMemsetAsync(h->sc_prof.p, 0, 5 * sizeof(unsigned long long), s));
     d.prof = h->sc_prof.p;
   }

@@ -1552,6 +1552,7 @@ void sc_exact_kernel(ScArgs a) {
   const int64_t w0 = hp->w0;
   const uint64_t ci = (uint64_t)f * a.nchunks + hp->chunk;
   const int64_t fmin = (int64_t)a.fmin[ci], fmax = (int64_t)a.fmax[ci];
+  const unsigned long long t_rec = a.prof ? (unsigned long long)wall_clock64() + (fmin & 0) : 0ull;
   int it_lo = (int)std::max<int64_t>(0, (fmin - (int64_t)a.cp - 2 - w0) / kScIt);
   int it_hi = (int)std::min<int64_t>(kScIters - 1, (fmax - w0) / kScIt);
   const auto x = iq_row<S>(a.iq, a.iq_scale, ((uint64_t)f * a.N + s) * a.stride);
@@ -1621,9 +1622,18 @@ void sc_exact_kernel(ScArgs a) {
   block_scan<4>(c, t4, scan_ws[par]);
   par ^= 1;
   double Pc_re = t4[0], Pc_im = t4[1], Zc = t4[2], Cc = t4[3], Ac = t4[2];
+  const unsigned long long t_setup = a.prof ? (unsigned long long)wall_clock64() : 0ull;
+  if (a.prof && tid == 0) {
+    atomicAdd(&a.prof[20], t_rec - t_item);
+    atomicAdd(&a.prof[21], t_setup - t_rec);
+    atomicAdd(&a.prof[23], (unsigned long long)(it_hi - it_lo + 1));
+    atomicMax(&a.prof[25], t_item);
+    atomicAdd(&a.prof[26], t_item);
+  }
 #pragma unroll 1
   for (int it = it_lo; it <= it_hi; it++) {
     const int64_t ib = w0 + (int64_t)it * kScIt;
+    const unsigned long long tq0 = a.prof ? (unsigned long long)wall_clock64() : 0ull;
     {
       const int sl0 = (M + it * kScIt) % RING + 2 * tid;
       if (pf) {
@@ -1644,6 +1654,7 @@ void sc_exact_kernel(ScArgs a) {
       }
     }
     __syncthreads();
+    const unsigned long long tq1 = a.prof ? (unsigned long long)wall_clock64() : 0ull;
     if (it + 1 <= it_hi) pf = fetch_block(pre, x, ib + kScIt, L, vec);
     const float2 *xn = ring + ring_pad((M + it * kScIt + kScS * tid) % RING);
     const float2 *xr = ring + ring_pad((RL + it * kScIt + kScS * tid) % RING);
@@ -1676,6 +1687,7 @@ void sc_exact_kernel(ScArgs a) {
     d[3] = (double)dc;
     block_scan<5>(d, tot, scan_ws[par]);
     par ^= 1;
+    const unsigned long long tq2 = a.prof ? (unsigned long long)wall_clock64() : 0ull;
     double Pre = Pc_re + d[0], Pim = Pc_im + d[1], Z = Zc + d[2], C = Cc + d[3];
     const double Aend = Ac + tot[4];
     const double zfloor = 1e-6 * Aend;
@@ -1731,6 +1743,12 @@ void sc_exact_kernel(ScArgs a) {
       if (a.n_exact) atomicAdd(a.n_exact, 1ull);
     }
     __syncthreads();
+    const unsigned long long tq3 = a.prof ? (unsigned long long)wall_clock64() : 0ull;
+    if (a.prof && tid == 0) {
+      atomicAdd(&a.prof[16], tq1 - tq0);
+      atomicAdd(&a.prof[17], tq2 - tq1);
+      atomicAdd(&a.prof[18], tq3 - tq2);
+    }
     const int namb = (a.diag & 8) ? 0 : min(s_namb, kLocAmb);          // uniform
     const unsigned long long t_r0 = a.prof ? (unsigned long long)wall_clock64() : 0ull;
     if (namb > 0) {
@@ -1796,6 +1814,7 @@ void sc_exact_kernel(ScArgs a) {
     hp->wbits[((int)s * kScIters + it) * kScT + tid] = (uint16_t)bits;
     __syncthreads();   // every lane's phase B reads of the ring precede the next block's writes
   }
+  if (a.prof && tid == 0) atomicAdd(&a.prof[22], (unsigned long long)wall_clock64() - t_setup - t_res);
   }   // active
   // the item's last antenna pass: plateau rule over every antenna's words
   if (a.prof && tid == 0) {
