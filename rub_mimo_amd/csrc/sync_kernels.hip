@@ -1539,7 +1539,15 @@ void sc_exact_kernel(ScArgs a) {
   const uint32_t IT = a.split_iters ? kScIters : 1u;
   const uint32_t s = blockIdx.x / IT;
   const int itw = (int)(blockIdx.x % IT);
-  for (uint32_t slot = item0 + blockIdx.y; slot < count; slot += gridDim.y) {
+  // the first slot's record is read before the count is known (it is inside the allocation
+  // whatever the count, and used only if the slot is live): in phase 1 (item0 = 0) its loads
+  // go out with the count's instead of one memory latency after it
+  uint32_t slot = item0 + blockIdx.y;
+  const ScHot *hs = a.hot + min(slot, a.hot_cap - 1u);
+  uint32_t f_n = hs->f;
+  int64_t w0_n = hs->w0;
+  uint64_t chunk_n = hs->chunk;
+  for (; slot < count; slot += gridDim.y) {
   ScHot *hp = a.hot + slot;
   const int tid = threadIdx.x;
   if (tid == 0) s_namb = 0;
@@ -1547,10 +1555,10 @@ void sc_exact_kernel(ScArgs a) {
   if (a.prof && tid == 0) atomicMin(&a.prof[0], t_item);
   unsigned long long t_res = 0;
   uint32_t n_win = 0, n_smp = 0;   // diagnostics: resolve windows and samples of this pass
-  const uint32_t f = hp->f;
+  const uint32_t f = f_n;
   const int64_t L = (int64_t)a.frame_len;
-  const int64_t w0 = hp->w0;
-  const uint64_t ci = (uint64_t)f * a.nchunks + hp->chunk;
+  const int64_t w0 = w0_n;
+  const uint64_t ci = (uint64_t)f * a.nchunks + chunk_n;
   const int64_t fmin = (int64_t)a.fmin[ci], fmax = (int64_t)a.fmax[ci];
   const unsigned long long t_rec = a.prof ? (unsigned long long)wall_clock64() + (fmin & 0) : 0ull;
   int it_lo = (int)std::max<int64_t>(0, (fmin - (int64_t)a.cp - 2 - w0) / kScIt);
@@ -1866,6 +1874,12 @@ void sc_exact_kernel(ScArgs a) {
     }
   }
   __syncthreads();
+  if (slot + gridDim.y < count) {   // the next slot's record (uniform)
+    const ScHot *hn = a.hot + slot + gridDim.y;
+    f_n = hn->f;
+    w0_n = hn->w0;
+    chunk_n = hn->chunk;
+  }
   }
 }
 
