@@ -1577,7 +1577,10 @@ void sc_exact_kernel(ScArgs a) {
   }
   const int64_t ib_lo = w0 + (int64_t)it_lo * kScIt;
   if (active) {
-  // history [ib_lo - M, ib_lo) -> its ring slots; the block in flight behind it
+  // the first block's loads, then the history [ib_lo - M, ib_lo) -> its ring slots: both in
+  // flight together (the window sums below wait for the history only)
+  float4 pre[kScIt / (2 * kScT)];
+  bool pf = fetch_block(pre, x, ib_lo, L, vec);
   const int wb = (kScIt * it_lo) % RING;
   if (vec && ib_lo - M >= 0 && ib_lo <= L) {
     // all history pairs in flight together, then the ring writes
@@ -1606,8 +1609,6 @@ void sc_exact_kernel(ScArgs a) {
       *reinterpret_cast<float4 *>(ring + ring_pad(sl)) = ld_pair(x, ib_lo - M + 2 * j, L, vec);
     }
   }
-  float4 pre[kScIt / (2 * kScT)];
-  bool pf = fetch_block(pre, x, ib_lo, L, vec);
   __syncthreads();
   // window sums ending at ib_lo - 1: P over the last M/2, 2R and the nonzero count over M
   double c[4] = {0.0, 0.0, 0.0, 0.0}, t4[4], tot[5];
