@@ -44,6 +44,13 @@ namespace mimo {
 #else
 #define MARK(s)
 #endif
+// diagnostics build only (-DDS_PROF, RMIMO_DEC_PROF=1): shader-clock split of the symbol loop
+// of workgroup wave 0 (top wait, transform, apply, tail) into DecodeArgs::prof
+#ifdef DS_PROF
+#define DSP(...) __VA_ARGS__
+#else
+#define DSP(...)
+#endif
 constexpr uint32_t kStreamMaxFrames = 192;   // per-frame tables in LDS beside a 157 KB working set
 constexpr uint32_t kStreamMaxQam = 256;          // constellation points (256-QAM)
 
@@ -104,14 +111,16 @@ MIMO_DEV void st_store(v2f *buf, const v2f *v, uint32_t tid) {
   }
 }
 
-// pass P with the twiddles from the LDS table (twl: passes 1.. in order, [(r-1) NS + jm])
+// pass P with its base twiddle from the LDS table (twl: passes 1.. in order, one row of NS
+// entries each, [jm] = e^{-2 pi i jm / (NS R)}) and the powers r = 2 .. R-1 in registers: one
+// LDS read per butterfly instead of R - 1 (the transform phase is bound by LDS instructions)
 template <int LOG2M, int NA, int P>
 MIMO_DEV void st_load_t(const v2f *buf, v2f *v, const v2f *twl, uint32_t tid) {
   using PL = StreamPlan<LOG2M, NA>;
   constexpr uint32_t R = PL::radix(P), NB = PL::M / R, NS = PL::ns(P);
   constexpr int OFF = [] {
     int o = 0;
-    for (int q = 1; q < P; q++) o += (PL::radix(q) - 1) * PL::ns(q);
+    for (int q = 1; q < P; q++) o += PL::ns(q);
     return o;
   }();
 #pragma unroll
@@ -120,9 +129,10 @@ MIMO_DEV void st_load_t(const v2f *buf, v2f *v, const v2f *twl, uint32_t tid) {
     const v2f *bp = buf + g * PL::PB + lds_pad((int)j);
 #pragma unroll
     for (int r = 0; r < (int)R; r++) v[i * R + r] = bp[r * NB + (r * NB) / 32];
-    const v2f *tw = twl + OFF + (j % NS);
+    v2f w[R];
+    twiddle_powers<R>(w, twl[OFF + (j % NS)]);
 #pragma unroll
-    for (int r = 1; r < (int)R; r++) v[i * R + r] = cmul_pk(v[i * R + r], tw[(r - 1) * NS]);
+    for (int r = 1; r < (int)R; r++) v[i * R + r] = cmul_pk(v[i * R + r], w[r]);
     dft_fwd_pk<R>(v + i * R);
   }
 }
@@ -157,10 +167,10 @@ struct WavePlan {
   using SP = StreamPlan<LOG2M - 3, 1>;
   static constexpr int QS = ((lds_padded_len(MS) + 3) / 8) * 8 + 4;
   static constexpr int GS = 8 * QS;
-  static constexpr int TW0 = 4 * MS;                     // W_M^{nq}, q = 1..4, n < MS
+  static constexpr int TW0 = MS;                         // W_M^n, n < MS (powers q = 2..7 in registers)
   static constexpr int TWS = [] {
     int s = 0;
-    for (int p = 1; p < SP::NP; p++) s += (SP::radix(p) - 1) * SP::ns(p);
+    for (int p = 1; p < SP::NP; p++) s += SP::ns(p);
     return s;
   }();
 };
@@ -263,7 +273,7 @@ constexpr size_t stream_dyn_lds(bool wave_fft, int ref_mode, bool sc16) {
   if (wave_fft) {
     tw = (size_t)WP::TW0 + WP::TWS;
   } else {
-    for (int p = 1; p < PL::NP; p++) tw += (size_t)(PL::radix(p) - 1) * PL::ns(p);
+    for (int p = 1; p < PL::NP; p++) tw += (size_t)PL::ns(p);
   }
   const size_t img = wave_fft ? (size_t)NA * WP::GS : (size_t)NA * PL::PB;
   const size_t stage = sc16 ? sizeof(short2) * (size_t)(PL::M + 4) * NA
@@ -333,34 +343,26 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
     gidx[e] = (uint8_t)((gray_enc(mI) << a.qam.b) | gray_enc(mQ));
   }
 
-  // twiddles of passes 1..NP-1: twl[off(p) + (r-1) NS + jm] = e^{-2 pi i jm r / (NS R)}
+  // base twiddles of passes 1..NP-1: twl[off(p) + jm] = e^{-2 pi i jm / (NS R)} (the powers
+  // r = 2 .. R-1 are formed in registers, st_load_t)
   if constexpr (WF) {
-    // W_M^{nq} (q = 1..4, n < MS), then the sub-transform plan's passes
-    for (int e = tid; e < WP::TW0; e += T) {
-      const int q = e / MS + 1, n = e % MS;
-      twl[e] = twiddle<false>(a.tw, ((n * q) % M) * (kTwN / M));
-    }
+    // W_M^n (n < MS; pass 0's W_M^{nq} are its powers), then the sub-transform plan's passes
+    for (int e = tid; e < WP::TW0; e += T) twl[e] = twiddle<false>(a.tw, e * (kTwN / M));
     using SP = typename WP::SP;
     int off = WP::TW0;
 #pragma unroll
     for (int p = 1; p < SP::NP; p++) {
       const int R = SP::radix(p), NS = SP::ns(p);
-      for (int e = tid; e < (R - 1) * NS; e += T) {
-        const int r = e / NS + 1, jm = e % NS;
-        twl[off + e] = twiddle<false>(a.tw, ((jm * r) % (NS * R)) * (kTwN / (NS * R)));
-      }
-      off += (R - 1) * NS;
+      for (int e = tid; e < NS; e += T) twl[off + e] = twiddle<false>(a.tw, e * (kTwN / (NS * R)));
+      off += NS;
     }
   } else {
     int off = 0;
 #pragma unroll
     for (int p = 1; p < PL::NP; p++) {
       const int R = PL::radix(p), NS = PL::ns(p);
-      for (int e = tid; e < (R - 1) * NS; e += T) {
-        const int r = e / NS + 1, jm = e % NS;
-        twl[off + e] = twiddle<false>(a.tw, ((jm * r) % (NS * R)) * (kTwN / (NS * R)));
-      }
-      off += (R - 1) * NS;
+      for (int e = tid; e < NS; e += T) twl[off + e] = twiddle<false>(a.tw, e * (kTwN / (NS * R)));
+      off += NS;
     }
   }
   // decodable symbols of frames < f (status OK, min(n_sym, max_out) each), and each frame's
@@ -583,11 +585,14 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
   // assumes only stores behind the DMA)
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();                                    // twiddle table and guarded staging
+  DSP(unsigned long long ds_t[8] = {0, 0, 0, 0, 0, 0, 0, 0}; unsigned long long ds_c = __builtin_amdgcn_s_memtime();)
   for (uint32_t i = i_begin; i < i_end; i++) {
     // this symbol's staging has landed (the previous symbol's stores may still be in flight)
     MARK(";@@A top");
+    DSP(const unsigned long long ds_0 = __builtin_amdgcn_s_memtime(); ds_t[4] += ds_0 - ds_c;)
     asm volatile("s_waitcnt vmcnt(%0)" :: "n"(NSTORE) : "memory");
     __syncthreads();
+    DSP(const unsigned long long ds_1 = __builtin_amdgcn_s_memtime(); ds_t[1] += ds_1 - ds_0;)
     if constexpr (CPE) {
       if (cpe_valid) {   // the previous kCpeEvery symbols' residual phase: rot *= conj(c) / |c|
         cpe_valid = false;
@@ -662,20 +667,16 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
     if constexpr (WF) {     // pass 0's twiddles W_M^{nq}; c_q[n] to region (g, q)
       const uint32_t t0 = (uint32_t)opq(tid);
       const uint32_t n = t0 % MS, g = t0 / MS;
-      const v2f *w = twl + n;
-      const v2f w1 = w[0], w2 = w[MS], w3 = w[2 * MS], w4 = w[3 * MS];
-      v[1] = cmul_pk(v[1], w1);
-      v[2] = cmul_pk(v[2], w2);
-      v[3] = cmul_pk(v[3], w3);
-      v[4] = cmul_pk(v[4], w4);
-      v[5] = cmul_pk(v[5], cmul_pk(w4, w1));
-      v[6] = cmul_pk(v[6], cmul_pk(w4, w2));
-      v[7] = cmul_pk(v[7], cmul_pk(w4, w3));
+      v2f w[8];
+      twiddle_powers<8>(w, twl[n]);
+#pragma unroll
+      for (int q = 1; q < 8; q++) v[q] = cmul_pk(v[q], w[q]);
       v2f *e = img + g * GS + lds_pad((int)n);
 #pragma unroll
       for (int q = 0; q < 8; q++) e[q * QS] = v[q];
     }
     __syncthreads();                                  // staging consumed by every wave
+    DSP(const unsigned long long ds_2 = __builtin_amdgcn_s_memtime(); ds_t[5] += ds_2 - ds_1;)
     MARK(";@@C fetch");
     // the item after this one (uniform) and its staging, in flight during this symbol
     uint32_t fn = f, sn = s + 1, n_out_n = n_out_f;
@@ -694,6 +695,7 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
     // passes 1 .. NP-1 through the LDS images (pass 1 needs no leading barrier: the previous
     // symbol's image readers finished before the barrier at the top), then the exchange that
     // leaves the spectra in natural order
+    DSP(const unsigned long long ds_2b = __builtin_amdgcn_s_memtime(); ds_t[6] += ds_2b - ds_2;)
     MARK(";@@D subfft");
     if constexpr (WF) {
       // sub-transform (g, q) on lane group t0 / LG, inside one wave
@@ -723,6 +725,7 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
     }
 
     MARK(";@@E apply");
+    DSP(const unsigned long long ds_3 = __builtin_amdgcn_s_memtime(); ds_t[2] += ds_3 - ds_1; ds_t[7] += ds_3 - ds_2b;)
     // apply, demap, EVM, stores: subcarriers k = tid + q T (KADJ: S tid + q) of every stream
     const uint64_t frame_id = a.frame_id0 + (fcr[f] >> 16);
     // output row (f, t, s) = ob0 + t * max_out * M_occ: uniform, one 64-bit product per symbol
@@ -831,6 +834,7 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
       }
     }
     MARK(";@@F tail");
+    DSP(ds_c = __builtin_amdgcn_s_memtime(); ds_t[3] += ds_c - ds_3; ds_t[0]++;)
     const bool last = (i + 1 == i_end);
     if constexpr (CPE)
       if (a.cpe == 2) rot = uni(cmul_pk(rot, cfo_e));   // the next symbol's body start
@@ -853,6 +857,9 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
     s = __builtin_amdgcn_readfirstlane(sn);
     odd = __builtin_amdgcn_readfirstlane(odd_n);
   }
+  DSP(if (a.prof && threadIdx.x == 0) {
+    for (int q = 0; q < 8; q++) atomicAdd(&a.prof[q], ds_t[q]);
+  })
 }
 
 // ------------------------------------------------------------------------------------

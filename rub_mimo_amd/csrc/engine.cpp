@@ -647,7 +647,7 @@ int run_decode(mimo_rx *h, const float2 *iq, uint64_t stride, uint32_t F, uint64
   static const bool dprof = [] { const char *e = getenv("RMIMO_DEC_PROF"); return e && e[0] == '1'; }();
   if (dprof) {
     if (!h->sc_prof.p) HIPCHK(h->sc_prof.ensure(28));
-    HIPCHK(hipMemsetAsync(h->sc_prof.p, 0, 5 * sizeof(unsigned long long), s));
+    HIPCHK(hipMemsetAsync(h->sc_prof.p, 0, 8 * sizeof(unsigned long long), s));
     d.prof = h->sc_prof.p;
   }
   hipEvent_t e = h->timer.begin(s);
@@ -676,12 +676,13 @@ int run_decode(mimo_rx *h, const float2 *iq, uint64_t stride, uint32_t F, uint64
   if (!parts)   // run_batch widens every sc16 batch the streaming decode does not take
     return fail(MIMO_ERR_UNSUPPORTED, "no decode kernel takes this configuration");
   if (dprof) {   // diagnostics: per-item cycle split of the decode kernel
-    unsigned long long v[5];
+    unsigned long long v[8];
     HIPCHK(hipMemcpyAsync(v, h->sc_prof.p, sizeof(v), hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
     const double it = v[0] ? (double)v[0] : 1.0;
-    fprintf(stderr, "dec_prof items %llu cycles/item load %.0f fft %.0f apply %.0f reduce %.0f\n",
-            v[0], v[1] / it, v[2] / it, v[3] / it, v[4] / it);
+    fprintf(stderr, "dec_prof items %llu cycles/item load %.0f fft %.0f apply %.0f reduce %.0f "
+            "| stream split: pass0 %.0f fetch %.0f subfft %.0f\n",
+            v[0], v[1] / it, v[2] / it, v[3] / it, v[4] / it, v[5] / it, v[6] / it, v[7] / it);
   }
   EvmArgs ea{};
   ea.N = h->N; ea.max_out = max_out; ea.parts = parts; ea.info = h->info.p;

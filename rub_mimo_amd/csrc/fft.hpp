@@ -74,6 +74,32 @@ MIMO_DEV v2f vmulc(v2f a, v2f b) {
   return r;
 }
 
+// w[q] = w1^q for q < R (w[0] unused), at most three roundings deep (as reg_compute)
+template <int R>
+MIMO_DEV void twiddle_powers(v2f *w, v2f w1) {
+  w[1] = w1;
+  if constexpr (R >= 4) {
+    w[2] = vmul(w[1], w[1]);
+    w[3] = vmul(w[2], w[1]);
+  }
+  if constexpr (R >= 8) {
+    w[4] = vmul(w[2], w[2]);
+    w[5] = vmul(w[4], w[1]);
+    w[6] = vmul(w[3], w[3]);
+    w[7] = vmul(w[4], w[3]);
+  }
+  if constexpr (R == 16) {
+    w[8] = vmul(w[4], w[4]);
+    w[9] = vmul(w[8], w[1]);
+    w[10] = vmul(w[5], w[5]);
+    w[11] = vmul(w[8], w[3]);
+    w[12] = vmul(w[6], w[6]);
+    w[13] = vmul(w[8], w[5]);
+    w[14] = vmul(w[7], w[7]);
+    w[15] = vmul(w[8], w[7]);
+  }
+}
+
 // forward radix-2/4/8 DFTs on the packed forms (same arithmetic as dft_small<R, false>)
 template <int R>
 MIMO_DEV void dft_fwd_pk(v2f *a) {

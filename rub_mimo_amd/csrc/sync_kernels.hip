@@ -131,6 +131,34 @@ MIMO_DEV float sc_exact(const float2 *__restrict__ x, int64_t n, int64_t M) {
 }
 
 
+// a double moved across lanes by one DPP control (both halves; lanes with no source, or in a
+// row the row mask leaves out, read 0.0)
+template <int CTRL, int ROWS = 0xF>
+MIMO_DEV double dpp_f64(double x) {
+  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(x), CTRL, ROWS, 0xF, true);
+  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(x), CTRL, ROWS, 0xF, true);
+  return __hiloint2double(hi, lo);
+}
+
+// wave-inclusive scan of NV doubles on the DPP path (row_shr 1, 2, 4, 8 within rows of 16,
+// then row_bcast 15 and 31 across rows): VALU moves, no LDS round trip per step as the
+// ds_bpermute of __shfl_up
+template <int NV>
+MIMO_DEV void wave_scan_f64(double (&x)[NV]) {
+#pragma unroll
+  for (int k = 0; k < NV; k++) x[k] += dpp_f64<0x111>(x[k]);
+#pragma unroll
+  for (int k = 0; k < NV; k++) x[k] += dpp_f64<0x112>(x[k]);
+#pragma unroll
+  for (int k = 0; k < NV; k++) x[k] += dpp_f64<0x114>(x[k]);
+#pragma unroll
+  for (int k = 0; k < NV; k++) x[k] += dpp_f64<0x118>(x[k]);
+#pragma unroll
+  for (int k = 0; k < NV; k++) x[k] += dpp_f64<0x142, 0xA>(x[k]);
+#pragma unroll
+  for (int k = 0; k < NV; k++) x[k] += dpp_f64<0x143, 0xC>(x[k]);
+}
+
 // block-wide exclusive scan of NV doubles plus the block totals (one barrier; the caller
 // alternates ws between consecutive scans)
 template <int NV>
@@ -139,14 +167,7 @@ MIMO_DEV void block_scan(double (&v)[NV], double (&tot)[NV], double (*ws)[kScT /
   double inc[NV];
 #pragma unroll
   for (int k = 0; k < NV; k++) inc[k] = v[k];
-#pragma unroll
-  for (int off = 1; off < 64; off <<= 1) {
-#pragma unroll
-    for (int k = 0; k < NV; k++) {
-      const double o = __shfl_up(inc[k], off);
-      if (lane >= off) inc[k] += o;
-    }
-  }
+  wave_scan_f64<NV>(inc);
   if (lane == 63) {
 #pragma unroll
     for (int k = 0; k < NV; k++) ws[k][wv] = inc[k];
