@@ -35,6 +35,7 @@
 #include <cstdlib>
 
 #include "fft.hpp"
+#include "fft_reg.hpp"
 #include "kernels.hpp"
 
 namespace mimo {
@@ -913,6 +914,90 @@ __global__ __launch_bounds__(T) void spectra_kernel(DecodeArgs a) {
   for (int k = tid; k < M; k += T) o[(uint64_t)(k >> 6) * cstep + (k & 63)] = lds_sp[lds_pad(k)];
 }
 
+// Persistent form of spectra_kernel for M = 2^LOG2M >= 2048 (C4: M = 4096): each workgroup
+// walks (frame, symbol, antenna) items with a stride of the grid, the next item's body loaded
+// straight into registers (PTS = 16 per thread, in the order the first radix-16 pass reads)
+// while the current one is transformed (register-resident radix-16 Stockham FFT, two LDS
+// exchanges, base twiddles held per thread) and stored from registers (each wave store
+// instruction writes 512 contiguous bytes of one 64-subcarrier chunk). The one-item-per-
+// workgroup kernel waited on its load, four global twiddle reads and its stores in turn.
+template <int LOG2M, bool SC16>
+__global__ __launch_bounds__((1 << LOG2M) / 16) void spectra_persist_kernel(DecodeArgs a) {
+  using PL = RegPlan<LOG2M, 16>;
+  constexpr int M = 1 << LOG2M, T = PL::T, NCH = M / 64;
+  static_assert(T % 64 == 0, "whole waves");
+  extern __shared__ __attribute__((aligned(16))) float2 lds_sp[];
+  v2f *buf = reinterpret_cast<v2f *>(lds_sp);
+  const int tid = threadIdx.x;
+  v2f w1[PL::NTW > 0 ? PL::NTW : 1];
+  reg_twiddles<LOG2M, 16>(w1, a.tw, tid);
+  const uint32_t NI = a.N;
+  const uint64_t per_frame = (uint64_t)a.sym_cap * NI;
+  const uint64_t total = per_frame * a.n_frames;
+  const int64_t L = (int64_t)a.frame_len;
+  // item -> (frame, scratch slot, antenna); false when its symbol is not decoded
+  auto item = [&](uint64_t it, uint32_t &f, uint32_t &sl, uint32_t &r, int64_t &abs0,
+                  uint32_t &cap) -> bool {
+    f = (uint32_t)(it / per_frame);
+    const uint32_t rem = (uint32_t)(it % per_frame);
+    sl = rem / NI;
+    r = rem % NI;
+    const FrameInfo &I = a.info[f];
+    const uint32_t n_out = (I.status == 0) ? min(I.n_sym, a.max_out) : 0u;
+    abs0 = I.base + (int64_t)I.i0 + (int64_t)(a.sym0 + sl) * a.SL + a.cp;
+    cap = I.cap;
+    return a.sym0 + sl < n_out;
+  };
+  auto load = [&](v2f (&x)[16], uint32_t cap, uint32_t r, int64_t abs0) {
+    const auto xs = iq_row<SC16>(a.iq, a.iq_scale, ((uint64_t)cap * a.N + r) * a.stride);
+    if (abs0 >= 0 && abs0 + M <= L) {
+#pragma unroll
+      for (int e = 0; e < 16; e++) {
+        const float2 t = xs.at(abs0 + reg_index<LOG2M, 16>(tid, e));
+        x[e] = v2f{t.x, t.y};
+      }
+    } else {   // the capture's edge: zero outside it
+#pragma unroll
+      for (int e = 0; e < 16; e++) {
+        const int64_t n = abs0 + reg_index<LOG2M, 16>(tid, e);
+        const float2 t = xs.at(n < 0 ? 0 : (n >= L ? L - 1 : n));
+        x[e] = (n >= 0 && n < L) ? v2f{t.x, t.y} : v2f{0.0f, 0.0f};
+      }
+    }
+  };
+  uint64_t it = blockIdx.x;
+  uint32_t f = 0, sl = 0, r = 0, cap = 0;
+  int64_t abs0 = 0;
+  // the first live item of this workgroup
+  while (it < total && !item(it, f, sl, r, abs0, cap)) it += gridDim.x;
+  if (it >= total) return;                            // uniform
+  v2f v[16], nx[16];
+  load(v, cap, r, abs0);
+  for (;;) {
+    // the next live item's body, in flight during this transform
+    uint64_t nit = it + gridDim.x;
+    uint32_t nf = 0, nsl = 0, nr = 0, ncap = 0;
+    int64_t nabs0 = 0;
+    while (nit < total && !item(nit, nf, nsl, nr, nabs0, ncap)) nit += gridDim.x;
+    if (nit < total) load(nx, ncap, nr, nabs0);
+    reg_compute<LOG2M, 16, 0, false>(v, w1);
+    reg_rest<LOG2M, 16, 1, false>(buf, v, w1, tid);
+    // X[k], k = tid + T e, into [frame][chunk][slot][antenna][64]
+    float2 *o = a.spec + (((uint64_t)f * NCH * a.sym_cap + sl) * a.N + r) * 64;
+    const uint64_t cstep = (uint64_t)a.sym_cap * a.N * 64;
+#pragma unroll
+    for (int e = 0; e < 16; e++) {
+      const uint32_t k = (uint32_t)reg_index<LOG2M, 16>(tid, e);
+      o[(uint64_t)(k >> 6) * cstep + (k & 63)] = make_float2(v[e].x, v[e].y);
+    }
+    if (nit >= total) break;                          // uniform
+    it = nit; f = nf; sl = nsl; r = nr;
+#pragma unroll
+    for (int e = 0; e < 16; e++) v[e] = nx[e];
+    // (reg_rest opens with a barrier: this transform's LDS readers finish before the next store)
+  }
+}
+
 template <int NA, int REF>
 __global__ __launch_bounds__(32 * NA) void apply_split_kernel(DecodeArgs a) {
   constexpr int T = 32 * NA;                          // NA/2 waves
@@ -1072,6 +1157,14 @@ uint32_t split_plan(uint32_t max_out, int log2M, uint32_t *groups_out, uint32_t 
   return groups * NCH * P * 4 / kSplitSets;
 }
 
+// workgroups of a kernel resident per CU at this block size and dynamic LDS (a persistent
+// grid is that many times the CU count: no workgroup waits for another to finish)
+static uint32_t resident_blocks(const void *k, int threads, size_t shm) {
+  int n = 1;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k, threads, shm) != hipSuccess || n < 1) n = 1;
+  return (uint32_t)n;
+}
+
 // 8x8 split decode; returns the partial sets per record (0: not handled)
 uint32_t launch_decode_split(const DecodeArgs &a, int log2M, uint32_t n_frames, hipStream_t s) {
   if (!a.spec || !a.nrec || !decode_split_accepts(a, log2M)) return 0;
@@ -1093,13 +1186,22 @@ uint32_t launch_decode_split(const DecodeArgs &a, int log2M, uint32_t n_frames, 
     if (a.sc16) hipLaunchKernelGGL((spectra_kernel<L2, T1, true>), g1, dim3(T1), shm, s, g); \
     else hipLaunchKernelGGL((spectra_kernel<L2, T1, false>), g1, dim3(T1), shm, s, g);       \
   } while (0)
+#define SPECTRA_P(L2)                                                                    \
+  do {                                                                                   \
+    constexpr int TP = (1 << L2) / 16;                                                   \
+    auto kp = a.sc16 ? spectra_persist_kernel<L2, true> : spectra_persist_kernel<L2, false>; \
+    hipLaunchKernelGGL(kp, dim3(a.n_cu * resident_blocks((const void *)kp, TP, shm)), dim3(TP), \
+                       shm, s, g);                                                       \
+  } while (0)
+    static const bool one_item = [] { const char *e = getenv("RMIMO_SPECTRA_ITEM"); return e && e[0] == '1'; }();
     switch (log2M) {
       case 9: SPECTRA(9); break;
       case 10: SPECTRA(10); break;
-      case 11: SPECTRA(11); break;
-      default: SPECTRA(12); break;
+      case 11: if (one_item) SPECTRA(11); else SPECTRA_P(11); break;
+      default: if (one_item) SPECTRA(12); else SPECTRA_P(12); break;
     }
 #undef SPECTRA
+#undef SPECTRA_P
     if (a.ref_mode == 1) hipLaunchKernelGGL((apply_split_kernel<8, 1>), g2, dim3(256), 0, s, g);
     else if (a.ref_mode == 2) hipLaunchKernelGGL((apply_split_kernel<8, 2>), g2, dim3(256), 0, s, g);
     else hipLaunchKernelGGL((apply_split_kernel<8, 0>), g2, dim3(256), 0, s, g);
