@@ -1096,8 +1096,12 @@ __global__ __launch_bounds__(32 * NA) void apply_split_kernel(DecodeArgs a) {
       e_num[tt] = __builtin_fmaf(er.x, er.x, __builtin_fmaf(er.y, er.y, e_num[tt]));
       e_den[tt] = __builtin_fmaf(pt.x, pt.x, __builtin_fmaf(pt.y, pt.y, e_den[tt]));
 #ifndef SPLIT_ABL_NOSTORE   // timing ablation: no output stores
+#ifndef SPLIT_ABL_NOSYM       // (timing ablation: no symbol stores)
       if (a.out_sym) reinterpret_cast<v2f *>(a.out_sym)[o] = acc;
+#endif
+#ifndef SPLIT_ABL_NOIDX       // (timing ablation: no index stores)
       if (a.out_idx) a.out_idx[o] = (uint8_t)d;
+#endif
 #endif
     }
   };
@@ -1123,6 +1127,138 @@ __global__ __launch_bounds__(32 * NA) void apply_split_kernel(DecodeArgs a) {
 #pragma unroll
     for (int tt = 0; tt < 2; tt++)
       if (t == 2 * h + tt) v = comp == 0 ? e_num[tt] : (comp == 1 ? e_den[tt] : (float)n_err[tt]);
+    ep[lane] = (double)v;
+  }
+}
+
+// The same 8x8 apply over 128-subcarrier chunks: wave w owns output stream w and lane l the
+// adjacent subcarriers 2l, 2l+1 of the chunk, so each lane stores 16 bytes of symbols and 2 of
+// indices per symbol (a wave writes 1 KB of symbols and one whole 128-byte line of indices).
+// The 64-subcarrier form (apply_split_kernel, RMIMO_APPLY_V1=1) wrote 64-byte index segments:
+// 98 of its 767 us at C4 x 8 went to the index stores (a store-ablation build), for 11% of
+// the bytes. EVM sets: (group, chunk, range, wave), NA per record as before.
+template <int NA, int REF>
+__global__ __launch_bounds__(64 * NA) void apply_split2_kernel(DecodeArgs a) {
+  constexpr int T = 64 * NA;                          // NA waves: one output stream each
+  constexpr int PF = 4;                               // symbols in flight per workgroup
+  constexpr int CW = 128;                             // subcarriers per chunk
+  static_assert(NA == 8, "one 16-byte load per thread covers a symbol's 8 x 128 spectra");
+  const uint32_t c2 = blockIdx.x, f = blockIdx.y, part = blockIdx.z;
+  const uint32_t NCH2 = gridDim.x, P = gridDim.z, NCH = 2 * NCH2;   // NCH: scratch chunks of 64
+  const int tid = threadIdx.x, lane = tid & 63;
+  const uint32_t w = __builtin_amdgcn_readfirstlane((uint32_t)tid >> 6);
+  __shared__ v2f ptab[kStreamMaxQam];
+  __shared__ __attribute__((aligned(16))) v2f xs[2][NA * CW];     // [antenna][subcarrier]
+  __shared__ __attribute__((aligned(16))) uint8_t rs[2][NA * CW];   // [stream][subcarrier]
+  for (uint32_t e = tid; e < a.qam.L * a.qam.L; e += T) {
+    const float2 p = qam_point(e, a.qam);
+    ptab[e] = v2f{p.x, p.y};
+  }
+  const FrameInfo &I = a.info[f];
+  const uint32_t n_out = (I.status == 0) ? min(I.n_sym, a.max_out) : 0u;
+  const uint32_t grp = a.sym0 / a.sym_cap;            // this launch's symbol group
+  if (grp == 0 && c2 == 0 && part == 0 && tid == 0)
+    a.nrec[f] = a.sym_groups * NCH2 * P * (T / 64) / kSplitSets;
+  const uint32_t ng = n_out > a.sym0 ? min(n_out - a.sym0, a.sym_cap) : 0u;
+  const uint32_t s0 = a.sym0 + (uint32_t)((uint64_t)ng * part / P);
+  const uint32_t s1 = a.sym0 + (uint32_t)((uint64_t)ng * (part + 1) / P);
+  const uint32_t M = a.M, kb = c2 * CW + 2 * lane;    // this lane's subcarriers kb, kb + 1
+  v2f Wr[2][NA];
+  {
+    const float2 g2 = *reinterpret_cast<const float2 *>(a.gain + (uint64_t)f * M + kb);
+    const float gk0 = g2.x * a.dn, gk1 = g2.y * a.dn;
+#pragma unroll
+    for (int r = 0; r < NA; r++) {
+      const float4 wv = *reinterpret_cast<const float4 *>(a.W + (((uint64_t)f * NA + w) * NA + r) * M + kb);
+      Wr[0][r] = v2f{wv.x * gk0, wv.y * gk0};
+      Wr[1][r] = v2f{wv.z * gk1, wv.w * gk1};
+    }
+  }
+  const v2f inv_sc = v2f{a.qam.inv_scale, a.qam.inv_scale};
+  const v2f Lf = v2f{(float)a.qam.L, (float)a.qam.L};
+  const uint32_t Lm1 = a.qam.L - 1;
+  const uint64_t frame_id = a.frame_id0 + I.ref;
+  // thread t loads float4 u = t % 256 of the symbol's 4 KB block of 64-chunk 2 c2 + t / 256
+  // (antenna u / 32, subcarriers 2 (u % 32) + 0, 1); threads < 64 load 16 bytes of reference
+  // indices (stream t / 8, bytes 16 (t % 8) ..)
+  const uint32_t half = (uint32_t)tid >> 8, u = (uint32_t)tid & 255u;
+  const float4 *spec4 = reinterpret_cast<const float4 *>(a.spec) +
+                        ((uint64_t)f * NCH + 2 * c2 + half) * a.sym_cap * (NA * 64 / 2) + u;
+  v4f *xdst0 = reinterpret_cast<v4f *>(&xs[0][(u >> 5) * CW + half * 64 + 2 * (u & 31)]);
+  v4f *xdst1 = reinterpret_cast<v4f *>(&xs[1][(u >> 5) * CW + half * 64 + 2 * (u & 31)]);
+  const uint8_t *refb = (REF == 1) ? a.ref_idx + ((uint64_t)I.ref * NA + (tid >> 3)) * a.max_out * a.M_occ +
+                                         c2 * CW + (tid & 7) * 16
+                                   : nullptr;
+  const uint32_t slast = s1 > s0 ? s1 - 1 : s0;
+  float4 pf0, pf1, pf2, pf3;                          // symbol slots (named: no scratch)
+  uint4 pr0, pr1, pr2, pr3;
+  auto load_sym = [&](float4 &x, uint4 &r, uint32_t s) {
+    const uint32_t sc = min(s, slast);
+    x = spec4[(uint64_t)(sc - a.sym0) * (NA * 64 / 2)];
+    if constexpr (REF == 1)
+      if (tid < 64) r = *reinterpret_cast<const uint4 *>(refb + (uint64_t)sc * a.M_occ);
+  };
+  if (s0 < s1) {
+    load_sym(pf0, pr0, s0);
+    load_sym(pf1, pr1, s0 + 1);
+    load_sym(pf2, pr2, s0 + 2);
+    load_sym(pf3, pr3, s0 + 3);
+  }
+  float e_num = 0.0f, e_den = 0.0f;
+  uint32_t n_err = 0u;
+  auto one = [&](float4 &x, uint4 &r, uint32_t s, int b) {
+    *(b ? xdst1 : xdst0) = v4f{x.x, x.y, x.z, x.w};
+    if constexpr (REF == 1)
+      if (tid < 64) reinterpret_cast<uint4 *>(rs[b])[tid] = r;
+    load_sym(x, r, s + PF);
+    __syncthreads();                                  // xs[b] complete; xs[b^1] readers done
+    if (s >= s1) return;                              // uniform: the range's last block
+    v2f acc[2] = {v2f{0.0f, 0.0f}, v2f{0.0f, 0.0f}};
+#pragma unroll
+    for (int q = 0; q < NA; q++) {
+      const v4f xv = *reinterpret_cast<const v4f *>(&xs[b][q * CW + 2 * lane]);
+      acc[0] = cmac_pk(acc[0], Wr[0][q], v2f{xv.x, xv.y});
+      acc[1] = cmac_pk(acc[1], Wr[1][q], v2f{xv.z, xv.w});
+    }
+    uint32_t d[2];
+#pragma unroll
+    for (int j = 0; j < 2; j++) {
+      d[j] = qam_slice_pk(acc[j], inv_sc, Lf, Lm1, a.qam.b);
+      uint32_t refi;
+      if constexpr (REF == 1) refi = rs[b][w * CW + 2 * lane + j];
+      else if constexpr (REF == 2)
+        refi = (uint32_t)(hash5(a.ref_seed, DOM_DATA, frame_id, w, (uint64_t)s * a.M_occ + kb + j) &
+                          (uint64_t)(a.qam.L * a.qam.L - 1));
+      else refi = d[j];
+      n_err += (uint32_t)__builtin_popcountll(__builtin_amdgcn_ballot_w64(refi != d[j]));
+      const v2f pt = ptab[refi];
+      const v2f er = acc[j] - pt;
+      e_num = __builtin_fmaf(er.x, er.x, __builtin_fmaf(er.y, er.y, e_num));
+      e_den = __builtin_fmaf(pt.x, pt.x, __builtin_fmaf(pt.y, pt.y, e_den));
+    }
+    const uint64_t o = (((uint64_t)f * NA + w) * a.max_out + s) * a.M_occ + kb;
+    if (a.out_sym)
+      *reinterpret_cast<v4f *>(reinterpret_cast<v2f *>(a.out_sym) + o) =
+          v4f{acc[0].x, acc[0].y, acc[1].x, acc[1].y};
+    if (a.out_idx) *reinterpret_cast<uint16_t *>(a.out_idx + o) = (uint16_t)(d[0] | (d[1] << 8));
+  };
+  for (uint32_t sb = s0; sb < s1; sb += PF) {
+    one(pf0, pr0, sb, 0);
+    one(pf1, pr1, sb + 1, 1);
+    one(pf2, pr2, sb + 2, 0);
+    one(pf3, pr3, sb + 3, 1);
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    e_num += __shfl_xor(e_num, off);
+    e_den += __shfl_xor(e_den, off);
+  }
+  // partial set ((grp * NCH2 + c2) * P + part) * waves + w: this wave's stream, zeros elsewhere
+  const uint64_t set = (((uint64_t)grp * NCH2 + c2) * P + part) * (T / 64) + w;
+  double *ep = a.evm_part + ((uint64_t)f * a.rec_stride * kSplitSets + set) * NA * 3;
+  if (lane < NA * 3) {
+    const uint32_t t = lane / 3, comp = lane % 3;
+    const float v = t != w ? 0.0f : (comp == 0 ? e_num : (comp == 1 ? e_den : (float)n_err));
     ep[lane] = (double)v;
   }
 }
@@ -1202,9 +1338,19 @@ uint32_t launch_decode_split(const DecodeArgs &a, int log2M, uint32_t n_frames, 
     }
 #undef SPECTRA
 #undef SPECTRA_P
-    if (a.ref_mode == 1) hipLaunchKernelGGL((apply_split_kernel<8, 1>), g2, dim3(256), 0, s, g);
-    else if (a.ref_mode == 2) hipLaunchKernelGGL((apply_split_kernel<8, 2>), g2, dim3(256), 0, s, g);
-    else hipLaunchKernelGGL((apply_split_kernel<8, 0>), g2, dim3(256), 0, s, g);
+    static const bool v1_env = [] { const char *e = getenv("RMIMO_APPLY_V1"); return e && e[0] == '1'; }();
+    // (the 128-subcarrier form stores 16 bytes of symbols and 2 of indices per lane)
+    const bool v1 = v1_env || ((uintptr_t)a.out_sym & 15u) || ((uintptr_t)a.out_idx & 1u);
+    if (v1) {
+      if (a.ref_mode == 1) hipLaunchKernelGGL((apply_split_kernel<8, 1>), g2, dim3(256), 0, s, g);
+      else if (a.ref_mode == 2) hipLaunchKernelGGL((apply_split_kernel<8, 2>), g2, dim3(256), 0, s, g);
+      else hipLaunchKernelGGL((apply_split_kernel<8, 0>), g2, dim3(256), 0, s, g);
+    } else {
+      const dim3 g3(NCH / 2, n_frames, P);
+      if (a.ref_mode == 1) hipLaunchKernelGGL((apply_split2_kernel<8, 1>), g3, dim3(512), 0, s, g);
+      else if (a.ref_mode == 2) hipLaunchKernelGGL((apply_split2_kernel<8, 2>), g3, dim3(512), 0, s, g);
+      else hipLaunchKernelGGL((apply_split2_kernel<8, 0>), g3, dim3(512), 0, s, g);
+    }
   }
   return kSplitSets;
 }
