@@ -96,26 +96,40 @@ MIMO_DEV uint32_t opq_s(uint32_t x) {
 template <int NS, int R>
 constexpr int st_off(int r) { return r * NS + (r * NS) / 32; }
 
-template <int LOG2M, int NA, int P>
+// The wave-local 256-point sub-transforms (WavePlan with M/8 = 256) use a second padding,
+// pad2(i) = i + i/32 + 4 (i/64): with one slot per 32 the middle pass's stores (elements
+// 64 (j/8) + j%8 + 8 r) hit 4-way bank conflicts; pad2 leaves them 2-way and every other
+// access of the region conflict-free (searched over additive paddings and XOR swizzles of the
+// region's six access patterns; none is conflict-free everywhere). The identities the
+// compile-time offsets rely on hold for that plan: pad2(o + r NS) = pad2(o) + pad2(r NS) and
+// pad2(j + r NB) = pad2(j) + pad2(r NB) for its stores (o = (j/NS) NS R + j%NS) and loads
+// (j < NB, NB = 32 or 64).
+MIMO_DEV constexpr int pad2(int i) { return i + (i >> 5) + 4 * (i >> 6); }
+template <int PADK>
+MIMO_DEV constexpr int padk(int i) { return PADK ? pad2(i) : i + (i >> 5); }   // (lds_pad)
+
+template <int LOG2M, int NA, int P, int PADK = 0>
 MIMO_DEV void st_store(v2f *buf, const v2f *v, uint32_t tid) {
   using PL = StreamPlan<LOG2M, NA>;
   constexpr uint32_t R = PL::radix(P), NS = PL::ns(P), NB = PL::M / R;
   static_assert(NB % 32 == 0 && (NS >= 32 || (32 % (NS * R) == 0) || (NS * R) % 32 == 0),
                 "padded-offset identity");
+  static_assert(!PADK || PL::M == 256, "pad2 identities checked for the 256-point plan only");
 #pragma unroll
   for (int i = 0; i < PL::bt(P); i++) {
     const uint32_t u = tid + i * PL::T, g = u / NB, j = u % NB;
     const uint32_t o = (j / NS) * NS * R + (j % NS);
-    v2f *bp = buf + g * PL::PB + lds_pad((int)o);
+    v2f *bp = buf + g * PL::PB + padk<PADK>((int)o);
 #pragma unroll
-    for (int r = 0; r < (int)R; r++) bp[st_off<NS, R>(r)] = v[i * R + r];
+    for (int r = 0; r < (int)R; r++)
+      bp[PADK ? pad2(r * (int)NS) : st_off<NS, R>(r)] = v[i * R + r];
   }
 }
 
 // pass P with its base twiddle from the LDS table (twl: passes 1.. in order, one row of NS
 // entries each, [jm] = e^{-2 pi i jm / (NS R)}) and the powers r = 2 .. R-1 in registers: one
 // LDS read per butterfly instead of R - 1 (the transform phase is bound by LDS instructions)
-template <int LOG2M, int NA, int P>
+template <int LOG2M, int NA, int P, int PADK = 0>
 MIMO_DEV void st_load_t(const v2f *buf, v2f *v, const v2f *twl, uint32_t tid) {
   using PL = StreamPlan<LOG2M, NA>;
   constexpr uint32_t R = PL::radix(P), NB = PL::M / R, NS = PL::ns(P);
@@ -127,9 +141,10 @@ MIMO_DEV void st_load_t(const v2f *buf, v2f *v, const v2f *twl, uint32_t tid) {
 #pragma unroll
   for (int i = 0; i < PL::bt(P); i++) {
     const uint32_t u = tid + i * PL::T, g = u / NB, j = u % NB;
-    const v2f *bp = buf + g * PL::PB + lds_pad((int)j);
+    const v2f *bp = buf + g * PL::PB + padk<PADK>((int)j);
 #pragma unroll
-    for (int r = 0; r < (int)R; r++) v[i * R + r] = bp[r * NB + (r * NB) / 32];
+    for (int r = 0; r < (int)R; r++)
+      v[i * R + r] = bp[PADK ? pad2(r * (int)NB) : r * NB + (r * NB) / 32];
     v2f w[R];
     twiddle_powers<R>(w, twl[OFF + (j % NS)]);
 #pragma unroll
@@ -166,7 +181,8 @@ template <int LOG2M, int NA>
 struct WavePlan {
   static constexpr int M = 1 << LOG2M, MS = M / 8, LG = MS / 8;
   using SP = StreamPlan<LOG2M - 3, 1>;
-  static constexpr int QS = ((lds_padded_len(MS) + 3) / 8) * 8 + 4;
+  static constexpr int PADK = (MS == 256) ? 1 : 0;      // region padding (pad2 for 256 points)
+  static constexpr int QS = ((padk<PADK>(MS - 1) + 1 + 3) / 8) * 8 + 4;
   static constexpr int GS = 8 * QS;
   static constexpr int TW0 = MS;                         // W_M^n, n < MS (powers q = 2..7 in registers)
   static constexpr int TWS = [] {
@@ -184,17 +200,17 @@ MIMO_DEV void lds_wave_sync() {
 
 // sub-transform passes P .. NP-1 on a lane group (pass P-1's outputs in registers), ending with
 // the natural-order store
-template <int L2, int P>
+template <int L2, int P, int PADK>
 MIMO_DEV void wave_passes(v2f *buf, v2f *v, const v2f *twl, uint32_t s) {
   using SP = StreamPlan<L2, 1>;
   if constexpr (P < SP::NP) {
-    st_store<L2, 1, P - 1>(buf, v, s);
+    st_store<L2, 1, P - 1, PADK>(buf, v, s);
     lds_wave_sync();
-    st_load_t<L2, 1, P>(buf, v, twl, s);
-    wave_passes<L2, P + 1>(buf, v, twl, s);
+    st_load_t<L2, 1, P, PADK>(buf, v, twl, s);
+    wave_passes<L2, P + 1, PADK>(buf, v, twl, s);
   } else {
     lds_wave_sync();
-    st_store<L2, 1, SP::NP - 1>(buf, v, s);
+    st_store<L2, 1, SP::NP - 1, PADK>(buf, v, s);
   }
 }
 
@@ -672,7 +688,7 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
       twiddle_powers<8>(w, twl[n]);
 #pragma unroll
       for (int q = 1; q < 8; q++) v[q] = cmul_pk(v[q], w[q]);
-      v2f *e = img + g * GS + lds_pad((int)n);
+      v2f *e = img + g * GS + padk<WP::PADK>((int)n);
 #pragma unroll
       for (int q = 0; q < 8; q++) e[q * QS] = v[q];
     }
@@ -701,14 +717,15 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
     if constexpr (WF) {
       // sub-transform (g, q) on lane group t0 / LG, inside one wave
       static_assert(LG % 32 == 0, "lds_pad(s + r LG) = lds_pad(s) + r (LG + LG/32)");
+      static_assert(!WP::PADK || LG == 32, "pad2(s + 32 r) = pad2(s) + pad2(32 r) for s < 32");
       const uint32_t t0 = (uint32_t)opq(tid);
       const uint32_t s = t0 & (LG - 1), sg = t0 / LG;
       v2f *rg = img + (sg >> 3) * GS + (sg & 7) * QS;
-      const v2f *rp = rg + lds_pad((int)s);
+      const v2f *rp = rg + padk<WP::PADK>((int)s);
 #pragma unroll
-      for (int r = 0; r < 8; r++) v[r] = rp[r * (LG + LG / 32)];
+      for (int r = 0; r < 8; r++) v[r] = rp[WP::PADK ? pad2(r * LG) : r * (LG + LG / 32)];
       dft_fwd_pk<8>(v);
-      wave_passes<LOG2M - 3, 1>(rg, v, twl + WP::TW0, s);
+      wave_passes<LOG2M - 3, 1, WP::PADK>(rg, v, twl + WP::TW0, s);
       __syncthreads();                                // every spectrum in its region
     } else {
       st_store<LOG2M, NA, 0>(img, v, (uint32_t)opq(tid));
@@ -766,7 +783,7 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
 #pragma unroll
       for (int q = 0; q < S; q++) {
         const uint32_t kk = (uint32_t)opq(tid) * S + q;
-        const v2f *xp = img + (kk & 7u) * QS + lds_pad((int)(kk >> 3));
+        const v2f *xp = img + (kk & 7u) * QS + padk<WP::PADK>((int)(kk >> 3));
 #pragma unroll
         for (int r = 0; r < NA; r++) X[q][r] = xp[r * GS];
       }
@@ -792,7 +809,7 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
         v2f X[NA];
         if constexpr (WF) {
           const uint32_t kk = (uint32_t)opq(tid) + q * T;
-          const v2f *xp = img + (kk & 7u) * QS + lds_pad((int)(kk >> 3));
+          const v2f *xp = img + (kk & 7u) * QS + padk<WP::PADK>((int)(kk >> 3));
 #pragma unroll
           for (int r = 0; r < NA; r++) X[r] = xp[r * GS];
         } else {
