@@ -52,6 +52,10 @@ namespace mimo {
 #else
 #define DSP(...)
 #endif
+// staging DMA issued by one wave per antenna row (0: spread over every wave, the round-3 form)
+#ifndef DS_ROW_DMA
+#define DS_ROW_DMA 1
+#endif
 constexpr uint32_t kStreamMaxFrames = 192;   // per-frame tables in LDS beside a 157 KB working set
 constexpr uint32_t kStreamMaxQam = 256;          // constellation points (256-QAM)
 
@@ -326,6 +330,10 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
   constexpr int RS = M + SPC;
   constexpr int NBLK = (RS / SPC + 63) / 64;      // wave DMA instructions per staged row
   constexpr int NWI = (NA * NBLK + T / 64 - 1) / (T / 64);   // ... per wave and symbol
+  constexpr int LASTC = RS / SPC - (NBLK - 1) * 64;          // chunks in a row's last block
+  static_assert(RS % SPC == 0 && LASTC >= 1 && LASTC <= 64 && 64 * SPC * SB == 1024,
+                "row DMA blocks of 1 KB");
+  static_assert(!DS_ROW_DMA || NA <= T / 64, "one wave per staged row");
   constexpr int NREF = NA * M / 16;               // 16-byte chunks of the reference indices
   // store instructions per symbol: the wait at the top of a symbol leaves them in flight
   using WP = WavePlan<LOG2M, NA>;
@@ -436,23 +444,59 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
   // sample a_g <= its first sample e_g (alignment taken in the whole batch, so rows of any
   // stride stay on the DMA path and every lane moves one aligned 16-byte chunk); returns the
   // offsets e_g - a_g (< SPC), 4 bits per row
-  auto fetch = [&](uint32_t ff, uint32_t ss) -> uint32_t {
+  // per-frame bases of the staging (uniform, SGPRs; read from the LDS frame tables once per
+  // frame instead of once per symbol): first body sample, row 0's batch offset, reference row
+  struct FrameBase {
+    int64_t body, row0;
+    uint64_t ref;
+  };
+  auto frame_base = [&](uint32_t ff) -> FrameBase {
     const int64_t b0 = fbody[ff];
-    const int64_t abs0 = (int64_t)((((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)b0)) |
-                                    ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)((uint64_t)b0 >> 32)) << 32))) +
-                         (int64_t)ss * a.SL;
-    const int64_t row0 = (int64_t)(__builtin_amdgcn_readfirstlane(fcr[ff]) & 0xFFFFu) * NA * (int64_t)a.stride;
+    const uint32_t cr = __builtin_amdgcn_readfirstlane(fcr[ff]);
+    FrameBase fb;
+    fb.body = (int64_t)((((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)b0)) |
+                         ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)((uint64_t)b0 >> 32)) << 32)));
+    fb.row0 = (int64_t)(cr & 0xFFFFu) * NA * (int64_t)a.stride;
+    fb.ref = (uint64_t)(cr >> 16) * NA * a.max_out * a.M_occ;
+    return fb;
+  };
+  // the rows' offsets e_g - a_g in SPC-sample chunks are (e0 + g stride) mod SPC: nibble g of
+  // (ptn + (e0 mod SPC) * REP) with ptn's nibble g = (g stride) mod SPC (sums < 16, no carries)
+  constexpr uint32_t REP = NA == 1 ? 0x1u : (NA == 2 ? 0x11u : (NA == 4 ? 0x1111u : 0x11111111u));
+  uint32_t ptn = 0;
+#pragma unroll
+  for (int g = 0; g < NA; g++) ptn |= (((uint32_t)g * (uint32_t)a.stride) & (SPC - 1)) << (4 * g);
+  ptn = __builtin_amdgcn_readfirstlane(ptn);
+  auto fetch = [&](const FrameBase &fb, uint32_t ss) -> uint32_t {
+    const int64_t abs0 = fb.body + (int64_t)((uint64_t)ss * a.SL);
+    const int64_t row0 = fb.row0;
     const int64_t e0 = row0 + abs0;                   // batch sample index of row 0's first
     const int t0 = opq(tid);
-    uint32_t odds = 0;
-#pragma unroll
-    for (int g = 0; g < NA; g++)
-      odds |= (uint32_t)((e0 + (int64_t)g * a.stride) & (SPC - 1)) << (4 * g);
+    const uint32_t odds = (ptn + ((uint32_t)e0 & (SPC - 1)) * REP) & ((SPC - 1) * REP);
 #ifdef DS_ABL_NODMA   // timing ablation (tools/abl_decode.sh): no sample loads
     if (true) {
     } else
 #endif
     if (abs0 >= SPC && abs0 + RS <= (int64_t)a.frame_len && ((uintptr_t)a.iq & 15u) == 0) {
+#if DS_ROW_DMA
+      // wave g < NA stages antenna row g: NBLK wave instructions of 64 consecutive 16-byte
+      // chunks from the row's aligned start a_g (its last block is the row's one remaining
+      // chunk). Only NA waves compute the row base and issue DMAs: the address arithmetic is
+      // scalar, and 16 waves doing it at once kept the CU's one scalar unit busy ~2k cycles
+      // per symbol while every VALU waited; the other waves start their sub-transforms
+      if (wv < (uint32_t)NA) {
+        const uint32_t g = wv;
+        const int64_t ag = (e0 + (int64_t)g * a.stride) & ~(int64_t)(SPC - 1);
+        const auto xa = sgpr_ptr(reinterpret_cast<const char *>(a.iq) + ag * SB);
+        const uint32_t lane = (uint32_t)(opq(tid) & 63);
+        const uint32_t dst0 = __builtin_amdgcn_readfirstlane(stg_base + g * RS * (uint32_t)SB);
+#pragma unroll
+        for (int b = 0; b < NBLK; b++) {
+          if (b + 1 < NBLK || lane < (uint32_t)LASTC)
+            dma16((uint32_t)b * 1024u + lane * 16u, xa, dst0 + (uint32_t)b * 1024u);
+        }
+      }
+#else
       // base SPC samples before row 0's aligned start: every row's a_g - base is in [0, 2^32).
       // One wave instruction moves 64 consecutive chunks of one row (row g, block b uniform;
       // a row's last block is its one remaining chunk), so the lane offsets are a scalar plus
@@ -472,6 +516,7 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
           if (b + 1 < NBLK || lane16 == 0) dma16(voff + lane16, xa, dst);
         }
       }
+#endif
     } else {                                          // edge of the capture: guarded loads
       const char *xf = reinterpret_cast<const char *>(a.iq) + row0 * SB;
       for (int c = t0; c < NA * RS; c += T) {
@@ -488,10 +533,15 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
       }
     }
     if constexpr (REF == 1) {
-      if (t0 < NREF) {
-        const uint32_t dst = __builtin_amdgcn_readfirstlane(rstg_base + (uint32_t)(wv * 64) * 16u);
-        const uint32_t t = (uint32_t)t0 / (M / 16), q = (uint32_t)t0 % (M / 16);
-        const auto rb = sgpr_ptr(a.ref_idx + ((uint64_t)(__builtin_amdgcn_readfirstlane(fcr[ff]) >> 16) * NA * a.max_out + ss) * a.M_occ);
+      // (waves RW0 .. RW0 + NREF/64 - 1: with DS_ROW_DMA the waves after the row waves)
+      constexpr int RW0 = DS_ROW_DMA ? NA : 0;
+      static_assert(!DS_ROW_DMA || (NREF % 64 == 0 && RW0 + NREF / 64 <= T / 64),
+                    "reference DMA waves after the row waves");
+      const int tr = t0 - RW0 * 64;
+      if (tr >= 0 && tr < NREF) {
+        const uint32_t dst = __builtin_amdgcn_readfirstlane(rstg_base + (uint32_t)((wv - RW0) * 64) * 16u);
+        const uint32_t t = (uint32_t)tr / (M / 16), q = (uint32_t)tr % (M / 16);
+        const auto rb = sgpr_ptr(a.ref_idx + fb.ref + (uint64_t)ss * a.M_occ);
         dma16(t * (uint32_t)(a.max_out * a.M_occ) + 16 * q, rb, dst);
       }
     }
@@ -597,7 +647,8 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
   };
   load_w(f);
   cfo_frame(f, s);
-  uint32_t odd = fetch(f, s);
+  FrameBase fbase = frame_base(f);
+  uint32_t odd = fetch(fbase, s);
   // the first symbol's staging (issued after the weight loads: the counted wait in the loop
   // assumes only stores behind the DMA)
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -698,16 +749,19 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
     // the item after this one (uniform) and its staging, in flight during this symbol
     uint32_t fn = f, sn = s + 1, n_out_n = n_out_f;
     uint32_t odd_n = 0;
+    FrameBase fbase_n = fbase;
     if (i + 1 < i_end) {
       if (sn >= n_out_f) {
         do { fn++; } while (pfx[fn + 1] == pfx[fn]);
         sn = 0;
         n_out_n = pfx[fn + 1] - pfx[fn];
+        fn = __builtin_amdgcn_readfirstlane(fn);
+        fbase_n = frame_base(fn);
       }
       fn = __builtin_amdgcn_readfirstlane(fn);
       sn = __builtin_amdgcn_readfirstlane(sn);
       n_out_n = __builtin_amdgcn_readfirstlane(n_out_n);
-      odd_n = fetch(fn, sn);
+      odd_n = fetch(fbase_n, sn);
     }
     // passes 1 .. NP-1 through the LDS images (pass 1 needs no leading barrier: the previous
     // symbol's image readers finished before the barrier at the top), then the exchange that
@@ -874,6 +928,7 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
     f = __builtin_amdgcn_readfirstlane(fn);
     s = __builtin_amdgcn_readfirstlane(sn);
     odd = __builtin_amdgcn_readfirstlane(odd_n);
+    fbase = fbase_n;
   }
   DSP(if (a.prof && threadIdx.x == 0) {
     for (int q = 0; q < 8; q++) atomicAdd(&a.prof[q], ds_t[q]);
