@@ -441,6 +441,9 @@ int run_sync(mimo_rx *h, const float2 *iq, uint64_t stride, uint32_t F, uint64_t
       sa.chunk_len = K; sa.chunk_lo = chunk_lo; sa.nchunks = nchunks;
       sa.flag = h->scr_flag.p; sa.fmin = h->scr_min.p; sa.fmax = h->scr_max.p;
       sa.count = a.hot_count; sa.hot = a.hot; sa.cap = a.hot_cap;
+      // batches: every capture starts at its (first) framesync's origin; the streaming execute's
+      // capture may begin mid-stream after a trim (its history is not empty)
+      sa.empty_history = reset_trig ? 1u : 0u;
       if (a.diag & 32) a.diag |= 16;   // diagnostics: finalize as a separate kernel
       // Two phases for one frame per capture: the first eighth of every capture's chunks (a
       // frame's S0 plateau sits near its capture's start), then the rest only for captures with
@@ -453,10 +456,11 @@ int run_sync(mimo_rx *h, const float2 *iq, uint64_t stride, uint32_t F, uint64_t
                               ? std::max<uint64_t>(2, nchunks / 8) : nchunks;
       sa.chunk_hi = c1;
       launch_sc_screen(sa, F, s);
-      launch_sc_exact(a, s);   // resolves and finalises its items itself
+      ScArgs a1 = a;
+      if (c1 < nchunks) a1.snap = h->queue.p + 2;   // phase-1 items: done after this launch
+      launch_sc_exact(a1, s);   // resolves and finalises its items itself
       if (a.diag & 32) launch_sc_finalize(a, s);
       if (c1 < nchunks) {
-        launch_sc_snapshot(h->queue.p + 2, a.hot_count, s);   // phase-1 items: done
         sa.chunk_lo = c1;
         sa.chunk_hi = nchunks;
         sa.trig = h->trig.p;
@@ -497,11 +501,13 @@ int run_sync(mimo_rx *h, const float2 *iq, uint64_t stride, uint32_t F, uint64_t
               v[14] & 0xFFFFFFFFull, v[15]);
       const double np = v[4] ? (double)v[4] : 1.0;
       fprintf(stderr, "exact_split record %.2f us setup %.2f us iterations %.2f us (%.2f per pass) "
-              "start offset avg %.2f max %.2f us | per iteration: ring %.2f scan %.2f walk %.2f us\n",
+              "start offset avg %.2f max %.2f us | per iteration: ring %.2f scan %.2f walk %.2f us "
+              "(first iteration's ring %.2f us per pass; guarded fills %llu)\n",
               v[20] / np / 100.0, v[21] / np / 100.0,
               v[22] / np / 100.0, v[23] / np, (v[26] / np - (double)v[0]) / 100.0,
               (double)(v[25] - v[0]) / 100.0, v[23] ? v[16] / (double)v[23] / 100.0 : 0.0,
-              v[23] ? v[17] / (double)v[23] / 100.0 : 0.0, v[23] ? v[18] / (double)v[23] / 100.0 : 0.0);
+              v[23] ? v[17] / (double)v[23] / 100.0 : 0.0, v[23] ? v[18] / (double)v[23] / 100.0 : 0.0,
+              v[19] / np / 100.0, v[24]);
     } else if (prof_env) {   // diagnostics: per-item cycle split of the S&C kernel
       unsigned long long v[20];
       HIPCHK(hipMemcpyAsync(v, h->sc_prof.p, sizeof(v), hipMemcpyDeviceToHost, s));

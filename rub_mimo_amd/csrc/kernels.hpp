@@ -69,6 +69,7 @@ struct ScArgs {
   int no_skip;
   uint32_t diag;            // diagnostics (RMIMO_SC_DIAG bits 8/16: skip in-place resolve/finalize)
   uint32_t split_iters;     // sc_exact_kernel: one workgroup per (antenna, iteration) (else per antenna)
+  uint32_t *snap;           // sc_exact_kernel: copy of *hot_count (the items of this phase), or null
 };
 
 // S&C screen over antenna 0 (sc_screen_kernel): blocks of kScrB positions, kScrSpan positions
@@ -93,6 +94,9 @@ struct ScreenArgs {
   uint32_t *count;                         // listed chunks (= hot items)
   ScHot *hot;                              // [cap] one per listed chunk
   uint32_t cap;
+  // capture sample 0 is the framesync origin (batched path): the delay line is empty there,
+  // so every lagged sample of positions n < M/2 is zero and P[n] = 0 (framing.cc:598-637)
+  uint32_t empty_history;
 };
 // several small 32-bit-word fills in one launch (the per-batch resets of the S&C queues,
 // flags and trigger words: one kernel instead of one memset node each)

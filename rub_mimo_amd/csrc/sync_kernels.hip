@@ -1472,6 +1472,12 @@ __global__ __launch_bounds__(kScrT) __attribute__((amdgpu_waves_per_eu(6))) void
   for (int j = 2 * D + tid; j < NB; j += kScrT) {
     const int64_t n0 = h0 + (int64_t)j * B;
     if (n0 >= L) break;
+    // positions n < M/2 of a capture that starts at the framesync's origin: every lagged
+    // sample x[k - M/2] of P[n] is the empty delay line's zero, so P[n] = 0 and y[n] is 0 (or
+    // the oracle's 0/0, compared false) -- never above the threshold. (Block sums cannot show
+    // it for the first block, whose energy lower bound is zero, and every capture's chunk 0
+    // used to become an exact-pass item for that block alone.)
+    if (a.empty_history && n0 + B <= (int64_t)RL) continue;
     double pr = 0.0, pi = 0.0, apw = 0.0, rz = 0.0, azw = 0.0;
     for (int u = 1; u <= D; u++) {
       const float4 r = recs[j - u];
@@ -1550,8 +1556,12 @@ void sc_exact_kernel(ScArgs a) {
   __shared__ long long run_ws[2][kScT / 64];
   __shared__ long long flo[kMaxStreams];
   __shared__ unsigned long long s_min;
-  const uint32_t count = min(*a.hot_count, a.hot_cap);
+  const uint32_t count_raw = *a.hot_count;
+  const uint32_t count = min(count_raw, a.hot_cap);
   const uint32_t item0 = a.item_lo ? *a.item_lo : 0u;   // items of earlier screen phases: done
+  // the next screen phase appends after this phase's items: their count, for its exact launch
+  // (the kernel boundary orders this store before the next screen's appends)
+  if (a.snap && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) *a.snap = count_raw;
   // one (antenna, iteration) of an item per workgroup, iteration fastest: an item's passes are
   // dispatched together, ahead of the grid's empty tail. Each iteration starts from its own
   // window sums (history of M samples), so an item's iterations run side by side instead of
@@ -1660,10 +1670,12 @@ void sc_exact_kernel(ScArgs a) {
     atomicMax(&a.prof[25], t_item);
     atomicAdd(&a.prof[26], t_item);
   }
+  unsigned long long pq_ring = 0, pq_scan = 0, pq_walk = 0, pq_first = 0;
 #pragma unroll 1
   for (int it = it_lo; it <= it_hi; it++) {
     const int64_t ib = w0 + (int64_t)it * kScIt;
     const unsigned long long tq0 = a.prof ? (unsigned long long)wall_clock64() : 0ull;
+    const bool pf_used = pf;
     {
       const int sl0 = (M + it * kScIt) % RING + 2 * tid;
       if (pf) {
@@ -1774,10 +1786,12 @@ void sc_exact_kernel(ScArgs a) {
     }
     __syncthreads();
     const unsigned long long tq3 = a.prof ? (unsigned long long)wall_clock64() : 0ull;
-    if (a.prof && tid == 0) {
-      atomicAdd(&a.prof[16], tq1 - tq0);
-      atomicAdd(&a.prof[17], tq2 - tq1);
-      atomicAdd(&a.prof[18], tq3 - tq2);
+    if (a.prof) {   // per-pass sums, added once per pass (atomics here would time themselves)
+      pq_ring += tq1 - tq0;
+      pq_scan += tq2 - tq1;
+      pq_walk += tq3 - tq2;
+      if (it == it_lo) pq_first += tq1 - tq0;
+      if (tid == 0 && !pf_used) atomicAdd(&a.prof[24], 1ull);   // diagnostics: guarded ring fills
     }
     const int namb = (a.diag & 8) ? 0 : min(s_namb, kLocAmb);          // uniform
     const unsigned long long t_r0 = a.prof ? (unsigned long long)wall_clock64() : 0ull;
@@ -1844,7 +1858,13 @@ void sc_exact_kernel(ScArgs a) {
     hp->wbits[((int)s * kScIters + it) * kScT + tid] = (uint16_t)bits;
     __syncthreads();   // every lane's phase B reads of the ring precede the next block's writes
   }
-  if (a.prof && tid == 0) atomicAdd(&a.prof[22], (unsigned long long)wall_clock64() - t_setup - t_res);
+  if (a.prof && tid == 0) {
+    atomicAdd(&a.prof[22], (unsigned long long)wall_clock64() - t_setup - t_res);
+    atomicAdd(&a.prof[16], pq_ring);
+    atomicAdd(&a.prof[17], pq_scan);
+    atomicAdd(&a.prof[18], pq_walk);
+    atomicAdd(&a.prof[19], pq_first);
+  }
   }   // active
   // the item's last antenna pass: plateau rule over every antenna's words
   if (a.prof && tid == 0) {
