@@ -573,17 +573,26 @@ void search_ls_wave_kernel(SearchArgs a) {
     const int off = (int)(u * a.SL);
     const uint32_t ws = a.SL * slot;                  // window index of lag 0
     unsigned long long best = 0ull;
+    if (a.corr_trace) {                               // uniform: DEBUG_LOG trace only
+#pragma unroll
+      for (int e = 0; e < 16; e++) {
+        const int m = (B > 1) ? tid + T * (e / B) + 1024 * (e % B) : reg_index<10, 16>(lane, e);
+        corr_trace_put(a, f, r, slot, m - off, (v[e].x * v[e].x + v[e].y * v[e].y) * vs);
+      }
+    }
+    // first maximum over the thread's lags, branch-free (selects, no per-lag exec masks): a
+    // lag outside [0, SL) or with a zero metric scores key 0, as the strict '>' from 0 of
+    // framing.cc:718, 735 ignores it
+    const uint32_t sl = a.SL;
 #pragma unroll
     for (int e = 0; e < 16; e++) {
       const int m = (B > 1) ? tid + T * (e / B) + 1024 * (e % B) : reg_index<10, 16>(lane, e);
-      const int i = m - off;
+      const uint32_t i = (uint32_t)(m - off);         // wraps for m < off: out of range
       const float val = (v[e].x * v[e].x + v[e].y * v[e].y) * vs;
-      corr_trace_put(a, f, r, slot, i, val);
-      if (i >= 0 && i < (int)a.SL && val > 0.0f) {
-        const unsigned long long key = ((unsigned long long)__float_as_uint(val) << 32) |
-                                       (unsigned long long)(0xFFFFFFFFu - (ws + (uint32_t)i));
-        best = key > best ? key : best;
-      }
+      const uint32_t hi = (i < sl && val > 0.0f) ? __float_as_uint(val) : 0u;
+      const unsigned long long key = ((unsigned long long)hi << 32) |
+                                     (unsigned long long)(0xFFFFFFFFu - (ws + i));
+      best = (hi != 0u && key > best) ? key : best;
     }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
