@@ -738,6 +738,30 @@ __global__ __launch_bounds__(256) void evm_kernel(EvmArgs a) {
   if (tid == 0) __hip_atomic_store(a.counter + f, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// the same totals for the persistent / split decodes, whose records per frame are few (one
+// per workgroup segment x waves): one workgroup per frame sums them in a fixed strided order
+// and an LDS pass in fixed order, with no chunk partials, counters or second phase
+__global__ __launch_bounds__(256) void evm_frame_kernel(EvmArgs a) {
+  __shared__ double red[256];
+  const uint32_t f = blockIdx.x, tid = threadIdx.x;
+  const FrameInfo &I = a.info[f];
+  const uint32_t n_out = (I.status == 0) ? min(I.n_sym, a.max_out) : 0u;
+  const uint32_t per = a.N * 3, G = 256 / per;
+  const uint64_t n = (n_out == 0) ? 0u : (uint64_t)a.nrec[f] * a.parts;
+  const uint32_t g = tid / per, c = tid % per;
+  const double *src = a.evm_part + (uint64_t)f * a.rec_stride * a.parts * per;
+  double v = 0.0;
+  if (g < G)
+    for (uint64_t e = g; e < n; e += G) v += src[e * per + c];
+  red[tid] = v;
+  __syncthreads();
+  if (tid < per) {
+    double t = 0.0;
+    for (uint32_t q = 0; q < G; q++) t += red[q * per + tid];
+    a.evm_out[(uint64_t)f * per + tid] = t;
+  }
+}
+
 // ------------------------------------------------------------------------------------
 template <int LOG2M, int NA>
 static uint32_t decode_launch_na(const DecodeArgs &a, uint32_t nf, hipStream_t s) {
@@ -849,7 +873,10 @@ uint32_t launch_decode(const DecodeArgs &a, int log2M, uint32_t n_frames, hipStr
 }
 
 void launch_evm(const EvmArgs &a, uint32_t n_frames, hipStream_t s) {
-  hipLaunchKernelGGL(evm_kernel, dim3(n_frames, kEvmChunks), dim3(256), 0, s, a);
+  if (a.nrec && a.few)   // a few records per frame (the streaming decode's segments)
+    hipLaunchKernelGGL(evm_frame_kernel, dim3(n_frames), dim3(256), 0, s, a);
+  else
+    hipLaunchKernelGGL(evm_kernel, dim3(n_frames, kEvmChunks), dim3(256), 0, s, a);
 }
 
 }  // namespace mimo

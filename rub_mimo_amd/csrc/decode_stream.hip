@@ -52,7 +52,8 @@ namespace mimo {
 #else
 #define DSP(...)
 #endif
-// staging DMA issued by one wave per antenna row (0: spread over every wave, the round-3 form)
+// staging DMA issued by DS_ROW_DMA waves per antenna row (0: spread over every wave with the
+// per-chunk address arithmetic, the earlier round-3 form)
 #ifndef DS_ROW_DMA
 #define DS_ROW_DMA 1
 #endif
@@ -333,7 +334,9 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
   constexpr int LASTC = RS / SPC - (NBLK - 1) * 64;          // chunks in a row's last block
   static_assert(RS % SPC == 0 && LASTC >= 1 && LASTC <= 64 && 64 * SPC * SB == 1024,
                 "row DMA blocks of 1 KB");
-  static_assert(!DS_ROW_DMA || NA <= T / 64, "one wave per staged row");
+  // waves staging each antenna row (at most the waves there are per row)
+  constexpr int WPR = DS_ROW_DMA == 0 ? 0 : ((T / 64) / NA < DS_ROW_DMA ? (T / 64) / NA : DS_ROW_DMA);
+  static_assert(!DS_ROW_DMA || (WPR >= 1 && NA * WPR <= T / 64), "waves per staged row");
   constexpr int NREF = NA * M / 16;               // 16-byte chunks of the reference indices
   // store instructions per symbol: the wait at the top of a symbol leaves them in flight
   using WP = WavePlan<LOG2M, NA>;
@@ -484,16 +487,17 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
       // chunk). Only NA waves compute the row base and issue DMAs: the address arithmetic is
       // scalar, and 16 waves doing it at once kept the CU's one scalar unit busy ~2k cycles
       // per symbol while every VALU waited; the other waves start their sub-transforms
-      if (wv < (uint32_t)NA) {
-        const uint32_t g = wv;
+      if (wv < (uint32_t)(NA * WPR)) {                // WPR waves per row
+        const uint32_t g = wv / WPR, sub = wv % WPR;
         const int64_t ag = (e0 + (int64_t)g * a.stride) & ~(int64_t)(SPC - 1);
         const auto xa = sgpr_ptr(reinterpret_cast<const char *>(a.iq) + ag * SB);
         const uint32_t lane = (uint32_t)(opq(tid) & 63);
         const uint32_t dst0 = __builtin_amdgcn_readfirstlane(stg_base + g * RS * (uint32_t)SB);
 #pragma unroll
-        for (int b = 0; b < NBLK; b++) {
-          if (b + 1 < NBLK || lane < (uint32_t)LASTC)
-            dma16((uint32_t)b * 1024u + lane * 16u, xa, dst0 + (uint32_t)b * 1024u);
+        for (int j = 0; j < (NBLK + WPR - 1) / WPR; j++) {
+          const uint32_t b = sub + (uint32_t)j * WPR;             // uniform
+          if (b < (uint32_t)NBLK && (b + 1 < (uint32_t)NBLK || lane < (uint32_t)LASTC))
+            dma16(b * 1024u + lane * 16u, xa, dst0 + b * 1024u);
         }
       }
 #else
@@ -534,9 +538,8 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
     }
     if constexpr (REF == 1) {
       // (waves RW0 .. RW0 + NREF/64 - 1: with DS_ROW_DMA the waves after the row waves)
-      constexpr int RW0 = DS_ROW_DMA ? NA : 0;
-      static_assert(!DS_ROW_DMA || (NREF % 64 == 0 && RW0 + NREF / 64 <= T / 64),
-                    "reference DMA waves after the row waves");
+      constexpr int RW0 = (WPR && NA * WPR + NREF / 64 <= T / 64) ? NA * WPR : 0;
+      static_assert(NREF % 64 == 0 && RW0 + NREF / 64 <= T / 64, "reference DMA waves");
       const int tr = t0 - RW0 * 64;
       if (tr >= 0 && tr < NREF) {
         const uint32_t dst = __builtin_amdgcn_readfirstlane(rstg_base + (uint32_t)((wv - RW0) * 64) * 16u);

@@ -698,6 +698,7 @@ int run_decode(mimo_rx *h, const float2 *iq, uint64_t stride, uint32_t F, uint64
   ea.chunk_part = h->evm_chunk.p;
   ea.counter = h->evm_cnt.p;
   ea.nrec = per_frame ? h->nrec.p : nullptr;
+  ea.few = path == MIMO_DECODE_STREAM ? 1 : 0;   // per workgroup segment, not per chunk x range
   e = h->timer.begin(s);
   launch_evm(ea, F, s);
   h->timer.end(6, e, s);

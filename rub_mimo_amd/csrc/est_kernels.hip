@@ -480,14 +480,26 @@ void search_ls_wave_kernel(SearchArgs a) {
   const bool inb = abs0 >= 0 && abs0 + F <= L;
   v2f v[16], X[16];
   // segment loads in the block pass's order: v[i B + rr] = x[n_i + 1024 rr], n_i = tid + T i
+  // (a uniform branch: inside the capture plain loads off one base, else clamped indices)
+  if (inb) {
+    const auto xb = xs.row((uint64_t)abs0);
 #pragma unroll
-  for (int i = 0; i < NB; i++)
+    for (int i = 0; i < NB; i++)
 #pragma unroll
-    for (int rr = 0; rr < B; rr++) {
-      const int64_t n = abs0 + tid + T * i + 1024 * rr;
-      const float2 t = xs.at(inb ? n : (n < 0 ? 0 : (n >= L ? L - 1 : n)));
-      v[i * B + rr] = v2f{t.x, t.y};
-    }
+      for (int rr = 0; rr < B; rr++) {
+        const float2 t = xb.at(tid + T * i + 1024 * rr);
+        v[i * B + rr] = v2f{t.x, t.y};
+      }
+  } else {
+#pragma unroll
+    for (int i = 0; i < NB; i++)
+#pragma unroll
+      for (int rr = 0; rr < B; rr++) {
+        const int64_t n = abs0 + tid + T * i + 1024 * rr;
+        const float2 t = xs.at(n < 0 ? 0 : (n >= L ? L - 1 : n));
+        v[i * B + rr] = v2f{t.x, t.y};
+      }
+  }
   if (!inb) {
 #pragma unroll
     for (int i = 0; i < NB; i++)

@@ -309,6 +309,7 @@ struct EvmArgs {
   const double *evm_part;
   double *evm_out;                 // [F][N][3]
   double *chunk_part;              // [F][kEvmChunks][N][3]
+  int few;                         // nrec records are few per frame: one workgroup per frame
   uint32_t *counter;               // [F] chunks done, zero between launches (self-resetting)
   const uint32_t *nrec;            // [F] records per frame (streaming decode) or null: n_sym
   uint32_t rec_stride;             // records per frame in evm_part (DecodeArgs::rec_stride)
