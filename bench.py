@@ -138,8 +138,9 @@ def decode_kernel_name(M, N, args, path=None):
     lg = M.bit_length() - 1
     if path == 1:
         return "decode_stream_kernel<%d,%d>" % (lg, N)
-    if path == 2:
-        return "spectra_kernel<%d>|apply_split_kernel<8>" % lg
+    if path == 2:   # (the persistent spectra form for M >= 2048 and the 128-subcarrier apply)
+        return ("spectra_persist_kernel<%d>|apply_split2_kernel<8>" % lg if lg >= 11 else
+                "spectra_kernel<%d>|apply_split2_kernel<8>" % lg)
     stream_ok = (os.environ.get("RMIMO_DECODE_STREAM", "1") != "0" and args.detector != "siso"
                  and args.qam <= 256 and (N, lg) in ((4, 11), (4, 10), (2, 12), (2, 11), (2, 10)))
     if stream_ok:

@@ -5,7 +5,7 @@ R=$(cd "$(dirname "$0")/.." && pwd)
 tag=${1:-r02}
 export PMC_KERNEL="decode|search|ls_|sc_screen|sc_exact|weights|plateau|evm|fill"
 "$R/tools/pmc_all.sh" "${tag}_c3" || exit 1
-export PMC_KERNEL="decode|search|ls_|weights"
+export PMC_KERNEL="decode|spectra|apply_split|search|ls_|weights"
 "$R/tools/pmc_run.sh" "${tag}_c4_sqa" "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU" --workload c4 || exit 1
 "$R/tools/pmc_run.sh" "${tag}_c4_fetch" "FETCH_SIZE" --workload c4 || exit 1
 "$R/tools/pmc_run.sh" "${tag}_c4_write" "WRITE_SIZE" --workload c4 || exit 1
