@@ -645,6 +645,48 @@ def test_two_phase_screen_finds_late_frames():
     assert synced >= 2 and late >= 1
 
 
+def test_captures_starting_at_the_frame_origin():
+    """The S&C screen proves positions n < M/2 of a batch capture outright (every lagged sample
+    of P[n] precedes the capture, i.e. the framesync's empty delay line: P = 0, y = 0 or 0/0).
+    Captures cut so that the frame's S0 begins at or just after sample 0, or preceded by M
+    exact zeros (0/0 windows), sync exactly as the oracle does on the same samples."""
+    M, cp, N, nac, pid, qam = 1024, 76, 2, 4, 40, 16
+    SL = M + cp
+    S = Synthesizer(SynthParams(M=M, cp_len=cp, num_streams=N, num_access_codes=nac, pid=pid,
+                                qam_order=qam, seed=23, snr_db=25.0))
+    L0 = S.frame_len(0)
+    out = _lib.DeviceBuffer(N * L0 * 8)
+    S.generate(out, L0, L0, 1)
+    full = out.download(np.complex64, N * L0).reshape(N, L0)
+    o = ref.FrameSyncRef(M, cp, N, nac, pid_max=pid, detector=_lib.DET_ZF2)
+    assert o.execute(full) == ref.STATE_MIMO
+    s0 = min(o.get_plateau_start(s) for s in range(N)) - M   # about where S0's body begins
+    caps = []
+    for cut in (s0 - cp, s0, s0 + M // 4):                   # S0 at / just before sample 0
+        caps.append(np.ascontiguousarray(full[:, max(cut, 0):]))
+    caps.append(np.concatenate([np.zeros((N, M), np.complex64), caps[0]], axis=1))
+    L = max(c.shape[1] for c in caps)
+    F = len(caps)
+    host = np.zeros((F, N, L), np.complex64)
+    for f, c in enumerate(caps):
+        host[f, :, :c.shape[1]] = c
+    buf = _lib.DeviceBuffer(host.nbytes)
+    buf.upload(host)
+    rxo = Receiver(RxParams(M=M, cp_len=cp, num_streams=N, num_access_codes=nac, pid_max=pid,
+                            detector=_lib.DET_ZF2, qam_order=qam))
+    rxo.process(buf, L, L, F, max_out=pid)
+    res = rxo.results(F)
+    for f in range(F):
+        of = ref.FrameSyncRef(M, cp, N, nac, pid_max=pid, detector=_lib.DET_ZF2)
+        st = of.execute(host[f])
+        r = res[f]
+        assert (r["status"] == _lib.FRAME_OK) == (st == ref.STATE_MIMO), f
+        if st == ref.STATE_MIMO:
+            assert r["sync_index"] == of.get_sync_index(), (f, r["sync_index"], of.get_sync_index())
+            assert r["plateau_start"][:N] == [of.get_plateau_start(s) for s in range(N)], f
+            assert r["num_samples_processed"] == of.get_num_samples_processed(), f
+
+
 def test_c4_full_codes_against_parseval_oracle():
     """C4 with all 20 access codes per stream (160 codes, 8 rx) on a reduced PID. The oracle
     runs its Parseval search variant (search_mode 1: one overlap-save correlation per (rx,
