@@ -596,8 +596,14 @@ void search_ls_wave_kernel(SearchArgs a) {
     // lag outside [0, SL) or with a zero metric scores key 0, as the strict '>' from 0 of
     // framing.cc:718, 735 ignores it
     const uint32_t sl = a.SL;
+    // (B > 1: the thread's lags m lie in 1024-blocks p = e mod B; only the blocks that meet
+    // [off, off + SL) -- three of B at C3 -- can score, so the others are skipped on a uniform
+    // test instead of being masked lane by lane)
+    const int p_lo = off / 1024, p_hi = (off + (int)sl - 1) / 1024;
 #pragma unroll
     for (int e = 0; e < 16; e++) {
+      if constexpr (B > 1)
+        if (e % B < p_lo || e % B > p_hi) continue;   // uniform
       const int m = (B > 1) ? tid + T * (e / B) + 1024 * (e % B) : reg_index<10, 16>(lane, e);
       const uint32_t i = (uint32_t)(m - off);         // wraps for m < off: out of range
       const float val = (v[e].x * v[e].x + v[e].y * v[e].y) * vs;
