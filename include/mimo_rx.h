@@ -72,13 +72,19 @@ typedef struct mimo_rx_config {
   double plateau_threshold;   /* PLATEAU_THREASHOLD (config.h:87), 0.95 */
   uint32_t qam_order;         /* square Gray QAM for the fused demap/EVM stage (4..256) */
   int32_t cfo_correct;        /* batched path, opt-in (absent from the reference: FIXME at
-                                 framing.cc:486): 1 = estimate each synced frame's CFO from the
-                                 S0 half-period correlation ending at its trigger, summed over
-                                 the antennas, and derotate its window (into a device scratch
-                                 copy; the caller's capture is not modified) before search, LS
-                                 and decode. 0 = off (the reference's behaviour). Batches
-                                 with frames_per_capture > 1 are refused with
-                                 MIMO_ERR_UNSUPPORTED. */
+                                 framing.cc:486): 1 = estimate each synced frame's CFO (eps0
+                                 from the S0 half-period correlation ending at its trigger,
+                                 delta from the data symbols' cyclic prefixes, both summed
+                                 over the antennas) and derotate before search, LS and decode
+                                 (in the loads where the fused search and the streaming
+                                 decode run, else into a device scratch copy; the caller's
+                                 capture is not modified); where the streaming decode takes
+                                 the batch with reference indices from HBM, each symbol's
+                                 common phase is also measured from its own decisions and
+                                 removed (mimo_rx_get_cfo_mode). The stages are restated in
+                                 oracle/mimo_ref.c (cfo_mode). 0 = off (the reference's
+                                 behaviour). Scratch-path batches with frames_per_capture > 1
+                                 are refused with MIMO_ERR_UNSUPPORTED. */
 } mimo_rx_config;
 
 typedef struct mimo_rx mimo_rx;
@@ -204,6 +210,10 @@ int mimo_rx_get_sc_exact_count(mimo_rx *h, uint64_t *out);
 enum { MIMO_DECODE_NONE = 0, MIMO_DECODE_STREAM = 1, MIMO_DECODE_SPLIT = 2,
        MIMO_DECODE_SYMBOL = 3 };
 int mimo_rx_get_decode_path(const mimo_rx *h, int32_t *path);
+/* the CFO stages the last batch ran (diagnostic, no sync): 0 off, 1 estimate and derotation,
+ * 2 the same plus the per-symbol common phase (the streaming decode's CPE variant) -- the
+ * oracle's cfo_mode for the same batch */
+int mimo_rx_get_cfo_mode(const mimo_rx *h, int32_t *mode);
 /* streaming execute: the device capture's capacity and the samples it holds per antenna
  * (diagnostic). While seeking, only the samples a later trigger can still reach are kept
  * (the reference's bounded window ring, framing.cc:387-388), so the capture stays near the

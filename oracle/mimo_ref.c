@@ -560,8 +560,11 @@ struct ref_framesync {
   uint64_t win_head;
   uint64_t *plateau_start, *plateau_end;
   int *in_plateau;
-  uint64_t sync_index, nsp;
+  uint64_t sync_index, nsp, trigger;
   int state;
+  /* opt-in CFO (cfo_mode): estimates, and the decode's derotation of the current symbol */
+  double cfo_eps0, cfo_delta, cfo_nu;
+  uint64_t cfo_body;
   /* channel */
   ref_cf32 *G, *W; /* [M][N][N] */
   float *gain;     /* [M_occ] */
@@ -715,6 +718,7 @@ static void execute_sc_sync(ref_framesync *fs, const ref_cf32 *x) { /* framing.c
   fs->nz_pos = (fs->nz_pos + 1) % fs->M;
   if (fs->cfg.trace_sc) trace_push(fs, y);
   if (proceed) {
+    fs->trigger = fs->nsp;
     for (uint32_t s = 0; s < fs->N; s++) fs->sync_index += fs->plateau_start[s];
     fs->sync_index /= fs->N;
     fs->state = REF_STATE_SAVE_ACCESS_CODES;
@@ -731,12 +735,99 @@ static void emit_symbol(ref_framesync *fs, const ref_cf32 *X /* [N][M_occ] */) {
   fs->n_out++;
 }
 
+/* ====================================================================================
+ * Opt-in CFO -- a BUILD EXTENSION, not the reference: framing.cc:486 leaves the frequency
+ * offset as a FIXME and never derotates. This restates the CFO stages of rub_mimo_amd's
+ * batched receive (cfo_kernels.hip, the derotating loads of est_kernels.hip,
+ * ls_combine_q_kernel, decode_stream.hip) so that path has an oracle. On the window buf
+ * (index j = absolute sample - base, base = sync_index - SL), every sum in fp64:
+ *  1. eps0 = arg(sum_r sum_{n<M/2} conj(x[t0+n]) x[t0+n+M/2]) / pi, t0 = trigger - M + 1: the S&C
+ *     window that ends at the trigger lies in the M/2-periodic S0 on every antenna;
+ *  2. search and LS read x1[j] = x[j] exp(-j 2 pi eps0 j / M);
+ *  3. delta = arg(P1) / (2 pi), P1 = exp(-j 2 pi eps0) sum over the data symbols s < PID+2,
+ *     antennas and prefix interiors (n in [4, cp-4)) of conj(x[k]) x[k+M], k = i0 + s SL + n,
+ *     k + M inside the window (i0 = corr[N-1][last] + M, framing.cc:857);
+ *  4. each access code's LS terms X/S1 turned by exp(-j 2 pi delta (c + M/2) / M), c its window;
+ *  5. the decode reads x[j] exp(-j 2 pi (eps0 + delta) j / M);
+ *  6. cfo_mode 2: per symbol, c = sum conj(Q(y)) y over the outputs y of every stream at even
+ *     occupied index j (Q the hard decision's point), and every output of the symbol turned
+ *     by conj(c) / |c|. (Every stream: each stream's output carries its own static phase error
+ *     from its column of G, and one stream's would turn the others by it.)
+ * ==================================================================================== */
+static ref_cf32 cfo_turn(ref_cf32 v, double nu, uint64_t j) {
+  double ph = -2.0 * nu * (double)j; /* units of pi */
+  ph -= 2.0 * rint(ph * 0.5);
+  float c = (float)cos(M_PI * ph), s = (float)sin(M_PI * ph);
+  ref_cf32 r;
+  r.re = v.re * c - v.im * s;
+  r.im = v.re * s + v.im * c;
+  return r;
+}
+
+static void cfo_common_phase(const ref_framesync *fs, ref_cf32 *out /* [N][M_occ] */) {
+  double cr = 0.0, ci = 0.0;
+  for (size_t i = 0; i < (size_t)fs->N * fs->M_occ; i++) { /* every stream, even j */
+    if ((i % fs->M_occ) & 1) continue;
+    ref_cf32 y = out[i];
+    ref_cf32 p = ref_qam_point(ref_qam_demap(y, fs->cfg.qam), fs->cfg.qam);
+    cr += (double)p.re * y.re + (double)p.im * y.im; /* conj(p) y */
+    ci += (double)p.re * y.im - (double)p.im * y.re;
+  }
+  double m = sqrt(cr * cr + ci * ci);
+  if (m == 0.0) return;
+  ref_cf32 u = {(float)(cr / m), (float)(-ci / m)};
+  for (size_t i = 0; i < (size_t)fs->N * fs->M_occ; i++) out[i] = cmul(out[i], u);
+}
+
+/* stage 1 on the window: eps0, and x1 = buf derotated by it (stages 1-2) */
+static double cfo_stage1(const ref_framesync *fs, const ref_cf32 *buf, ref_cf32 *x1) {
+  const uint32_t M = fs->M, N = fs->N;
+  const uint64_t base = fs->nsp - fs->win_len;
+  const int64_t t0 = (int64_t)(fs->trigger - base) - (int64_t)M + 1;
+  double re = 0.0, im = 0.0;
+  for (uint32_t r = 0; r < N; r++)
+    for (uint32_t n = 0; n < M / 2; n++) {
+      int64_t k = t0 + (int64_t)n;
+      if (k < 0 || (uint64_t)(k + M / 2) >= fs->win_len) continue;
+      ref_cf32 u = buf[(size_t)r * fs->win_len + k], v = buf[(size_t)r * fs->win_len + k + M / 2];
+      re += (double)u.re * v.re + (double)u.im * v.im;
+      im += (double)u.re * v.im - (double)u.im * v.re;
+    }
+  double eps0 = (re == 0.0 && im == 0.0) ? 0.0 : atan2(im, re) / M_PI;
+  for (uint32_t r = 0; r < N; r++)
+    for (uint64_t j = 0; j < fs->win_len; j++)
+      x1[(size_t)r * fs->win_len + j] = cfo_turn(buf[(size_t)r * fs->win_len + j], eps0 / M, j);
+  return eps0;
+}
+
+/* stage 3 (after the search): delta from the data prefixes of the raw window */
+static double cfo_stage3(const ref_framesync *fs, const ref_cf32 *buf, uint64_t i0, double eps0) {
+  const uint32_t M = fs->M, N = fs->N, cp = fs->cp, SL = fs->SL, margin = 4;
+  const uint32_t inner = cp > 2 * margin ? cp - 2 * margin : 0;
+  double re = 0.0, im = 0.0;
+  for (uint32_t s = 0; s < fs->cfg.pid_max + 2; s++)
+    for (uint32_t r = 0; r < N; r++)
+      for (uint32_t n = 0; n < inner; n++) {
+        uint64_t k = i0 + (uint64_t)s * SL + margin + n;
+        if (k + M >= fs->win_len) continue;
+        ref_cf32 u = buf[(size_t)r * fs->win_len + k], v = buf[(size_t)r * fs->win_len + k + M];
+        re += (double)u.re * v.re + (double)u.im * v.im;
+        im += (double)u.re * v.im - (double)u.im * v.re;
+      }
+  const double c = cos(-2.0 * M_PI * eps0), sn = sin(-2.0 * M_PI * eps0);
+  const double r2 = re * c - im * sn, i2 = re * sn + im * c;
+  return (r2 == 0.0 && i2 == 0.0) ? 0.0 : atan2(i2, r2) / (2.0 * M_PI);
+}
+
 /* framing.cc:535-589 (MIMO) and 508-533 (SISO) */
 static void decode_symbol(ref_framesync *fs, ref_cf32 *X /* scratch [N][M] */,
                           ref_cf32 *out /* [N][M_occ] */) {
   uint32_t M = fs->M, N = fs->N, cp = fs->cp;
   for (uint32_t r = 0; r < N; r++) {
     memcpy(X + (size_t)r * M, fs->sym + (size_t)r * fs->SL + cp, sizeof(ref_cf32) * M);
+    if (fs->cfg.cfo_mode) /* opt-in CFO: the body at window index cfo_body derotated by eps */
+      for (uint32_t n = 0; n < M; n++)
+        X[(size_t)r * M + n] = cfo_turn(X[(size_t)r * M + n], fs->cfo_nu, fs->cfo_body + n);
     if (fs->cfg.detector == REF_DET_SISO && r != fs->cfg.siso_rx) continue;
     ref_fft(X + (size_t)r * M, M, 0);
     for (uint32_t k = 0; k < M; k++) {
@@ -770,6 +861,7 @@ static void decode_symbol(ref_framesync *fs, ref_cf32 *X /* scratch [N][M] */,
       out[(size_t)t * fs->M_occ + j].re *= fs->gain[j];
       out[(size_t)t * fs->M_occ + j].im *= fs->gain[j];
     }
+  if (fs->cfg.cfo_mode == 2) cfo_common_phase(fs, out);
 }
 
 /* complex double Gauss-Jordan with partial pivoting: solve A X = B, A n x n, B n x n */
@@ -907,6 +999,13 @@ static void estimate_channel(ref_framesync *fs) { /* framing.cc:653-886 */
       buf[(size_t)s * fs->win_len + j] =
           fs->win[(size_t)s * fs->win_len + (fs->win_head + j) % fs->win_len];
   ref_cf32 *X = (ref_cf32 *)malloc(sizeof(ref_cf32) * (size_t)N * M);
+  /* opt-in CFO stage 1: search and LS read the window derotated by eps0 */
+  ref_cf32 *raw = buf;
+  fs->cfo_eps0 = fs->cfo_delta = fs->cfo_nu = 0.0;
+  if (fs->cfg.cfo_mode) {
+    buf = (ref_cf32 *)malloc(sizeof(ref_cf32) * (size_t)N * fs->win_len);
+    fs->cfo_eps0 = cfo_stage1(fs, raw, buf);
+  }
   for (uint32_t i = 0; i < (size_t)N * nacN; i++) { fs->corr_max[i] = 0.0f; fs->corr_idx[i] = 0; }
   for (uint32_t s = 0; s < N; s++) { fs->s0_max[s] = 0.0f; fs->s0_idx[s] = 0; }
   double t0 = wall_now();
@@ -950,6 +1049,11 @@ static void estimate_channel(ref_framesync *fs) { /* framing.cc:653-886 */
   if (!fs->cfg.keep_identity_bias)
     for (size_t i = 0; i < (size_t)M * N * N; i++) { fs->G[i].re = 0.0f; fs->G[i].im = 0.0f; }
   double *sv = (double *)calloc((size_t)M * N * N * 3, sizeof(double));
+  if (fs->cfg.cfo_mode) { /* opt-in CFO stage 3: the residual from the data prefixes */
+    const uint64_t i0 = (uint64_t)fs->corr_idx[(N - 1) * nacN + nacN - 1] + M;
+    fs->cfo_delta = cfo_stage3(fs, raw, i0, fs->cfo_eps0);
+    fs->cfo_nu = (fs->cfo_eps0 + fs->cfo_delta) / (double)M;
+  }
   for (uint32_t code = 0; code < nac; code++)
     for (uint32_t r = 0; r < N; r++)
       for (uint32_t tx = 0; tx < N; tx++) {
@@ -958,9 +1062,22 @@ static void estimate_channel(ref_framesync *fs) { /* framing.cc:653-886 */
                sizeof(ref_cf32) * M);
         ref_fft(X, M, 0);
         const ref_cf32 *S = fs->S1 + (size_t)tx * nac * M + (size_t)code * M;
+        /* opt-in CFO stage 4: the code's terms turned by delta at its window centre */
+        double rc = 1.0, rs = 0.0;
+        if (fs->cfg.cfo_mode) {
+          double ph = -2.0 * (fs->cfo_delta / (double)M) *
+                      ((double)fs->corr_idx[r * nacN + ac] + 0.5 * (double)M);
+          ph -= 2.0 * rint(ph * 0.5);
+          rc = cos(M_PI * ph);
+          rs = sin(M_PI * ph);
+        }
         for (uint32_t k = 0; k < M; k++) {
           if (!is_occ(fs, k)) continue;
           ref_cf32 q = cdiv(X[k], S[k]);
+          if (fs->cfg.cfo_mode) {
+            ref_cf32 q2 = {(float)(q.re * rc - q.im * rs), (float)(q.re * rs + q.im * rc)};
+            q = q2;
+          }
           size_t gi = ((size_t)k * N + r) * N + tx;
           fs->G[gi] = cadd(fs->G[gi], q);
           sv[gi * 3 + 0] += q.re;
@@ -1005,7 +1122,12 @@ static void estimate_channel(ref_framesync *fs) { /* framing.cc:653-886 */
     j++;
   }
   double t2 = wall_now();
-  /* replay decode of the window, framing.cc:853-868 */
+  /* replay decode of the window, framing.cc:853-868 (opt-in CFO: the raw window, each body
+   * derotated by eps0 + delta in decode_symbol) */
+  if (fs->cfg.cfo_mode) {
+    free(buf);
+    buf = raw;
+  }
   ref_cf32 *out = (ref_cf32 *)malloc(sizeof(ref_cf32) * (size_t)N * (fs->M_occ ? fs->M_occ : 1));
   fs->sym_count = 0;
   for (uint64_t i = (uint64_t)fs->corr_idx[(N - 1) * nacN + nacN - 1] + M; i < fs->win_len; i++) {
@@ -1013,6 +1135,7 @@ static void estimate_channel(ref_framesync *fs) { /* framing.cc:653-886 */
       fs->sym[(size_t)s * SL + fs->sym_count] = buf[(size_t)s * fs->win_len + i];
     fs->sym_count++;
     if (fs->sym_count < SL) continue;
+    fs->cfo_body = i + 1 - SL + fs->cp; /* window index of the body's first sample */
     decode_symbol(fs, X, out);
     emit_symbol(fs, out);
     fs->sym_count = 0;
@@ -1061,6 +1184,11 @@ void ref_framesync_get_phase_times(const ref_framesync *fs, double *t4) {
 
 void ref_framesync_reset(ref_framesync *fs) { fs->state = REF_STATE_SEEK_PLATEAU; }
 
+void ref_framesync_get_cfo(const ref_framesync *fs, double *eps2) {
+  eps2[0] = fs->cfo_eps0;
+  eps2[1] = fs->cfo_delta;
+}
+
 /* CPU-baseline helper (not a reference entry point): put a fresh framesync in the state the
  * plateau rule leaves it in when it fires at sample `trigger` with `sync_index`
  * (framing.cc:617-623): the window ring holds samples up to `trigger` (zeros before 0), the
@@ -1077,6 +1205,7 @@ int ref_framesync_skip_to_sync(ref_framesync *fs, const ref_cf32 *const *in, uin
     win_push(fs, x);
   }
   fs->nsp = trigger + 1;
+  fs->trigger = trigger;
   fs->sync_index = sync_index;
   fs->state = REF_STATE_SAVE_ACCESS_CODES;
   return 0;

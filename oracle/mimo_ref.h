@@ -119,6 +119,12 @@ typedef struct {
                                  1: Parseval variant (CPU-baseline mode 3 of BASELINE.md, labelled):
                                  one overlap-save FFT correlation per (rx, code); same metric up
                                  to fp32 rounding */
+  int      cfo_mode;          /* build extension, not in the reference (framing.cc:486 FIXME):
+                                 0 off (the reference); 1 the CFO stages of rub_mimo_amd's
+                                 batched path (S0 coarse, prefix fine, derotated search, LS
+                                 and decode); 2 the same plus the per-symbol common phase.
+                                 See "Opt-in CFO" in mimo_ref.c */
+  uint32_t qam;               /* QAM order of the hard decision (cfo_mode 2 only) */
 } ref_rx_cfg;
 
 typedef struct ref_framesync ref_framesync;
@@ -151,6 +157,9 @@ uint32_t ref_framesync_M_occ(const ref_framesync *fs);
 /* wall seconds spent per phase since create: [0] S&C + plateau, [1] access-code search,
  * [2] LS + weights, [3] replay decode (FFT, detect, gain) */
 void     ref_framesync_get_phase_times(const ref_framesync *fs, double *t4);
+/* cfo_mode != 0: the estimates of the last estimate_channel in subcarrier spacings: [0] eps0
+ * (S0 coarse), [1] delta (prefix fine); the frame's offset is eps0 + delta */
+void     ref_framesync_get_cfo(const ref_framesync *fs, double *eps2);
 /* search metric traces by lag i in [0,SL): corr [N][N*nac][SL], s0 [N][SL] */
 int      ref_framesync_get_corr_trace(const ref_framesync *fs, float *corr, float *s0);
 

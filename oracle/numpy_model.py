@@ -10,6 +10,8 @@ evidence that both follow the reference logic:
   framing.cc:702-744  access-code search (first maximum, strict >, initial 0)
   framing.cc:801-831  LS estimate with identity start, 2x2 invert
   framing.cc:535-589  replay decode from corr_indices[N-1][last] + M
+and, with cfo=True, the opt-in CFO stages (a build extension: the reference has no CFO step,
+framing.cc:486) as oracle/mimo_ref.c restates them ("Opt-in CFO"), here in float64 numpy.
 """
 from __future__ import annotations
 
@@ -95,9 +97,24 @@ def plateau_trigger(ys, cp, thr=0.95):
     return n, st, sum(st) // N
 
 
+def qam_decision_point(y, order):
+    """Square QAM hard decision (as mimo_ref.c ref_qam_demap): each dimension's level
+    floor((v sqrt(2(L^2-1)/3) + L) / 2) clamped to [0, L-1], point (2m - (L-1)) / that scale."""
+    L = int(round(np.sqrt(order)))
+    s = np.sqrt(2.0 * (L * L - 1) / 3.0)
+
+    def lev(v):
+        return np.clip(np.floor((v * s + L) * 0.5), 0, L - 1)
+    return ((2 * lev(y.real) - (L - 1)) + 1j * (2 * lev(y.imag) - (L - 1))) / s
+
+
 def receive(rx, M, cp, N, nac, pid_max, s0_bits, s1_bits, p=None, detector="zf2",
-            noise_var=None, keep_identity_bias=True, thr=0.95):
-    """Full frame receive. Returns a dict, or None if no sync / incomplete capture."""
+            noise_var=None, keep_identity_bias=True, thr=0.95, cfo=False, qam=None):
+    """Full frame receive. Returns a dict, or None if no sync / incomplete capture.
+    cfo=True: the opt-in CFO stages (eps0 from the S&C window at the trigger, search and LS on
+    the window turned by eps0, delta from the data prefixes, LS terms turned by delta at their
+    window centres, decode of the window turned by eps0 + delta) and, with qam, the per-symbol
+    common phase from the decisions of every stream at even occupied index."""
     if p is None:
         p = np.full(M, 2, np.uint8)
     SL = M + cp
@@ -124,6 +141,15 @@ def receive(rx, M, cp, N, nac, pid_max, s0_bits, s1_bits, p=None, detector="zf2"
     win = np.zeros((N, win_len), np.complex128)
     lo = max(0, base)
     win[:, lo - base:] = rx[:, lo:base + win_len]
+    raw = win
+    eps0 = delta = 0.0
+    jj = np.arange(win_len)
+    if cfo:
+        t0 = n_trig - base - M + 1
+        a = win[:, t0:t0 + M // 2]
+        b = win[:, t0 + M // 2:t0 + M]
+        eps0 = float(np.angle(np.sum(np.conj(a) * b)) / np.pi)
+        win = raw * np.exp(-2j * np.pi * eps0 * jj / M)[None, :]
     nacN = nac * N
     corr_idx = np.zeros((N, nacN), np.int64)
     s0_idx = np.zeros(N, np.int64)
@@ -145,6 +171,15 @@ def receive(rx, M, cp, N, nac, pid_max, s0_bits, s1_bits, p=None, detector="zf2"
     if keep_identity_bias:
         for r in range(N):
             G[occ, r, r] = 1.0
+    if cfo:
+        i0 = corr_idx[N - 1, nacN - 1] + M
+        ks = []
+        for s in range(pid_max + 2):
+            k = i0 + s * SL + 4 + np.arange(max(cp - 8, 0))
+            ks.append(k[k + M < win_len])
+        k = np.concatenate(ks)
+        P1 = np.sum(np.conj(raw[:, k]) * raw[:, k + M]) * np.exp(-2j * np.pi * eps0)
+        delta = float(np.angle(P1) / (2 * np.pi))
     per_code = np.zeros((nac, M, N, N), np.complex128)
     for code in range(nac):
         for r in range(N):
@@ -152,6 +187,8 @@ def receive(rx, M, cp, N, nac, pid_max, s0_bits, s1_bits, p=None, detector="zf2"
                 i0 = corr_idx[r, code * N + t]
                 X = np.fft.fft(win[r, i0:i0 + M])
                 per_code[code, occ, r, t] = X[occ] / S1[t][code][occ]
+                if cfo:
+                    per_code[code, occ, r, t] *= np.exp(-2j * np.pi * delta * (i0 + M / 2) / M)
     G[occ] += per_code[:, occ].sum(axis=0)
     G[occ] *= dn / nac
     v = per_code[:, occ]
@@ -176,12 +213,20 @@ def receive(rx, M, cp, N, nac, pid_max, s0_bits, s1_bits, p=None, detector="zf2"
     i0 = corr_idx[N - 1, nacN - 1] + M
     nsym = (win_len - i0) // SL
     syms = np.zeros((nsym, N, mocc), np.complex128)
+    if cfo:
+        win = raw * np.exp(-2j * np.pi * (eps0 + delta) * jj / M)[None, :]
     for s in range(nsym):
         st = i0 + s * SL + cp
         X = np.fft.fft(win[:, st:st + M], axis=1) * dn
         Y = np.einsum("ktr,rk->tk", W[occ], X[:, occ])
         syms[s] = Y * gain[None, :]
+        if cfo and qam:
+            ev = syms[s][:, 0::2]          # every stream, even occupied index
+            c = np.sum(np.conj(qam_decision_point(ev, qam)) * ev)
+            if c != 0:
+                syms[s] *= np.conj(c) / abs(c)
     return dict(trigger=n_trig, plateau_start=starts, plateau_end=[n_trig] * N,
+                cfo_eps0=eps0, cfo_delta=delta,
                 sync_index=sync, base=base, corr_idx=corr_idx, s0_idx=s0_idx, G=G, W=W,
                 gain=gain, noise_var=nv_est, symbols=syms, y=ys,
                 num_samples_processed=n_e + 2 if n_e + 1 < rx.shape[1] else n_e + 1)

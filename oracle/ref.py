@@ -71,6 +71,7 @@ def lib():
             "ref_framesync_M_occ": (C.c_uint32, [vp]),
             "ref_framesync_get_corr_trace": (C.c_int, [vp, f32p, f32p]),
             "ref_framesync_get_phase_times": (None, [vp, f64p]),
+            "ref_framesync_get_cfo": (None, [vp, f64p]),
             "ref_framesync_skip_to_sync": (C.c_int, [vp, vp, C.c_uint64, C.c_uint64]),
             "ref_sc_metric_at": (C.c_float, [vp, C.c_uint64, C.c_uint32]),
             "ref_demap_evm": (None, [vp, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32,
@@ -100,7 +101,8 @@ class _RxCfg(C.Structure):
                 ("pid_max", C.c_uint32), ("detector", C.c_int), ("noise_var", C.c_float),
                 ("keep_identity_bias", C.c_int), ("siso_tx", C.c_uint32),
                 ("siso_rx", C.c_uint32), ("threshold", C.c_double), ("trace_sc", C.c_int),
-                ("trace_corr", C.c_int), ("search_mode", C.c_int)]
+                ("trace_corr", C.c_int), ("search_mode", C.c_int), ("cfo_mode", C.c_int),
+                ("qam", C.c_uint32)]
 
 
 def _u8(a):
@@ -235,9 +237,13 @@ class FrameSyncRef:
 
     def __init__(self, M, cp, N, nac, pid_max=1000, detector=DET_ZF2, noise_var=-1.0,
                  keep_identity_bias=True, siso_tx=0, siso_rx=0, threshold=0.95,
-                 trace_sc=False, trace_corr=False, p=None, s1_polys=None, search_mode=0):
+                 trace_sc=False, trace_corr=False, p=None, s1_polys=None, search_mode=0,
+                 cfo_mode=0, qam=0):
         """search_mode 0: the reference's brute-force search (framing.cc:702-744); 1: the
-        Parseval overlap-save variant (a CPU-baseline mode, labelled as such where used)."""
+        Parseval overlap-save variant (a CPU-baseline mode, labelled as such where used).
+        cfo_mode (a build extension; the reference has no CFO step, framing.cc:486): 1 the CFO
+        stages of the GPU's batched path, 2 the same plus the per-symbol common phase (needs
+        qam, the order of the hard decision); see mimo_ref.c "Opt-in CFO"."""
         from oracle.codes import s1_polynomials
         self.M, self.cp, self.N, self.nac, self.pid_max = M, cp, N, nac, pid_max
         self.p = default_sctype(M) if p is None else np.ascontiguousarray(p, np.uint8)
@@ -246,7 +252,8 @@ class FrameSyncRef:
         s0b, s1b = code_bits(M, N, nac, s1_polys)
         cfg = _RxCfg(M, cp, N, nac, pid_max, detector, noise_var,
                      1 if keep_identity_bias else 0, siso_tx, siso_rx, threshold,
-                     1 if trace_sc else 0, 1 if trace_corr else 0, int(search_mode))
+                     1 if trace_sc else 0, 1 if trace_corr else 0, int(search_mode),
+                     int(cfo_mode), int(qam))
         self._h = lib().ref_framesync_create(C.byref(cfg), _u8(self.p), _u8(s0b), _u8(s1b))
         if not self._h:
             raise ValueError("ref_framesync_create failed")
@@ -276,6 +283,12 @@ class FrameSyncRef:
         if lib().ref_framesync_skip_to_sync(self._h, ptrs, int(trigger), int(sync_index)) != 0:
             raise RuntimeError("skip_to_sync needs a fresh framesync")
         return self.execute([r[int(trigger) + 1:] for r in rx])
+
+    def cfo(self):
+        """(eps0, delta) of the last estimate (cfo_mode != 0), subcarrier spacings."""
+        e = np.zeros(2)
+        lib().ref_framesync_get_cfo(self._h, e.ctypes.data_as(C.POINTER(C.c_double)))
+        return float(e[0]), float(e[1])
 
     def phase_times(self):
         """Wall seconds per phase: S&C+plateau, search, LS+weights, replay decode."""
@@ -424,3 +437,21 @@ def stream_ref_file(path, M, cp, N, nac, pid_max, max_frames, detector, max_syms
                 _, num, den, err = demap_evm(r["symbols"], qam, np.asarray(tx[j][:, :max_syms]))
                 r.update(tx_frame=j, evm_num=num, evm_den=den, errors=err)
     return recs
+
+
+def frame_ref_file(path, M, cp, N, nac, pid_max, detector, qam=0, cfo_mode=0, search_mode=1,
+                   max_syms=None):
+    """One framesync over a capture saved with numpy.save ([N][L] complex64; worker entry for
+    parallel checks): the records of the frame (state, sync index, the CFO estimates, corr
+    indices, symbols cut to max_syms). search_mode 1 is the Parseval search (labelled CPU
+    mode; the brute force gives the same indices up to fp32 ties)."""
+    rx = np.load(path, mmap_mode="r")
+    fs = FrameSyncRef(M, cp, N, nac, pid_max=pid_max, detector=detector, qam=qam,
+                      cfo_mode=cfo_mode, search_mode=search_mode)
+    st = fs.execute([np.asarray(r) for r in rx])
+    out = dict(state=st, sync_index=fs.get_sync_index())
+    if st == STATE_MIMO:
+        syms = fs.symbols()
+        out.update(cfo=fs.cfo(), corr_idx=fs.get_corr()[0],
+                   symbols=syms if max_syms is None else syms[:max_syms])
+    return out

@@ -93,6 +93,7 @@ SIGNATURES = {
     "mimo_rx_get_stage_times": (C.c_int, [_vp, _P(C.c_double), _P(_u32)]),
     "mimo_rx_get_sc_exact_count": (C.c_int, [_vp, _P(_u64)]),
     "mimo_rx_get_decode_path": (C.c_int, [_vp, _P(_i32)]),
+    "mimo_rx_get_cfo_mode": (C.c_int, [_vp, _P(_i32)]),
     "mimo_rx_get_stream_capacity": (C.c_int, [_vp, _P(_u64), _P(_u64)]),
     "mimo_rx_set_debug_log": (C.c_int, [_vp, C.c_char_p]),
     "mimo_tx_create": (C.c_int, [_u32, _u32, _u32, _u32, _vp, _vp, _vp, _P(_vp)]),

@@ -124,6 +124,9 @@ __global__ __launch_bounds__(kCfoThreads) void cfo_batch_est_kernel(CfoBatchArgs
     // one memory latency per symbol and antenna)
     const uint32_t inner = a.cp > 2 * kCfoMargin ? a.cp - 2 * kCfoMargin : 0;
     const int64_t d0 = I.base + cfo_i0(a, f);               // data symbol 0's prefix
+    // (the reads stay inside the framesync's window, as the reference's ring holds it: the
+    // capture may hold more, the window does not)
+    const int64_t wend = std::min<int64_t>(L, I.base + (int64_t)a.win);
     const uint32_t nsym = a.n_data > b ? (a.n_data - b + kCfoBlocks - 1) / kCfoBlocks : 0u;
     const uint32_t runs = nsym * a.N;
     const float2 *cap = src + (uint64_t)I.cap * a.N * a.stride;
@@ -138,7 +141,7 @@ __global__ __launch_bounds__(kCfoThreads) void cfo_batch_est_kernel(CfoBatchArgs
           const uint32_t p = p0 + (uint32_t)e;          // uniform: run (symbol, antenna)
           const uint32_t js = p / a.N, r = p % a.N;
           const int64_t k = d0 + (int64_t)(b + js * kCfoBlocks) * a.SL + kCfoMargin + n;
-          ok[e] = p < runs && n < inner && k >= 0 && k + a.M < L;
+          ok[e] = p < runs && n < inner && k >= 0 && k + a.M < wend;
           const float2 *row = cap + (uint64_t)(p < runs ? r : 0u) * a.stride;
           const int64_t kk = ok[e] ? k : 0;
           u[e] = row[kk];
@@ -192,7 +195,10 @@ __global__ __launch_bounds__(kCfoThreads) void cfo_batch_rot_kernel(CfoBatchArgs
   if (STAGE == 1 ? !cfo_live(I) : I.status != 0) return;
   const double eps = cfo_stage_eps(a.part, blockIdx.z, STAGE);
   const double eps0 = STAGE == 2 ? cfo_stage_eps(a.part, blockIdx.z, 1) : 0.0;
-  if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) I.cfo_eps = (float)(eps + eps0);
+  if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) {
+    I.cfo_eps = (float)(eps + eps0);
+    I.cfo_E = cfo_fixed_freq(eps + eps0, a.M);
+  }
   const double nu = eps / (double)a.M;
   const uint64_t off = ((uint64_t)I.cap * a.N + blockIdx.y) * a.stride;
   const bool whole = STAGE == 1 || a.rot_window;

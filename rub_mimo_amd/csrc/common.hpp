@@ -175,6 +175,13 @@ struct FrameInfo {
   uint32_t ref;            // reference frame (ref_mode 1 index row, ref_mode 2 frame id - id0)
   float cfo_eps;           // opt-in CFO estimate (subcarrier spacings), 0 when off
   uint32_t pad_;
+  int64_t cfo_E;           // the same as nu = eps / M cycles per sample in 64-bit fixed point
+                           // (nu 2^64; the decode's per-symbol phasors, cfo_fixed_freq)
 };
+// the 64-bit fixed-point frequency of an offset of eps subcarrier spacings (|eps| < 2): the
+// phase of sample j in turns is the wrapped product E j / 2^64, exact for every j
+MIMO_DEV int64_t cfo_fixed_freq(double eps, uint32_t M) {
+  return (int64_t)rint(ldexp(eps / (double)M, 64));
+}
 
 }  // namespace mimo

@@ -309,17 +309,22 @@ constexpr bool stream_wave_fft() {
   return LOG2M >= 11 && stream_dyn_lds<LOG2M, NA>(true, REF, SC16) + kStreamStaticLds <= 163840;
 }
 
-// CPE (opt-in CFO path): decision-directed common-phase tracking. The residual frequency
-// offset left by the CFO estimate turns every symbol by a slowly growing angle; each symbol's
-// equalised outputs are rotated by the current estimate before the decision, and the sum of
-// conj(decided point) x rotated output over a group of kCpeEvery symbols (all streams, one
-// subcarrier slot per thread, reduced through LDS at the next symbol's top barrier) corrects
-// the estimate for the following symbols of the same frame. Off (CPE = false) the kernel is
-// unchanged.
-#ifndef MIMO_CPE_EVERY
-#define MIMO_CPE_EVERY 8
-#endif
-constexpr uint32_t kCpeEvery = MIMO_CPE_EVERY;   // CPE: symbols per common-phase update
+// CPE (opt-in CFO path): per-symbol common phase, decision directed and non-recursive. The
+// residual frequency offset left by the CFO estimate turns every symbol by a slowly growing
+// angle. Each symbol measures its own: c = sum over stream 0's outputs y of conj(Q(y)) y
+// (Q the hard decision's constellation point), reduced over the workgroup in a fixed order,
+// and every output of the symbol is turned by conj(c)/|c| before its decision, EVM and
+// stores. Nothing carries from one symbol to the next, so a symbol's outputs are a function
+// of the frame alone, not of where a workgroup's range starts (oracle/mimo_ref.c restates it,
+// cfo_mode 2). Off (CPE = false) the kernel is unchanged.
+// the constellation point of the hard decision of y (levels as qam_level_pair_pk; the point
+// as qam_point: (2m - (L-1)) * scale in fp32)
+MIMO_DEV v2f qam_dec_point_pk(v2f y, v2f inv_scale, v2f Lf, uint32_t Lm1, float scale) {
+#pragma clang fp contract(off)
+  const v2f t = (y * inv_scale + Lf) * 0.5f;
+  const uint32_t mI = min(cvt_u32_sat(t.x), Lm1), mQ = min(cvt_u32_sat(t.y), Lm1);
+  return v2f{(float)(int32_t)(2 * mI - Lm1) * scale, (float)(int32_t)(2 * mQ - Lm1) * scale};
+}
 template <int LOG2M, int NA, int REF, int OUTS, bool SC16 = false, bool CPE = false>
 __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(DecodeArgs a) {
   using PL = StreamPlan<LOG2M, NA>;
@@ -608,29 +613,29 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
     }
   };
 
-  v2f rot = v2f{1.0f, 0.0f};                          // CPE: current phase correction
-  bool cpe_valid = false;                             // cpe_part holds this frame's last K symbols
-  v2f cpe_acc = v2f{0.0f, 0.0f};                      // this thread's residual-phase sum
-  uint32_t cpe_k = 0;                                 // symbols of this frame segment so far
   // folded CFO (a.cpe == 2): the frame's estimate nu = (eps0 + delta) / M cycles per sample
-  // about its window base, split into the part inside a symbol body (time domain, before the
-  // transform: sample j of the body turns by exp(-j 2 pi nu j), the thread's j = t0 % W8 + r W8)
-  // and the body start's phase (a constant per symbol, applied to the outputs with the CPE
-  // rotation) -- the derotation the scratch passes of the unfolded path applied
-  // (the body start's phasor rides in rot: set at each frame segment's first symbol, advanced
-  // by cfo_e per symbol, corrected by the CPE as before)
+  // about its window base (fp64, from the stage partials), split into the part inside a symbol
+  // body (time domain, before the transform: sample j of the body turns by exp(-j 2 pi nu j),
+  // the thread's j = t0 % W8 + r W8) and the body start's phasor rot = exp(-j 2 pi nu j_s),
+  // j_s = i0 + cp + s SL, computed for every symbol from the frame's 64-bit fixed-point
+  // frequency (E = nu 2^64: the phase in turns is the wrapped product E j_s / 2^64, exact for
+  // any j_s) -- the derotation the scratch passes of the unfolded path applied, with nothing
+  // carried from symbol to symbol
   // (the thread's in-body phasor exp(-j2pi nu t0%W8) comes from an LDS table of the frame,
   // cfo_tab[n] = exp(-j2pi nu n) for n < CTN, times a wave-uniform exp(-j2pi nu CTN hi) when
   // W8 > CTN)
   v2f cfo_hi = v2f{1.0f, 0.0f};
   v2f cfo_w = v2f{1.0f, 0.0f};                              // exp(-j2pi nu W8)
-  v2f cfo_e = v2f{1.0f, 0.0f};                              // exp(-j2pi nu SL)
-  auto cfo_frame = [&](uint32_t ff, uint32_t ss) {
+  uint64_t cfo_E = 0;                                       // nu 2^64 (two's complement)
+  uint64_t cfo_j0 = 0;                                      // i0 + cp: symbol 0's body
+  auto cfo_frame = [&](uint32_t ff) {
     if constexpr (CPE) {
       if (a.cpe == 2) {
-        // (eps0 + delta, written by ls_combine_q_kernel; phases reduced in fp64, then fp32)
+        // (eps0 + delta as ls_combine_q_kernel left it: the fixed-point frequency, exact in
+        // fp64 as nu = E 2^-64)
         const FrameInfo &J = a.info[ff];
-        const double nu = (double)J.cfo_eps / (double)M;
+        const int64_t e64 = J.cfo_E;
+        const double nu = ldexp((double)e64, -64);
         auto ph = [](double cyc) {
           double p = -2.0 * cyc;
           p -= 2.0 * rint(p * 0.5);
@@ -643,13 +648,21 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
         for (int e = tid; e < CTN; e += T) cfo_tab[e] = ph(nu * (double)e);
         if constexpr (W8 > CTN) cfo_hi = uni(ph(nu * (double)((opq(tid) % W8) / CTN * CTN)));
         cfo_w = uni(ph(nu * (double)W8));
-        cfo_e = uni(ph(nu * (double)a.SL));
-        rot = uni(ph(nu * (double)((int64_t)J.i0 + a.cp + (int64_t)ss * a.SL)));
+        cfo_E = rfl64((uint64_t)e64);
+        cfo_j0 = rfl64((uint64_t)J.i0 + a.cp);
       }
     }
   };
+  // the body start's phasor of symbol ss of the current frame
+  auto cfo_rot = [&](uint32_t ss) -> v2f {
+    const uint64_t P = cfo_E * (cfo_j0 + (uint64_t)ss * a.SL);   // turns x 2^64, wrapped
+    const float turns = (float)(int32_t)(uint32_t)(P >> 32) * 0x1p-32f;   // [-1/2, 1/2)
+    float sn, cs;
+    sincospif(-2.0f * turns, &sn, &cs);
+    return uni(v2f{cs, sn});
+  };
   load_w(f);
-  cfo_frame(f, s);
+  cfo_frame(f);
   FrameBase fbase = frame_base(f);
   uint32_t odd = fetch(fbase, s);
   // the first symbol's staging (issued after the weight loads: the counted wait in the loop
@@ -664,20 +677,6 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
     asm volatile("s_waitcnt vmcnt(%0)" :: "n"(NSTORE) : "memory");
     __syncthreads();
     DSP(const unsigned long long ds_1 = __builtin_amdgcn_s_memtime(); ds_t[1] += ds_1 - ds_0;)
-    if constexpr (CPE) {
-      if (cpe_valid) {   // the previous kCpeEvery symbols' residual phase: rot *= conj(c) / |c|
-        cpe_valid = false;
-        v2f c = v2f{0.0f, 0.0f};
-#pragma unroll
-        for (int w = 0; w < T / 64; w++) c += cpe_part[w];
-        const float m2 = c.x * c.x + c.y * c.y;
-        if (m2 > 0.0f) {
-          const float inv = 1.0f / sqrtf(m2);
-          const v2f u = v2f{c.x * inv, -c.y * inv};
-          rot = uni(v2f{rot.x * u.x - rot.y * u.y, rot.x * u.y + rot.y * u.x});
-        }
-      }
-    }
     v2f v[8];
     {
       const int t0 = opq(tid);
@@ -717,20 +716,16 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
       }
     }
     if constexpr (CPE) {
-      // the symbol's phase correction, applied to its time samples (a constant rotation of
-      // the body turns every output by it, and costs one multiply per sample instead of one
-      // per output); folded CFO: times the in-body part of the derotation
+      // folded CFO: the symbol's derotation on its time samples (the body start's phasor
+      // times the in-body part)
       if (a.cpe == 2) {
-        v2f c = cmul_pk(cfo_tab[(opq(tid) % W8) % CTN], rot);
+        v2f c = cmul_pk(cfo_tab[(opq(tid) % W8) % CTN], cfo_rot(s));
         if constexpr (W8 > CTN) c = cmul_pk(c, cfo_hi);
 #pragma unroll
         for (int r = 0; r < 8; r++) {
           v[r] = cmul_pk(v[r], c);
           c = cmul_pk(c, cfo_w);
         }
-      } else {
-#pragma unroll
-        for (int r = 0; r < 8; r++) v[r] = cmul_pk(v[r], rot);
       }
     }
     MARK(";@@B pass0");
@@ -805,19 +800,19 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
     const uint64_t frame_id = a.frame_id0 + (fcr[f] >> 16);
     // output row (f, t, s) = ob0 + t * max_out * M_occ: uniform, one 64-bit product per symbol
     const uint64_t ob0 = rfl64((((uint64_t)f * NA) * a.max_out + s) * a.M_occ);
-    // one output (stream t, slot q, subcarrier k): apply, demap, EVM terms; returns the decision
-    auto one_out = [&](int t, int q, uint32_t k, const v2f *X, v2f &acc) -> uint32_t {
-      acc = v2f{0.0f, 0.0f};
+    // one output's apply (stream t, slot q): y = sum_r W[t][r][q] gain dn X_r
+    auto apply1 = [&](int t, int q, const v2f *X) -> v2f {
+      v2f acc = v2f{0.0f, 0.0f};
 #pragma unroll
       for (int r = 0; r < NA; r++) acc = cmac_pk(acc, Wr[t][r][q], X[r]);
+      return acc;
+    };
+    // demap and EVM terms of output acc (stream t, slot q, subcarrier k); returns the decision
+    auto finish = [&](int t, int q, uint32_t k, v2f acc) -> uint32_t {
 #ifdef DS_ABL_NODEMAP   // timing ablation: no demap / EVM
       return 0u;
 #endif
       const uint32_t d = gidx[qam_level_pair_pk(acc, inv_sc, Lf, Lm1, a.qam.L)];
-      // (the residual phase from the thread's first subcarrier of every stream: a quarter of the
-      // symbol's outputs at 4x4 measure it to far below the drift it tracks)
-      if constexpr (CPE)
-        if (q == 0) cpe_acc = cmac_pk(cpe_acc, v2f{ptab[d].x, -ptab[d].y}, acc);
       uint32_t refi;
       if constexpr (REF == 1) refi = (cref[(t * S + q) / 4] >> (8 * ((t * S + q) % 4))) & 0xFFu;
       else if constexpr (REF == 2)
@@ -832,6 +827,45 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
       e_den[t] = __builtin_fmaf(sp.x, sp.x, __builtin_fmaf(sp.y, sp.y, e_den[t]));
       return d;
     };
+    // CPE: the symbol's common phase c = sum conj(Q(y)) y over every stream's outputs at even
+    // subcarriers (per thread in stream-then-slot order, per wave by the xor tree, the waves
+    // in order), then every output of the symbol turned by conj(c) / |c|. (Every stream: each
+    // carries its own static phase error from its column of G, which one stream's estimate
+    // would impose on the others.)
+    auto cpe_turn = [&](v2f (&y)[NA][S]) {
+      v2f c = v2f{0.0f, 0.0f};
+      // KADJ: k = S tid + q, even for q = 0; else k = tid + q T (T even), even on even threads
+      const bool even_thread = KADJ || ((opq(tid) & 1) == 0);
+      if (even_thread) {
+#pragma unroll
+        for (int t = 0; t < NA; t++)
+#pragma unroll
+          for (int q = 0; q < (KADJ ? 1 : S); q++) {
+            const v2f pt = qam_dec_point_pk(y[t][q], inv_sc, Lf, Lm1, a.qam.scale);
+            c = cmac_pk(c, v2f{pt.x, -pt.y}, y[t][q]);
+          }
+      }
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) {
+        c.x += __shfl_xor(c.x, off);
+        c.y += __shfl_xor(c.y, off);
+      }
+      if ((tid & 63) == 0) cpe_part[wv] = c;
+      __syncthreads();
+      c = cpe_part[0];
+#pragma unroll
+      for (int w = 1; w < T / 64; w++) c += cpe_part[w];
+      const float m2 = c.x * c.x + c.y * c.y;
+      if (m2 > 0.0f) {
+        const float inv = 1.0f / sqrtf(m2);
+        const v2f u = v2f{c.x * inv, -c.y * inv};
+#pragma unroll
+        for (int t = 0; t < NA; t++)
+#pragma unroll
+          for (int q = 0; q < S; q++) y[t][q] = cmul_pk(y[t][q], u);
+      }
+    };
+    v2f yc[CPE ? NA : 1][CPE ? S : 1];                // CPE: the symbol's outputs, turned
     if constexpr (KADJ) {
       // the thread's S adjacent subcarriers k = S tid + q: every antenna's X of both, then per
       // stream both outputs and one 16-byte symbol store and one 2-byte index store (per stream
@@ -844,6 +878,13 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
 #pragma unroll
         for (int r = 0; r < NA; r++) X[q][r] = xp[r * GS];
       }
+      if constexpr (CPE) {
+#pragma unroll
+        for (int t = 0; t < NA; t++)
+#pragma unroll
+          for (int q = 0; q < S; q++) yc[t][q] = apply1(t, q, X[q]);
+        cpe_turn(yc);
+      }
 #pragma unroll
       for (int t = 0; t < NA; t++) {
         const uint64_t ob = ob0 + (uint64_t)t * rowstep;
@@ -851,8 +892,15 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
         const auto oidx = sgpr_ptr(a.out_idx + ob);
         const uint32_t kb = (uint32_t)opq(tid) * S;
         v2f y0, y1;
-        const uint32_t d0 = one_out(t, 0, kb, X[0], y0);
-        const uint32_t d1 = one_out(t, 1, kb + 1, X[1], y1);
+        if constexpr (CPE) {
+          y0 = yc[t][0];
+          y1 = yc[t][1];
+        } else {
+          y0 = apply1(t, 0, X[0]);
+          y1 = apply1(t, 1, X[1]);
+        }
+        const uint32_t d0 = finish(t, 0, kb, y0);
+        const uint32_t d1 = finish(t, 1, kb + 1, y1);
 #ifndef DS_ABL_NOSTORE   // timing ablation: no symbol / index stores
         if constexpr (OUTS & 1)
           *(gptr<v4f>)((gptr<char>)osym + kb * (uint32_t)sizeof(v2f)) = v4f{y0.x, y0.y, y1.x, y1.y};
@@ -860,10 +908,7 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
 #endif
       }
     } else {
-#pragma unroll
-      for (int q = 0; q < S; q++) {
-        const uint32_t k = (uint32_t)opq(tid) + q * T;
-        v2f X[NA];
+      auto load_x = [&](int q, v2f *X) {
         if constexpr (WF) {
           const uint32_t kk = (uint32_t)opq(tid) + q * T;
           const v2f *xp = img + (kk & 7u) * QS + padk<WP::PADK>((int)(kk >> 3));
@@ -874,6 +919,22 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
 #pragma unroll
           for (int r = 0; r < NA; r++) X[r] = xp[r * PB];
         }
+      };
+      if constexpr (CPE) {
+#pragma unroll
+        for (int q = 0; q < S; q++) {
+          v2f X[NA];
+          load_x(q, X);
+#pragma unroll
+          for (int t = 0; t < NA; t++) yc[t][q] = apply1(t, q, X);
+        }
+        cpe_turn(yc);
+      }
+#pragma unroll
+      for (int q = 0; q < S; q++) {
+        const uint32_t k = (uint32_t)opq(tid) + q * T;
+        v2f X[NA];
+        if constexpr (!CPE) load_x(q, X);
 #pragma unroll
         for (int t = 0; t < NA; t++) {
           // uniform row bases (SGPRs): the stores take a 32-bit per-lane offset
@@ -881,7 +942,9 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
           const auto osym = sgpr_ptr(reinterpret_cast<v2f *>(a.out_sym + ob));
           const auto oidx = sgpr_ptr(a.out_idx + ob);
           v2f acc;
-          const uint32_t d = one_out(t, q, k, X, acc);
+          if constexpr (CPE) acc = yc[t][q];
+          else acc = apply1(t, q, X);
+          const uint32_t d = finish(t, q, k, acc);
 #ifndef DS_ABL_NOSTORE   // timing ablation: no symbol / index stores
           if constexpr (OUTS & 1)
             *(gptr<v2f>)((gptr<char>)osym + k * (uint32_t)sizeof(v2f)) = acc;
@@ -891,40 +954,15 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
       }
     }
 
-    if constexpr (CPE) {
-      // the residual phase sum, per wave, read after the next barrier: after each of a frame
-      // segment's first four symbols (a range that starts mid-frame opens with the estimate's
-      // accumulated error), then once per kCpeEvery symbols (the error then moves ~1e-4 rad
-      // per symbol; one reduction per group saves the shuffles, the LDS round and the update)
-      cpe_k++;
-      if (cpe_k <= 4 || cpe_k % kCpeEvery == 0) {    // uniform
-#pragma unroll
-        for (int off = 32; off > 0; off >>= 1) {
-          cpe_acc.x += __shfl_xor(cpe_acc.x, off);
-          cpe_acc.y += __shfl_xor(cpe_acc.y, off);
-        }
-        if ((tid & 63) == 0) cpe_part[wv] = cpe_acc;
-        cpe_acc = v2f{0.0f, 0.0f};
-        cpe_valid = true;
-      }
-    }
     MARK(";@@F tail");
     DSP(ds_c = __builtin_amdgcn_s_memtime(); ds_t[3] += ds_c - ds_3; ds_t[0]++;)
     const bool last = (i + 1 == i_end);
-    if constexpr (CPE)
-      if (a.cpe == 2) rot = uni(cmul_pk(rot, cfo_e));   // the next symbol's body start
     if (last || fn != f) {
-      if constexpr (CPE) {
-        rot = v2f{1.0f, 0.0f};
-        cpe_valid = false;
-        cpe_acc = v2f{0.0f, 0.0f};
-        cpe_k = 0;
-      }
       flush(f);
       if (!last) {
         n_out_f = n_out_n;
         load_w(fn);
-        cfo_frame(fn, sn);
+        cfo_frame(fn);
       }
     }
     MARK(";@@G next");
@@ -1441,6 +1479,11 @@ static size_t stream_lds_bytes(int ref_mode, bool sc16) {
   return stream_dyn_lds<LOG2M, NA>(wf, ref_mode, sc16);
 }
 
+bool decode_stream_cpe(const DecodeArgs &a) {
+  const bool outs = (a.out_sym != nullptr) == (a.out_idx != nullptr);   // both or neither
+  return a.cpe && !a.sc16 && a.ref_mode == 1 && outs;
+}
+
 template <int LOG2M, int NA>
 static uint32_t stream_launch(const DecodeArgs &a, hipStream_t s) {
   using PL = StreamPlan<LOG2M, NA>;
@@ -1448,7 +1491,7 @@ static uint32_t stream_launch(const DecodeArgs &a, hipStream_t s) {
   auto pick_out = [&](auto ref) -> void (*)(DecodeArgs) {
     constexpr int R = decltype(ref)::value;
     const int outs = (a.out_sym ? 1 : 0) | (a.out_idx ? 2 : 0);
-    if (a.cpe && !a.sc16 && R == 1 && (outs == 3 || outs == 0)) {   // opt-in CFO path
+    if (R == 1 && decode_stream_cpe(a)) {   // opt-in CFO path
       if constexpr (R == 1)
         return outs == 3 ? decode_stream_kernel<LOG2M, NA, 1, 3, false, true>
                          : decode_stream_kernel<LOG2M, NA, 1, 0, false, true>;

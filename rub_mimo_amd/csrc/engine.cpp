@@ -246,10 +246,12 @@ struct mimo_rx {
   DevBuf<unsigned long long> sc_prof;   // RMIMO_SC_PROF=1 cycle counters
   uint32_t last_frames = 0, last_max_out = 0;
   int last_decode_path = MIMO_DECODE_NONE;   // kernel family of the last decode launch
+  int last_cfo_mode = 0;                     // CFO stages of the last batch (get_cfo_mode)
   // streaming state (facade). The device capture holds samples [origin, origin + total) of
   // the stream since construction/reset (positions inside it are capture-relative).
   DevBuf<float2> capbuf;
   uint64_t cap_len = 0, total = 0, origin = 0;
+  uint64_t trim_clo = ~0ull;   // the S&C chunk position of the last trim probe (maybe_trim)
   DevBuf<uint32_t> probe;               // trim probe: per antenna, a proven metric zero
   // DEBUG_LOG files of the streaming execute (framing.cc:390-402, 598-600, 675-696, 873-883)
   std::string dbg_dir;
@@ -662,7 +664,9 @@ int run_decode(mimo_rx *h, const float2 *iq, uint64_t stride, uint32_t F, uint64
   d.cfo_part = cfo_fold_part;
   static const bool no_split = [] { const char *e = getenv("RMIMO_DECODE_SPLIT"); return e && e[0] == '0'; }();
   d.rec_stride = max_out;
-  if (!no_split && decode_split_accepts(d, h->log2M)) {
+  // (the split records' stride only where the split kernels can run: RMIMO_DEC_EXPT forces
+  // the per-symbol kernels, whose records are max_out apart)
+  if (!no_split && d.expt == 0 && decode_split_accepts(d, h->log2M)) {
     // [F][M/64][group][N][64] complex64 spectra of the 8x8 split decode (one symbol group)
     if (h->spec.ensure((size_t)F * split_group_symbols(max_out) * h->N * h->M) != hipSuccess)
       return fail(MIMO_ERR_NOMEM, "split decode scratch");
@@ -679,6 +683,7 @@ int run_decode(mimo_rx *h, const float2 *iq, uint64_t stride, uint32_t F, uint64
   const uint32_t parts = launch_decode(d, h->log2M, F, s, &per_frame, &path);
   h->timer.end(5, e, s);
   h->last_decode_path = path;
+  h->last_cfo_mode = !h->cfo ? 0 : (path == MIMO_DECODE_STREAM && decode_stream_cpe(d) ? 2 : 1);
   if (!parts)   // run_batch widens every sc16 batch the streaming decode does not take
     return fail(MIMO_ERR_UNSUPPORTED, "no decode kernel takes this configuration");
   if (dprof) {   // diagnostics: per-item cycle split of the decode kernel
@@ -1006,7 +1011,9 @@ __global__ void trim_probe_kernel(const float2 *x, uint64_t stride, uint32_t M, 
     const double R = 0.5 * z;
     // the fp64 metric clears the threshold by more than the fp32 error band: the oracle's y
     // is not above the threshold either
-    zero = R > 0.0 && pr * pr + pi * pi < (thr - band) * R * R;
+    // an all-zero window (R = 0, so P = 0: an idle radio or zero padding) is the oracle's 0/0,
+    // which compares false: not above the threshold either
+    zero = R == 0.0 || pr * pr + pi * pi < (thr - band) * R * R;
   }
   const unsigned long long b = __ballot(zero);
   if (lane == 0) ok[s] = b ? 1u : 0u;
@@ -1021,6 +1028,10 @@ static int maybe_trim(mimo_rx *h) {
   const uint64_t D = (c_lo * K - need) / K * K;
   const int64_t lo = (int64_t)(D + h->SL + h->M), hi = (int64_t)(c_lo * K - H);
   if (hi - lo < (int64_t)K / 2) return MIMO_OK;
+  // the probe's span moves only when the S&C reaches a new chunk: a caller feeding small pieces
+  // pays one probe (and its host round trip) per chunk of stream, not one per call
+  if (c_lo == h->trim_clo) return MIMO_OK;
+  h->trim_clo = c_lo;
   HIPCHK(h->probe.ensure(h->N));
   hipLaunchKernelGGL(trim_probe_kernel, dim3(h->N), dim3(64), 0, h->stream, h->capbuf.p,
                      h->cap_len, h->M, lo, hi, h->thr, sc_band(h->M), h->probe.p);
@@ -1176,6 +1187,7 @@ int mimo_rx_reset(mimo_rx *h) {
   h->state = MIMO_STATE_SEEK_PLATEAU;
   h->total = 0;
   h->origin = 0;
+  h->trim_clo = ~0ull;
   h->nsp = 0;
   h->have_sync = false;
   h->have_est = false;
@@ -1364,7 +1376,7 @@ static int run_batch(mimo_rx *h, const mimo_batch *b, hipStream_t s) {
     if (h->cfo_eps.ensure(cfo_batch_part_doubles(slots)) != hipSuccess)
       return fail(MIMO_ERR_NOMEM, "cfo estimate allocation failed");
     ca.iq = iq; ca.out = nullptr; ca.stride = b->stride; ca.frame_len = b->frame_len;
-    ca.len = h->win_len + 64; ca.N = h->N; ca.M = h->M; ca.cp = h->cp; ca.SL = h->SL;
+    ca.len = h->win_len + 64; ca.win = h->win_len; ca.N = h->N; ca.M = h->M; ca.cp = h->cp; ca.SL = h->SL;
     ca.n_codes = h->N * h->nac; ca.n_data = h->pid + 2; ca.info = h->info.p;
     ca.part = h->cfo_eps.p;
     ca.fold = 1;
@@ -1378,7 +1390,7 @@ static int run_batch(mimo_rx *h, const mimo_batch *b, hipStream_t s) {
         h->cfo_eps.ensure(cfo_batch_part_doubles(slots)) != hipSuccess)
       return fail(MIMO_ERR_NOMEM, "cfo scratch allocation failed");
     ca.iq = iq; ca.out = h->cfo_iq.p; ca.stride = b->stride; ca.frame_len = b->frame_len;
-    ca.len = h->win_len + 64; ca.N = h->N; ca.M = h->M; ca.cp = h->cp; ca.SL = h->SL;
+    ca.len = h->win_len + 64; ca.win = h->win_len; ca.N = h->N; ca.M = h->M; ca.cp = h->cp; ca.SL = h->SL;
     ca.n_codes = h->N * h->nac; ca.n_data = h->pid + 2; ca.info = h->info.p;
     ca.part = h->cfo_eps.p;
     launch_cfo_batch(ca, slots, 1, s);
@@ -1601,6 +1613,12 @@ int mimo_rx_get_stream_capacity(const mimo_rx *h, uint64_t *samples, uint64_t *h
 int mimo_rx_get_decode_path(const mimo_rx *h, int32_t *path) {
   if (!h || !path) return fail(MIMO_ERR_ARG, "null argument");
   *path = h->last_decode_path;
+  return MIMO_OK;
+}
+
+int mimo_rx_get_cfo_mode(const mimo_rx *h, int32_t *mode) {
+  if (!h || !mode) return fail(MIMO_ERR_ARG, "null argument");
+  *mode = h->last_cfo_mode;
   return MIMO_OK;
 }
 

@@ -727,7 +727,11 @@ __global__ __launch_bounds__(256) void ls_combine_q_kernel(LsArgs a) {
     if (threadIdx.x == 0) {
       s_nu = cfo_stage_eps(a.cfo_part, f, 2) / (double)M;
       if (blockIdx.x == 0 && rt == 0)   // the frame's total estimate (stage 1 + stage 2)
-        const_cast<FrameInfo &>(I).cfo_eps = (float)(cfo_stage_eps(a.cfo_part, f, 1) + s_nu * M);
+      {
+        const double eps = cfo_stage_eps(a.cfo_part, f, 1) + s_nu * M;
+        const_cast<FrameInfo &>(I).cfo_eps = (float)eps;
+        const_cast<FrameInfo &>(I).cfo_E = cfo_fixed_freq(eps, M);
+      }
     }
     __syncthreads();
     if (rot_tab) {

@@ -226,6 +226,7 @@ struct CfoBatchArgs {
   const float2 *iq;
   float2 *out;                     // scratch capture, same layout as iq
   uint64_t stride, frame_len, len; // len: window samples derotated from each frame's base
+  uint64_t win;                    // the framesync window (ACB + TX): stage 2 reads inside it
   uint32_t N, M, cp, SL;
   uint32_t n_codes;                // access-code symbols (N * nac) after S0
   uint32_t n_data;                 // data symbols in a window (PID + 2)
@@ -292,6 +293,9 @@ uint32_t launch_decode_stream(const DecodeArgs &a, int log2M, uint32_t n_frames,
 // true when launch_decode_stream takes this configuration (nrec aside): the sc16 wire input
 // is decoded only there
 bool decode_stream_accepts(const DecodeArgs &a, int log2M, uint32_t n_frames);
+// true when launch_decode_stream runs its CPE variant for these arguments (folded CFO
+// derotation and the per-symbol common phase)
+bool decode_stream_cpe(const DecodeArgs &a);
 // decode_stream.hip: 8x8 split form (spectra to a scratch, then a chunked apply, optionally
 // alternating over symbol groups); 0 when the configuration is not handled or a.spec is null.
 // The scratch holds split_group_symbols(max_out) symbols per frame.

@@ -185,7 +185,7 @@ class Receiver:
                 # slot decodes into scratch and is copied into place
                 osym = None if out_sym is None else _ptr(out_sym) + sl * slot_sym
                 oidx = None if out_idx is None else _ptr(out_idx) + sl * slot_idx
-                scratch = None
+                scratch = ref2 = None
                 if rem == 1 and ref_mode == 1 and rs is None and refp is not None:
                     # the scratch second slot reads reference row refp + 1, one past the last
                     # capture's rows: give it a two-row copy
@@ -204,6 +204,10 @@ class Receiver:
                              ref_idx=refp, ref_seed=ref_seed, frame_id0=fid0, stream=stream,
                              frames_per_capture=max(rem, 2), ref_starts=rs,
                              ref_stride=K if rs is not None else 0)
+                if ref2 is not None and scratch is None:
+                    # ref2 is read by the asynchronous decode on `stream`: keep it alive until
+                    # that work has finished, not just until it is rebound
+                    torch.cuda.synchronize()
                 if scratch is not None:
                     torch.cuda.synchronize()
                     if osym:
@@ -277,6 +281,13 @@ class Receiver:
         """Kernel family of the last decode launch (_lib.DECODE_STREAM / _SPLIT / _SYMBOL)."""
         v = C.c_int32()
         check(lib().mimo_rx_get_decode_path(self._h, C.byref(v)), "decode_path")
+        return v.value
+
+    def cfo_mode(self):
+        """CFO stages of the last batch: 0 off, 1 estimate + derotation, 2 plus the per-symbol
+        common phase (the oracle's cfo_mode for the same batch)."""
+        v = C.c_int32()
+        check(lib().mimo_rx_get_cfo_mode(self._h, C.byref(v)), "cfo_mode")
         return v.value
 
     def stage_times(self):

@@ -132,12 +132,15 @@ def test_batch_then_reset_then_chunked_execute_on_one_handle():
     assert evm_delta(np.stack(got), g["symbols"]) <= SYM_TOL
 
 
-def test_streaming_execute_memory_is_bounded_by_the_window():
-    """A live stream that stays unsynchronised for a long time: a noise lead of more than 20
+@pytest.mark.parametrize("lead_kind", ["noise", "zeros"])
+def test_streaming_execute_memory_is_bounded_by_the_window(lead_kind):
+    """A live stream that stays unsynchronised for a long time: a lead of more than 20
     reference windows (ACB + TX, framing.cc:387-388) before a frame, fed to the streaming
     execute in random chunks. The device capture stays within 2x the window (the reference
     holds one window ring; here only what a later trigger can reach is kept while seeking),
-    and sync, plateau, samples processed and symbols equal the oracle's on the whole stream."""
+    and sync, plateau, samples processed and symbols equal the oracle's on the whole stream.
+    The lead is noise, or exact zeros (an idle radio: every S&C window is the oracle's 0/0,
+    which compares false, so those positions are proven zeros too)."""
     M, cp, N, nac, pid, qam = 1024, 76, 2, 4, 40, 16
     SL = M + cp
     win = SL * (nac * N + 4) + pid * SL                   # ACB + TX
@@ -147,6 +150,8 @@ def test_streaming_execute_memory_is_bounded_by_the_window():
     lead_len = 21 * win
     nstd = np.sqrt(0.0625 * 10 ** (-25.0 / 10) / 2)
     lead = (rng.standard_normal((N, lead_len)) + 1j * rng.standard_normal((N, lead_len))) * nstd
+    if lead_kind == "zeros":
+        lead[:] = 0
     stream = np.concatenate([lead.astype(np.complex64), rx], axis=1)
     o = ref.FrameSyncRef(M, cp, N, nac, pid_max=pid, detector=_lib.DET_ZF2)
     assert o.execute(stream) == ref.STATE_MIMO
@@ -866,8 +871,8 @@ def test_cfo_batch_corrects_rotated_c3_frames(eps_true, mode):
     - against the unrotated frames with no correction at all (the reference's path) within
       0.5 dB for every frame: the estimator's own variance (prefix correlation, std ~3e-6
       subcarrier spacings at 30 dB) would cost the cleanest (-32 dB) frames ~2.4 dB of drift
-      over 1000 symbols; the decode's decision-directed common-phase tracking takes that to
-      ~0.3 dB (the first symbol of each decode workgroup's range is not yet tracked);
+      over 1000 symbols; the decode's per-symbol common phase (each symbol's own decisions,
+      cfo_mode 2) removes it;
     - without the correction the rotated frames collapse (> 10 dB worse).
     mode "fold" (reference indices from HBM): the search + LS loads and the streaming decode
     derotate in place; "scratch" (ref_mode 2): the estimate-and-derotate scratch passes."""
@@ -912,11 +917,106 @@ def test_cfo_batch_corrects_rotated_c3_frames(eps_true, mode):
         assert abs(corr[f]["cfo_eps"] - eps_true) < 2e-5, (f, corr[f]["cfo_eps"])
         assert abs(clean[f]["cfo_eps"]) < 2e-5, (f, clean[f]["cfo_eps"])
         assert abs(e1 - e3) <= 0.1, (f, e3, e1)
-        # (the scratch mode's ref_mode-2 decode has no common-phase tracking: the estimator's
-        # residual drift costs the cleanest frames ~2.4 dB there)
+        # (the scratch mode's ref_mode-2 decode has no per-symbol common phase: the
+        # estimator's residual drift costs the cleanest frames ~2.4 dB there)
         assert e3 - e0 <= (0.5 if mode == "fold" else 3.0), (f, e0, e3)
         print("cfo frame %d: plain %.3f dB, corrected %.3f dB, raw %.3f dB" % (f, e0, e3, e2))
         assert e2 > e0 + 10.0, (f, e0, e2)
+
+
+def _oracle_frames(tmp_path, caps, M, cp, N, nac, pid, qam, cfo_mode):
+    """oracle/mimo_ref.c framesync (cfo_mode) over each capture [N][L], in parallel processes"""
+    from concurrent.futures import ProcessPoolExecutor
+    import multiprocessing as mp
+    paths = []
+    for i, c in enumerate(caps):
+        pth = tmp_path / ("cap%d.npy" % i)
+        np.save(pth, c)
+        paths.append(str(pth))
+    with ProcessPoolExecutor(max_workers=min(8, len(paths)),
+                             mp_context=mp.get_context("spawn")) as ex:
+        futs = [ex.submit(ref.frame_ref_file, pth, M, cp, N, nac, pid, ref.DET_MMSE, qam,
+                          cfo_mode, 1, pid) for pth in paths]
+        return [f.result() for f in futs]
+
+
+@pytest.mark.timeout(600)
+def test_cfo_folded_matches_oracle_and_is_frame_deterministic(tmp_path):
+    """Opt-in CFO (a build extension: the reference's framing.cc:486 is a FIXME) on the folded
+    path (fused search + LS loads and the streaming decode derotate; per-symbol common phase),
+    against its restatement in oracle/mimo_ref.c (cfo_mode 2, cross-checked by the numpy model
+    in test_oracle.py): C3 frames rotated by eps = 0.3 and -0.62 subcarrier spacings give the
+    oracle's sync index, its estimate eps0 + delta to 1e-6, and its equalised symbols to EVM
+    delta 1e-4 (all 1000 data symbols). And the decode is a function of the frame: each frame
+    received alone gives bit-identical symbols and indices to the batch, whose persistent
+    workgroups' symbol ranges start mid-frame."""
+    import torch
+    from rub_mimo_amd.receiver import cfo_derotate
+    M, cp, N, nac, pid, qam, F = 2048, 152, 4, 20, 1000, 64, 4
+    sp = SynthParams(M=M, cp_len=cp, num_streams=N, num_access_codes=nac, pid=pid,
+                     qam_order=qam, seed=812, snr_db=30.0)
+    S = Synthesizer(sp)
+    L = sp.max_frame_len()
+    iq = torch.empty((F, N, L), dtype=torch.complex64, device="cuda")
+    tx = torch.empty((F, N, pid, M), dtype=torch.uint8, device="cuda")
+    S.generate(iq, L, L, F, tx_idx=tx)
+    P = RxParams(M=M, cp_len=cp, num_streams=N, num_access_codes=nac, pid_max=pid,
+                 detector=_lib.DET_MMSE, qam_order=qam, cfo_correct=True)
+    for eps in (0.3, -0.62):
+        rot = iq.clone()
+        cfo_derotate(rot, L, F * N, L, 0, -eps, M)              # a CFO of +eps
+        rxo = Receiver(P)
+        sym = torch.zeros((F, N, pid, M), dtype=torch.complex64, device="cuda")
+        idx = torch.zeros((F, N, pid, M), dtype=torch.uint8, device="cuda")
+        rxo.process(rot, L, L, F, max_out=pid, out_sym=sym, out_idx=idx, ref_mode=1, ref_idx=tx)
+        torch.cuda.synchronize()
+        assert rxo.decode_path() == DECODE_STREAM and rxo.cfo_mode() == 2
+        res = rxo.results(F)
+        orc = _oracle_frames(tmp_path, list(rot.cpu().numpy()), M, cp, N, nac, pid, qam, 2)
+        ok = 0
+        for f in range(F):
+            o, r = orc[f], res[f]
+            assert (r["status"] == _lib.FRAME_OK) == (o["state"] == ref.STATE_MIMO), f
+            if r["status"] != _lib.FRAME_OK:
+                continue
+            ok += 1
+            assert r["sync_index"] == o["sync_index"], f
+            e0, d = o["cfo"]
+            assert abs(r["cfo_eps"] - (e0 + d)) <= 1e-6, (f, r["cfo_eps"], e0, d)
+            assert abs(e0 + d - eps) < 2e-5, (f, e0, d)
+            got = sym[f].cpu().numpy().transpose(1, 0, 2)
+            assert evm_delta(got, o["symbols"]) <= SYM_TOL, f
+            _, num, den, _ = ref.demap_evm(o["symbols"], qam, tx[f].cpu().numpy())
+            e_gpu = 10 * np.log10(r["evm_num"] / r["evm_den"])
+            assert np.abs(e_gpu - 10 * np.log10(num / den)).max() <= EVM_DB_TOL, f
+            # the same frame alone: bit-identical
+            r1 = Receiver(P)
+            s1 = torch.zeros((1, N, pid, M), dtype=torch.complex64, device="cuda")
+            i1 = torch.zeros((1, N, pid, M), dtype=torch.uint8, device="cuda")
+            r1.process(rot[f:f + 1], L, L, 1, max_out=pid, out_sym=s1, out_idx=i1, ref_mode=1,
+                       ref_idx=tx[f:f + 1])
+            torch.cuda.synchronize()
+            assert torch.equal(s1[0], sym[f]) and torch.equal(i1[0], idx[f]), f
+            assert r1.results(1)[0]["cfo_eps"] == r["cfo_eps"], f
+        assert ok >= 2
+    # the unfolded (scratch) path -- EVM reference from the seed (ref_mode 2), so no CPE
+    # variant: estimate + scratch derotation, the oracle's cfo_mode 1
+    rxo = Receiver(P)
+    sym = torch.zeros((F, N, pid, M), dtype=torch.complex64, device="cuda")
+    idx = torch.zeros((F, N, pid, M), dtype=torch.uint8, device="cuda")
+    rxo.process(rot, L, L, F, max_out=pid, out_sym=sym, out_idx=idx, ref_mode=2, ref_seed=812,
+                frame_id0=0)
+    torch.cuda.synchronize()
+    assert rxo.cfo_mode() == 1
+    res = rxo.results(F)
+    orc = _oracle_frames(tmp_path, list(rot.cpu().numpy()), M, cp, N, nac, pid, qam, 1)
+    for f in range(F):
+        if res[f]["status"] != _lib.FRAME_OK:
+            continue
+        e0, d = orc[f]["cfo"]
+        assert abs(res[f]["cfo_eps"] - (e0 + d)) <= 1e-6, f
+        got = sym[f].cpu().numpy().transpose(1, 0, 2)
+        assert evm_delta(got, orc[f]["symbols"]) <= SYM_TOL, f
 
 
 def test_cfo_with_back_to_back_frames_is_refused_unfolded():

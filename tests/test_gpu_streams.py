@@ -167,10 +167,12 @@ def synth_streams(S, J, K, seed, M=2048, cp=152, N=4, nac=20, pid=1000, qam=64, 
 @pytest.mark.timeout(600)
 def test_c5_streams_8x3_c3_frames_match_oracle(tmp_path):
     """C5's per-stream workload at C3 geometry: 8 captures of 3 back-to-back frames, one batch
-    on the GPU, each capture checked against the oracle's stream driver (8 CPU processes)."""
+    on the GPU, each capture checked against the oracle's stream driver (8 CPU processes).
+    Every decoded frame is compared at its full PID (1000 data symbols, framing.cc:853-868),
+    as the C5 bench line decodes them."""
     import torch
     S, J, K, M, cp, N, nac, pid, qam = 8, 3, 4, 2048, 152, 4, 20, 1000, 64
-    MAXS = 48
+    MAXS = pid
     iq, L, tx, starts = synth_streams(S, J, K, seed=901)
     rxo = Receiver(RxParams(M=M, cp_len=cp, num_streams=N, num_access_codes=nac, pid_max=pid,
                             detector=_lib.DET_MMSE, qam_order=qam))
