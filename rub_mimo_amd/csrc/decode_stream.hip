@@ -186,8 +186,11 @@ template <int LOG2M, int NA>
 struct WavePlan {
   static constexpr int M = 1 << LOG2M, MS = M / 8, LG = MS / 8;
   using SP = StreamPlan<LOG2M - 3, 1>;
-  static constexpr int PADK = (MS == 256) ? 1 : 0;      // region padding (pad2 for 256 points)
-  static constexpr int QS = ((padk<PADK>(MS - 1) + 1 + 3) / 8) * 8 + 4;
+  // 256 points: sub256_fwd's per-exchange layouts (the region holds the largest, 282 entries;
+  // its stride 4 mod 32 keeps the apply's reads conflict-free); else lds_pad over the region
+  static constexpr bool X256 = (MS == 256);
+  static constexpr int PADK = 0;
+  static constexpr int QS = X256 ? 292 : ((padk<PADK>(MS - 1) + 1 + 3) / 8) * 8 + 4;
   static constexpr int GS = 8 * QS;
   static constexpr int TW0 = MS;                         // W_M^n, n < MS (powers q = 2..7 in registers)
   static constexpr int TWS = [] {
@@ -217,6 +220,71 @@ MIMO_DEV void wave_passes(v2f *buf, v2f *v, const v2f *twl, uint32_t s) {
     lds_wave_sync();
     st_store<L2, 1, SP::NP - 1, PADK>(buf, v, s);
   }
+}
+
+// The 256-point sub-transform of one 32-lane group (radix 8, 8, 4; StreamPlan<8, 1>) with a
+// layout of its own for each LDS exchange (every exchange is a store then a load, so each may
+// place the elements as it likes), chosen so that no access has a bank conflict on gfx950
+// (8-byte stores: 16-lane groups over 32 banks; 8-byte loads: 32-lane groups over 64 banks;
+// the census and the search are tools/lds/). One region-wide padding (pad2) left both radix-8
+// exchanges' stores 2-way conflicted, about a fifth of the kernel's LDS cycles:
+//   in:  element i at i (the block pass's store, lane-contiguous)
+//   x1:  i = 32 a + b at 33 a + (b ^ 4 (b >> 4)) -- stores 8 s + r from two bases per thread
+//        (the XOR flips bit 2 of r on threads with s & 2), loads s + 32 r from one
+//   x2:  i + 2 (i >> 5) + 4 (i >> 6)
+//   out: i (the apply reads across the regions, stride QS = 4 mod 32)
+MIMO_DEV void sub256_fwd(v2f *rg, v2f *v, const v2f *twl, uint32_t s) {
+  // initial load: x[s + 32 r]
+#pragma unroll
+  for (int r = 0; r < 8; r++) v[r] = rg[s + 32 * r];
+  dft_fwd_pk<8>(v);                                   // pass 0 (no twiddles): element 8 s + r
+  {
+    const uint32_t m = ((s & 3u) >> 1) << 2;          // 0 or 4
+    const uint32_t B = 33 * (s >> 2) + 8 * (s & 3u);
+    v2f *lo = rg + B + m, *hi = rg + B - m;
+#pragma unroll
+    for (int r = 0; r < 4; r++) lo[r] = v[r];
+#pragma unroll
+    for (int r = 4; r < 8; r++) hi[r] = v[r];
+  }
+  lds_wave_sync();
+  {
+    // pass 1 (radix 8, NS 8): elements s + 32 r, twiddle base W_64^{s % 8}
+    const v2f *p = rg + (s ^ ((s >> 4) << 2));
+#pragma unroll
+    for (int r = 0; r < 8; r++) v[r] = p[33 * r];
+    v2f w[8];
+    twiddle_powers<8>(w, twl[s & 7u]);
+#pragma unroll
+    for (int r = 1; r < 8; r++) v[r] = cmul_pk(v[r], w[r]);
+    dft_fwd_pk<8>(v);
+    // its outputs: elements o + 8 r, o = 64 (s / 8) + s % 8, stored at x2's layout
+    v2f *q = rg + 64 * (s >> 3) + (s & 7u) + 8 * (s >> 3);
+#pragma unroll
+    for (int r = 0; r < 8; r++) q[8 * r + 2 * (r >> 2)] = v[r];
+  }
+  lds_wave_sync();
+  {
+    // pass 2 (radix 4, NS 64): butterflies u = s, s + 32: elements u + 64 r, twiddle W_256^u
+#pragma unroll
+    for (int i = 0; i < 2; i++) {
+      const uint32_t u = s + 32 * i;
+      const v2f *p = rg + u + 2 * (u >> 5);
+#pragma unroll
+      for (int r = 0; r < 4; r++) v[4 * i + r] = p[72 * r];
+      v2f w[4];
+      twiddle_powers<4>(w, twl[8 + u]);
+#pragma unroll
+      for (int r = 1; r < 4; r++) v[4 * i + r] = cmul_pk(v[4 * i + r], w[r]);
+      dft_fwd_pk<4>(v + 4 * i);
+    }
+  }
+  lds_wave_sync();
+  // final store: element u + 64 r at its natural index
+#pragma unroll
+  for (int i = 0; i < 2; i++)
+#pragma unroll
+    for (int r = 0; r < 4; r++) rg[s + 32 * i + 64 * r] = v[4 * i + r];
 }
 
 // a wave-uniform complex value held in SGPRs
@@ -737,7 +805,7 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
       twiddle_powers<8>(w, twl[n]);
 #pragma unroll
       for (int q = 1; q < 8; q++) v[q] = cmul_pk(v[q], w[q]);
-      v2f *e = img + g * GS + padk<WP::PADK>((int)n);
+      v2f *e = img + g * GS + (WP::X256 ? (int)n : padk<WP::PADK>((int)n));
 #pragma unroll
       for (int q = 0; q < 8; q++) e[q * QS] = v[q];
     }
@@ -773,11 +841,15 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
       const uint32_t t0 = (uint32_t)opq(tid);
       const uint32_t s = t0 & (LG - 1), sg = t0 / LG;
       v2f *rg = img + (sg >> 3) * GS + (sg & 7) * QS;
-      const v2f *rp = rg + padk<WP::PADK>((int)s);
+      if constexpr (WP::X256) {
+        sub256_fwd(rg, v, twl + WP::TW0, s);
+      } else {
+        const v2f *rp = rg + padk<WP::PADK>((int)s);
 #pragma unroll
-      for (int r = 0; r < 8; r++) v[r] = rp[WP::PADK ? pad2(r * LG) : r * (LG + LG / 32)];
-      dft_fwd_pk<8>(v);
-      wave_passes<LOG2M - 3, 1, WP::PADK>(rg, v, twl + WP::TW0, s);
+        for (int r = 0; r < 8; r++) v[r] = rp[WP::PADK ? pad2(r * LG) : r * (LG + LG / 32)];
+        dft_fwd_pk<8>(v);
+        wave_passes<LOG2M - 3, 1, WP::PADK>(rg, v, twl + WP::TW0, s);
+      }
       __syncthreads();                                // every spectrum in its region
     } else {
       st_store<LOG2M, NA, 0>(img, v, (uint32_t)opq(tid));
@@ -874,7 +946,7 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
 #pragma unroll
       for (int q = 0; q < S; q++) {
         const uint32_t kk = (uint32_t)opq(tid) * S + q;
-        const v2f *xp = img + (kk & 7u) * QS + padk<WP::PADK>((int)(kk >> 3));
+        const v2f *xp = img + (kk & 7u) * QS + (WP::X256 ? (int)(kk >> 3) : padk<WP::PADK>((int)(kk >> 3)));
 #pragma unroll
         for (int r = 0; r < NA; r++) X[q][r] = xp[r * GS];
       }
@@ -911,7 +983,7 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
       auto load_x = [&](int q, v2f *X) {
         if constexpr (WF) {
           const uint32_t kk = (uint32_t)opq(tid) + q * T;
-          const v2f *xp = img + (kk & 7u) * QS + padk<WP::PADK>((int)(kk >> 3));
+          const v2f *xp = img + (kk & 7u) * QS + (WP::X256 ? (int)(kk >> 3) : padk<WP::PADK>((int)(kk >> 3)));
 #pragma unroll
           for (int r = 0; r < NA; r++) X[r] = xp[r * GS];
         } else {

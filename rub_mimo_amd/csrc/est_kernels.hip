@@ -549,7 +549,7 @@ void search_ls_wave_kernel(SearchArgs a) {
   }
   // wave-local 1024-point forward transform of c_q: X[B k + q], k = lane + 64 e, in v[e]
   reg_compute<10, 16, 0, false>(v, w1);
-  reg_rest_wave<10, 16, 1, false>(rg, v, w1, lane);
+  wave1024_rest<false>(rg, v, w1, lane);
 #pragma unroll
   for (int e = 0; e < 16; e++) X[e] = v[e];
   for (uint32_t u = 0; u < ns; u++) {                 // uniform
@@ -559,7 +559,7 @@ void search_ls_wave_kernel(SearchArgs a) {
 #pragma unroll
     for (int e = 0; e < 16; e++) v[e] = vmulc(X[e], csp[64 * e]);
     reg_compute<10, 16, 0, true>(v, w1);
-    reg_rest_wave<10, 16, 1, true>(rg, v, w1, lane);
+    wave1024_rest<true>(rg, v, w1, lane);
     // Y_q[m'] (m' = lane + 64 e) -> region q; then the radix-B pass over q per m'
     if constexpr (B > 1) {
 #pragma unroll

@@ -185,6 +185,43 @@ MIMO_DEV void reg_rest_wave(v2f *buf, v2f *v, const v2f *w1, int lane) {
   }
 }
 
+// passes 1.. of the wave-local 1024-point transform (RegPlan<10, 16>: radix 16, 4, 16) with
+// its first exchange in a layout of its own: pass 0 leaves elements 16 l + r in lane l, which
+// lds_pad places 2-way bank-conflicted for 8-byte stores (16-lane groups over 32 banks: lanes l
+// and l + 1 land on one bank) -- about a sixth of the search kernel's LDS cycles. Element
+// i = 32 a + b goes to 33 a + (b ^ 8 ((b >> 4) & 1)) instead: the stores (fixed r) then cover
+// all 16 bank pairs, from two bases per lane (the XOR swaps the halves r < 8 and r >= 8 on odd
+// lanes), and pass 1's loads (j + 256 r, fixed r) one bijection per 32 lanes. The footprint
+// (1055 entries) fits the lds_pad region (1056). Census: tools/lds/search_model.py.
+template <bool INV>
+MIMO_DEV void wave1024_rest(v2f *buf, v2f *v, const v2f *w1, int lane) {
+  using PL = RegPlan<10, 16>;
+  static_assert(PL::NP == 3 && PL::radix(0) == 16 && PL::radix(1) == 4 && PL::T == 64,
+                "plan 16, 4, 16");
+  int t = lane;
+  asm volatile("" : "+v"(t));
+  {
+    const int m = (t & 1) << 3;
+    const int B = 33 * (t >> 1) + 16 * (t & 1);
+    v2f *lo = buf + B + m, *hi = buf + B - m;
+#pragma unroll
+    for (int r = 0; r < 8; r++) lo[r] = v[r];
+#pragma unroll
+    for (int r = 8; r < 16; r++) hi[r] = v[r];
+  }
+  wave_lds_sync();
+  {
+    // pass 1: butterfly i reads elements (lane + 64 i) + 256 r
+    const v2f *p = buf + 33 * (t >> 5) + ((t & 31) ^ (((t >> 4) & 1) << 3));
+#pragma unroll
+    for (int i = 0; i < 4; i++)
+#pragma unroll
+      for (int r = 0; r < 4; r++) v[4 * i + r] = p[66 * i + 264 * r];
+  }
+  reg_compute<10, 16, 1, INV>(v, w1);
+  reg_rest_wave<10, 16, 2, INV>(buf, v, w1, lane);
+}
+
 // element index held in v[s] after the last pass (and read by pass 0): j + r*N/R, R the main
 // radix (the first and the last pass)
 template <int LOG2N, int PTS>
