@@ -68,7 +68,8 @@ struct StreamPlan {
   static constexpr int P8 = (LOG2M - 2) / 3;           // radix-8 passes (pass 0 included)
   static constexpr int TAIL = (LOG2M - 2) % 3;         // then one radix-2/-4 pass if nonzero
   static constexpr int NP = P8 + (TAIL ? 1 : 0) + 1;   // ... and a final radix-4 pass
-  static constexpr int PB = lds_padded_len(M);
+  // image stride per antenna: the largest exchange layout (x2, M + M/8; see st_store)
+  static constexpr int PB = M + M / 8;
   static constexpr int radix(int p) { return p < P8 ? 8 : (p == NP - 1 ? 4 : (1 << TAIL)); }
   static constexpr int ns(int p) {
     int n = 1;
@@ -113,28 +114,60 @@ MIMO_DEV constexpr int pad2(int i) { return i + (i >> 5) + 4 * (i >> 6); }
 template <int PADK>
 MIMO_DEV constexpr int padk(int i) { return PADK ? pad2(i) : i + (i >> 5); }   // (lds_pad)
 
-template <int LOG2M, int NA, int P, int PADK = 0>
+// Per-exchange layouts of the all-antenna plan (LAY; every exchange is a store then a load, so
+// each may place elements as it likes). With lds_pad the radix-8 stores of the first two
+// exchanges (elements 8 j + r, and 64 (j/8) + j%8 + 8 r) are 2-way bank-conflicted on gfx950
+// (8-byte stores: 16-lane groups over 32 banks), about a quarter of the transform's LDS
+// cycles; these two are conflict-free for every access (census: tools/lds/stream_plan_model.py):
+//   LAY 1 (after pass 0): i = 32 a + b at 33 a + (b ^ 4 ((b >> 4) & 1)) -- the store of 8 j + r
+//          from two bases (the XOR swaps r < 4 and r >= 4 where j & 2), the load of j + r NB
+//          from one (NB a multiple of 32);
+//   LAY 2 (after pass 1): x2(i) = i + 2 (i >> 5) + 4 (i >> 6) -- x2(o + 8 r) = x2(o) + 8 r +
+//          2 (r >> 2) for o = 64 (j/8) + j%8, x2(j + r NB) = x2(j) + 9 r NB / 8 (NB a multiple
+//          of 64); footprint M + M/8 (PB);
+//   LAY 0: lds_pad (padk<PADK>), later exchanges and the final natural-order store.
+MIMO_DEV constexpr int x2pad(int i) { return i + 2 * (i >> 5) + 4 * (i >> 6); }
+template <int NP>
+constexpr int ex_layout(int e) { return e == 0 ? 1 : ((e == 1 && e < NP - 1) ? 2 : 0); }
+
+template <int LOG2M, int NA, int P, int PADK = 0, int LAY = 0>
 MIMO_DEV void st_store(v2f *buf, const v2f *v, uint32_t tid) {
   using PL = StreamPlan<LOG2M, NA>;
   constexpr uint32_t R = PL::radix(P), NS = PL::ns(P), NB = PL::M / R;
   static_assert(NB % 32 == 0 && (NS >= 32 || (32 % (NS * R) == 0) || (NS * R) % 32 == 0),
                 "padded-offset identity");
   static_assert(!PADK || PL::M == 256, "pad2 identities checked for the 256-point plan only");
+  static_assert(LAY != 1 || (P == 0 && R == 8), "x1 stores: pass 0, radix 8");
+  static_assert(LAY != 2 || (P == 1 && R == 8 && NS == 8), "x2 stores: pass 1, radix 8");
 #pragma unroll
   for (int i = 0; i < PL::bt(P); i++) {
     const uint32_t u = tid + i * PL::T, g = u / NB, j = u % NB;
-    const uint32_t o = (j / NS) * NS * R + (j % NS);
-    v2f *bp = buf + g * PL::PB + padk<PADK>((int)o);
+    if constexpr (LAY == 1) {
+      const uint32_t m = ((j >> 1) & 1u) << 2;
+      const uint32_t B = g * PL::PB + 33 * (j >> 2) + 8 * (j & 3u);
+      v2f *lo = buf + B + m, *hi = buf + B - m;
 #pragma unroll
-    for (int r = 0; r < (int)R; r++)
-      bp[PADK ? pad2(r * (int)NS) : st_off<NS, R>(r)] = v[i * R + r];
+      for (int r = 0; r < 4; r++) lo[r] = v[i * R + r];
+#pragma unroll
+      for (int r = 4; r < 8; r++) hi[r] = v[i * R + r];
+    } else if constexpr (LAY == 2) {
+      v2f *bp = buf + g * PL::PB + 64 * (j >> 3) + (j & 7u) + 8 * (j >> 3);
+#pragma unroll
+      for (int r = 0; r < 8; r++) bp[8 * r + 2 * (r >> 2)] = v[i * R + r];
+    } else {
+      const uint32_t o = (j / NS) * NS * R + (j % NS);
+      v2f *bp = buf + g * PL::PB + padk<PADK>((int)o);
+#pragma unroll
+      for (int r = 0; r < (int)R; r++)
+        bp[PADK ? pad2(r * (int)NS) : st_off<NS, R>(r)] = v[i * R + r];
+    }
   }
 }
 
 // pass P with its base twiddle from the LDS table (twl: passes 1.. in order, one row of NS
 // entries each, [jm] = e^{-2 pi i jm / (NS R)}) and the powers r = 2 .. R-1 in registers: one
 // LDS read per butterfly instead of R - 1 (the transform phase is bound by LDS instructions)
-template <int LOG2M, int NA, int P, int PADK = 0>
+template <int LOG2M, int NA, int P, int PADK = 0, int LAY = 0>
 MIMO_DEV void st_load_t(const v2f *buf, v2f *v, const v2f *twl, uint32_t tid) {
   using PL = StreamPlan<LOG2M, NA>;
   constexpr uint32_t R = PL::radix(P), NB = PL::M / R, NS = PL::ns(P);
@@ -143,13 +176,25 @@ MIMO_DEV void st_load_t(const v2f *buf, v2f *v, const v2f *twl, uint32_t tid) {
     for (int q = 1; q < P; q++) o += PL::ns(q);
     return o;
   }();
+  static_assert(LAY != 1 || NB % 32 == 0, "x1 loads: NB a multiple of 32");
+  static_assert(LAY != 2 || NB % 64 == 0, "x2 loads: NB a multiple of 64");
 #pragma unroll
   for (int i = 0; i < PL::bt(P); i++) {
     const uint32_t u = tid + i * PL::T, g = u / NB, j = u % NB;
-    const v2f *bp = buf + g * PL::PB + padk<PADK>((int)j);
+    if constexpr (LAY == 1) {
+      const v2f *bp = buf + g * PL::PB + 33 * (j >> 5) + ((j & 31u) ^ (((j >> 4) & 1u) << 2));
 #pragma unroll
-    for (int r = 0; r < (int)R; r++)
-      v[i * R + r] = bp[PADK ? pad2(r * (int)NB) : r * NB + (r * NB) / 32];
+      for (int r = 0; r < (int)R; r++) v[i * R + r] = bp[33 * r * (int)(NB / 32)];
+    } else if constexpr (LAY == 2) {
+      const v2f *bp = buf + g * PL::PB + x2pad((int)j);
+#pragma unroll
+      for (int r = 0; r < (int)R; r++) v[i * R + r] = bp[9 * r * (int)(NB / 8)];
+    } else {
+      const v2f *bp = buf + g * PL::PB + padk<PADK>((int)j);
+#pragma unroll
+      for (int r = 0; r < (int)R; r++)
+        v[i * R + r] = bp[PADK ? pad2(r * (int)NB) : r * NB + (r * NB) / 32];
+    }
     v2f w[R];
     twiddle_powers<R>(w, twl[OFF + (j % NS)]);
 #pragma unroll
@@ -165,10 +210,10 @@ MIMO_DEV void st_passes2(v2f *img, v2f *v, const v2f *twl, uint32_t tid) {
   if constexpr (P < PL::NP) {
     const uint32_t t = (uint32_t)opq((int)tid);   // opaque per pass: addresses not hoisted
     __syncthreads();                        // the image is complete
-    st_load_t<LOG2M, NA, P>(img, v, twl, t);
+    st_load_t<LOG2M, NA, P, 0, ex_layout<PL::NP>(P - 1)>(img, v, twl, t);
     if constexpr (P + 1 < PL::NP) {
       __syncthreads();                      // readers of the image are done
-      st_store<LOG2M, NA, P>(img, v, t);
+      st_store<LOG2M, NA, P, 0, ex_layout<PL::NP>(P)>(img, v, t);
       st_passes2<LOG2M, NA, P + 1>(img, v, twl, tid);
     }
   }
@@ -852,7 +897,7 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
       }
       __syncthreads();                                // every spectrum in its region
     } else {
-      st_store<LOG2M, NA, 0>(img, v, (uint32_t)opq(tid));
+      st_store<LOG2M, NA, 0, 0, ex_layout<PL::NP>(0)>(img, v, (uint32_t)opq(tid));
 #ifndef DS_ABL_NOFFT   // timing ablation: no passes 1.. and no final exchange
       st_passes2<LOG2M, NA, 1>(img, v, twl, tid);
       {
