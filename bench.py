@@ -138,6 +138,8 @@ def decode_kernel_name(M, N, args, path=None):
     lg = M.bit_length() - 1
     if path == 1:
         return "decode_stream_kernel<%d,%d>" % (lg, N)
+    if path == 4:   # one pass, 8x8 at M = 4096 by subcarrier residue class
+        return "decode_res8_kernel"
     if path == 2:   # (the persistent spectra form for M >= 2048 and the 128-subcarrier apply)
         return ("spectra_persist_kernel<%d>|apply_split2_kernel<8>" % lg if lg >= 11 else
                 "spectra_kernel<%d>|apply_split2_kernel<8>" % lg)
@@ -500,7 +502,7 @@ def main():
     # transmitted index read when the EVM reference comes from HBM)
     kname = decode_kernel_name(M, N, args, rx.decode_path())
     # (sc16 is read in place by the streaming decode; other decode kernels read the widened copy)
-    dec_in = in_bytes if kname.startswith("decode_stream") else 8
+    dec_in = in_bytes if kname.startswith(("decode_stream", "decode_res8")) else 8
     per_sym = N * M * dec_in + N * m_occ * 9 + (N * m_occ if args.ref_mode == 1 else 0)
     dec_bytes = n_dec * per_sym
     achieved = dec_bytes / dec_avg_s / 1e9 if dec_avg_s > 0 else 0.0

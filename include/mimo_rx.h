@@ -205,10 +205,12 @@ int mimo_rx_get_stage_times(mimo_rx *h, double *ms, uint32_t *launches);
  * oracle's exact fp32 order, since the last call (diagnostic; synchronises) */
 int mimo_rx_get_sc_exact_count(mimo_rx *h, uint64_t *out);
 /* the replay-decode kernel family the last batch or execute launched (diagnostic, no sync):
- * STREAM = decode_stream_kernel (persistent, 2x2/4x4), SPLIT = spectra_kernel +
- * apply_split_kernel (8x8 at M >= 512), SYMBOL = the per-symbol kernels, NONE = no decode yet */
+ * STREAM = decode_stream_kernel (persistent, 2x2/4x4), RESIDUE = decode_res8_kernel (one pass,
+ * 8x8 at M = 4096, eight workgroups per symbol by subcarrier residue class), SPLIT =
+ * spectra_kernel + apply_split_kernel (8x8 at M >= 512 otherwise), SYMBOL = the per-symbol
+ * kernels, NONE = no decode yet */
 enum { MIMO_DECODE_NONE = 0, MIMO_DECODE_STREAM = 1, MIMO_DECODE_SPLIT = 2,
-       MIMO_DECODE_SYMBOL = 3 };
+       MIMO_DECODE_SYMBOL = 3, MIMO_DECODE_RESIDUE = 4 };
 int mimo_rx_get_decode_path(const mimo_rx *h, int32_t *path);
 /* the CFO stages the last batch ran (diagnostic, no sync): 0 off, 1 estimate and derotation,
  * 2 the same plus the per-symbol common phase (the streaming decode's CPE variant) -- the

@@ -21,7 +21,7 @@ STAGE_NAMES = ("sc", "plateau", "search", "ls", "weights", "decode", "evm")
 STATE_SEEK_PLATEAU, STATE_SAVE_ACCESS_CODES, STATE_WAIT, STATE_MIMO = 0, 1, 2, 3
 DET_ZF2, DET_ZF, DET_MMSE, DET_SISO = 0, 1, 2, 3
 FRAME_OK, FRAME_NO_SYNC, FRAME_INCOMPLETE, FRAME_RESCAN, FRAME_NONE = 0, 1, 2, 3, 4
-DECODE_NONE, DECODE_STREAM, DECODE_SPLIT, DECODE_SYMBOL = 0, 1, 2, 3
+DECODE_NONE, DECODE_STREAM, DECODE_SPLIT, DECODE_SYMBOL, DECODE_RESIDUE = 0, 1, 2, 3, 4
 
 
 class RxConfig(C.Structure):

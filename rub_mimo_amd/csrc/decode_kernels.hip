@@ -862,6 +862,7 @@ uint32_t launch_decode(const DecodeArgs &a, int log2M, uint32_t n_frames, hipStr
     // the folded CFO (cpe == 2: no derotated scratch capture) is applied by the streaming
     // decode only; any other kernel would decode the raw samples
     if (!parts && a.cpe == 2) return 0;
+    if (!parts && (parts = launch_decode_res8(a, log2M, n_frames, s))) *path = 4;
     if (!parts && (parts = launch_decode_split(a, log2M, n_frames, s))) *path = 2;
     if (parts) {
       *per_frame_records = true;

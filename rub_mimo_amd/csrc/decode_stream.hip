@@ -1493,6 +1493,369 @@ __global__ __launch_bounds__(64 * NA) void apply_split2_kernel(DecodeArgs a) {
   }
 }
 
+// ------------------------------------------------------------------------------------
+// One-pass 8x8 decode at M = 4096 by residue class (C4; replaces the split decode's spectra
+// round trip through HBM). With the radix-8 decimation in frequency over stride 512,
+//   X_g[8 k + q] = DFT_512( c_q )[k],   c_q[n] = W_4096^{n q} sum_{r<8} x_g[n + 512 r] W_8^{r q},
+// the subcarriers k = q (mod 8) of a symbol need only the 512-point transforms of c_q. So eight
+// workgroups share a symbol, workgroup q computing residue class q for all eight antennas
+// (the one-output DFT over r by Horner's rule, then eight wave-local 512-point transforms) and
+// applying the weights of its 512 subcarriers, which it keeps in registers for all symbols of a
+// frame (64 VGPRs: 512 x 8 x 8 complex = 256 KB per class, one 1024-thread workgroup). Every
+// workgroup reads the whole symbol (256 KB), from L2: the eight of a symbol are blocks
+// b, b + 8, ..., b + 56, dealt to one XCD by the round-robin placement (speed only), so HBM
+// reads each symbol once; their outputs (every eighth subcarrier) merge in that XCD's L2 into
+// whole lines. No scratch, no hand-over between workgroups, no atomics.
+// Per symbol: the samples arrive by antenna pair into registers (the next pair's loads in
+// flight, the next symbol's first pair during the transforms and the apply), c_q goes to one of
+// two LDS images (double-buffered: two barriers per symbol), waves 0-7 transform antennas 0-7
+// in their own regions (exchanges in conflict-free layouts, as the streaming decode), then all
+// 16 waves apply W (thread: one subcarrier, four of the eight output streams), demap, EVM and
+// store.
+constexpr int kR8T = 1024;
+constexpr int kR8MS = 512;                    // points of a residue transform
+constexpr int kR8RS = 576;                    // region stride (entries): the x2 layout's 570
+constexpr int kR8Groups = 8;                  // residue classes = workgroups per symbol
+
+// the wave-local 512-point forward transform of region rg (RegPlan<9, 8>: radix 8, 8, 8) with
+// the streaming decode's exchange layouts (x1 after pass 0, x2 after pass 1; lds_pad left both
+// radix-8 stores 2-way bank-conflicted); input and output in natural order, element lane + 64 e
+MIMO_DEV void wave512_fwd(v2f *rg, const v2f *w1, int lane) {
+  using PL = RegPlan<9, 8>;
+  static_assert(PL::NP == 3 && PL::RM == 8 && PL::T == 64, "plan 8, 8, 8 on one wave");
+  v2f v[8];
+  int t = lane;
+  asm volatile("" : "+v"(t));
+#pragma unroll
+  for (int r = 0; r < 8; r++) v[r] = rg[t + 64 * r];
+  reg_compute<9, 8, 0, false>(v, w1);
+  {   // x1: element 8 t + r at 33 (t >> 2) + 8 (t & 3) + (r ^ m), m = 4 ((t >> 1) & 1)
+    const int m = ((t >> 1) & 1) << 2;
+    const int B = 33 * (t >> 2) + 8 * (t & 3);
+    v2f *lo = rg + B + m, *hi = rg + B - m;
+#pragma unroll
+    for (int r = 0; r < 4; r++) lo[r] = v[r];
+#pragma unroll
+    for (int r = 4; r < 8; r++) hi[r] = v[r];
+  }
+  wave_lds_sync();
+  {   // pass 1 loads elements t + 64 r
+    const v2f *p = rg + 33 * (t >> 5) + ((t & 31) ^ (((t >> 4) & 1) << 2));
+#pragma unroll
+    for (int r = 0; r < 8; r++) v[r] = p[66 * r];
+  }
+  reg_compute<9, 8, 1, false>(v, w1);
+  {   // x2: element 64 (t/8) + t%8 + 8 r
+    v2f *q = rg + 64 * (t >> 3) + (t & 7) + 8 * (t >> 3);
+#pragma unroll
+    for (int r = 0; r < 8; r++) q[8 * r + 2 * (r >> 2)] = v[r];
+  }
+  wave_lds_sync();
+  {   // pass 2 loads elements t + 64 r
+    const v2f *p = rg + x2pad(t);
+#pragma unroll
+    for (int r = 0; r < 8; r++) v[r] = p[72 * r];
+  }
+  reg_compute<9, 8, 2, false>(v, w1);
+  wave_lds_sync();
+#pragma unroll
+  for (int r = 0; r < 8; r++) rg[t + 64 * r] = v[r];
+}
+
+template <int REF, int OUTS, bool SC16>
+__global__ __launch_bounds__(kR8T) void decode_res8_kernel(DecodeArgs a) {
+  constexpr int NA = 8, M = 4096, MS = kR8MS, RS = kR8RS, T = kR8T;
+  extern __shared__ __attribute__((aligned(16))) float2 lds_raw[];
+  v2f *img = reinterpret_cast<v2f *>(lds_raw);        // [2][NA][RS]
+  v2f *wl = img + 2 * NA * RS;                         // [NA][T]: output 4 h + 3's weights
+  v2f *wnl = wl + NA * T;                              // [MS]: W_4096^{n q}
+  v2f *w1l = wnl + MS;                                 // [64][2]: the 512-point plan's twiddles
+  __shared__ uint32_t pfx[kStreamMaxFrames + 1];
+  __shared__ v2f ptab[kStreamMaxQam];
+  __shared__ uint8_t gidx[kStreamMaxQam];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const uint32_t wv = __builtin_amdgcn_readfirstlane((uint32_t)tid >> 6);
+  // residue class and group: blocks b, b + 8, .., b + 56 (one XCD) are the classes of a group
+  const uint32_t q = (blockIdx.x >> 3) & 7u;
+  const uint32_t G = gridDim.x / kR8Groups;
+  const uint32_t grp = (blockIdx.x & 7u) + 8u * (blockIdx.x >> 6);
+  for (uint32_t e = tid; e < a.qam.L * a.qam.L; e += T) {
+    const float2 p = qam_point(e, a.qam);
+    ptab[e] = v2f{p.x, p.y};
+    const uint32_t mI = e / a.qam.L, mQ = e % a.qam.L;
+    gidx[e] = (uint8_t)((gray_enc(mI) << a.qam.b) | gray_enc(mQ));
+  }
+  for (uint32_t f0 = 0; f0 <= a.n_frames; f0 += T) {
+    const uint32_t f = f0 + tid;
+    if (f < a.n_frames) {
+      const FrameInfo &I = a.info[f];
+      pfx[f] = (I.status == 0) ? min(I.n_sym, a.max_out) : 0u;
+    } else if (f == a.n_frames) {
+      pfx[f] = 0;
+    }
+  }
+  __syncthreads();
+  if (tid == 0) {
+    uint32_t acc = 0;
+    for (uint32_t f = 0; f <= a.n_frames; f++) {
+      const uint32_t v = pfx[f];
+      pfx[f] = acc;
+      acc += v;
+    }
+  }
+  __syncthreads();
+  const uint32_t total = pfx[a.n_frames];
+  const uint32_t chunk = (total + G - 1) / G;
+  const uint32_t i_begin = grp * chunk;
+  const uint32_t i_end = min(i_begin + chunk, total);
+  if (i_begin >= i_end) return;                       // uniform (the whole group alike)
+  uint32_t f = 0;
+  {
+    uint32_t lo = 0, hi = a.n_frames;
+    while (hi - lo > 1) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (pfx[mid] <= i_begin) lo = mid; else hi = mid;
+    }
+    f = __builtin_amdgcn_readfirstlane(lo);
+  }
+  uint32_t s = __builtin_amdgcn_readfirstlane(i_begin - pfx[f]);
+
+  // stage A thread roles: antenna 2 j + (tid >> 9) of pair j, position n = tid & 511
+  const uint32_t n = (uint32_t)tid & (MS - 1), ga = (uint32_t)tid >> 9;
+  // W_8^{q} (Horner's rule over r; uniform), W_4096^{n q} and the 512-point plan's base
+  // twiddles tabled in LDS (read where used: registers are the scarce resource here)
+  const v2f w8 = uni(twiddle<false>(a.tw, (int)(q * (kTwN / 8))));
+  static_assert(RegPlan<9, 8>::NTW == 2, "two base twiddles per lane");
+  if (tid < MS) wnl[tid] = twiddle<false>(a.tw, (int)((((uint32_t)tid * q) & (M - 1)) * (kTwN / M)));
+  if (tid < 64) reg_twiddles<9, 8>(w1l + 2 * tid, a.tw, tid);
+  __syncthreads();                                    // the tables before their first readers
+  // stage C: subcarrier k = 8 (tid >> 1) + q, output streams 4 h .. 4 h + 3
+  const uint32_t kq = (uint32_t)tid >> 1, h = (uint32_t)tid & 1u;
+  const uint32_t k = 8 * kq + q;
+  // outputs 4 h .. 4 h + 2 in registers (48 VGPRs), 4 h + 3 in LDS (a fourth register set
+  // beside the symbol's samples in flight spilled)
+  v2f Wr[3][NA];
+  auto load_w = [&](uint32_t ff) {
+    const float gk = a.gain[(uint64_t)ff * M + k] * a.dn;
+#pragma unroll
+    for (int j = 0; j < 4; j++)
+#pragma unroll
+      for (int r = 0; r < NA; r++) {
+        const float2 w = a.W[(((uint64_t)ff * NA + 4 * h + j) * NA + r) * M + k];
+        const v2f wv = v2f{w.x * gk, w.y * gk};
+        if (j < 3) Wr[j][r] = wv;
+        else wl[r * T + tid] = wv;   // (this thread's own slots: read back by it alone)
+      }
+  };
+  const v2f inv_sc = v2f{a.qam.inv_scale, a.qam.inv_scale};
+  const v2f Lf = v2f{(float)a.qam.L, (float)a.qam.L};
+  const uint32_t Lm1 = a.qam.L - 1;
+  float e_num[4], e_den[4];
+  uint32_t n_err[2][4];                                // per lane parity (stream half), SGPRs
+#pragma unroll
+  for (int j = 0; j < 4; j++) {
+    e_num[j] = e_den[j] = 0.0f;
+    n_err[0][j] = n_err[1][j] = 0u;
+  }
+  // per-wave EVM partials of this (group, frame) segment, reduced through the two images
+  // (both dead here: this symbol's apply has read one, the other held the previous symbol;
+  // frame boundaries only: two barriers there, no shuffles -- their registers beside the
+  // weights spilled)
+  auto flush = [&](uint32_t ff) {
+    const uint32_t jrec = (grp - pfx[ff] / chunk) * kR8Groups + q;
+    if (tid == 0 && pfx[ff] >= i_begin && q == 0)   // the frame's first group, class 0
+      a.nrec[ff] = ((pfx[ff + 1] - 1) / chunk - pfx[ff] / chunk + 1) * kR8Groups;
+    __syncthreads();                                  // every wave's image reads done
+    static_assert(12 * T * sizeof(float) <= 2 * NA * RS * sizeof(v2f), "flush table fits");
+    float *red = reinterpret_cast<float *>(img);      // [12][T]: num, den, errors per j
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      red[(3 * j + 0) * T + tid] = e_num[j];
+      red[(3 * j + 1) * T + tid] = e_den[j];
+      red[(3 * j + 2) * T + tid] = (float)(h ? n_err[1][j] : n_err[0][j]);
+      e_num[j] = e_den[j] = 0.0f;
+      n_err[0][j] = n_err[1][j] = 0u;
+    }
+    __syncthreads();
+    // lane < 24 of each wave: stream t = lane / 3 (its parity h = t >> 2 of the lanes that
+    // computed it), component c; the errors are wave counts (every lane of a parity holds the
+    // same), the sums over the wave's lanes of that parity in lane order
+    if (lane < NA * 3) {
+      const uint32_t t = lane / 3, c = lane % 3, hh = t >> 2, j = t & 3u;
+      const float *src = red + (3 * j + c) * T + wv * 64 + hh;
+      float v = 0.0f;
+      if (c == 2) {
+        v = src[0];
+      } else {
+        for (int l = 0; l < 64; l += 2) v += src[l];
+      }
+      a.evm_part[(((uint64_t)ff * a.rec_stride + jrec) * (T / 64) + wv) * NA * 3 + lane] = (double)v;
+    }
+  };
+
+  // the samples of antenna pair j of symbol (ff, ss): x_g[n + 512 r], r < 8 (the row of
+  // antenna g = 2 j + ga is uniform per wave: an SGPR base and 32-bit lane offsets)
+  auto load_pair = [&](v2f (&x)[8], uint32_t ff, uint32_t ss, int j) {
+    const FrameInfo &I = a.info[ff];
+    const int64_t b0 = I.base + (int64_t)I.i0 + (int64_t)a.cp + (int64_t)ss * a.SL;
+    const uint32_t g = 2 * (uint32_t)j + ga;
+    const uint64_t row = ((uint64_t)I.cap * NA + g) * a.stride;
+    const uint32_t nn = (uint32_t)opq((int)n);
+    if (b0 >= 0 && b0 + M <= (int64_t)a.frame_len) {   // uniform
+      if constexpr (SC16) {
+        const auto xb = sgpr_ptr(reinterpret_cast<const uint32_t *>(a.iq) + row + (uint64_t)b0);
+        const Iq<true> cv{nullptr, a.iq_scale};
+#pragma unroll
+        for (int r = 0; r < 8; r++) {
+          const uint32_t w = xb[nn + MS * r];   // interleaved int16 I, Q
+          const float2 v = cv.cvt(make_short2((short)(w & 0xFFFFu), (short)(w >> 16)));
+          x[r] = v2f{v.x, v.y};
+        }
+      } else {
+        const auto xb = sgpr_ptr(reinterpret_cast<const v2f *>(a.iq) + row + (uint64_t)b0);
+#pragma unroll
+        for (int r = 0; r < 8; r++) x[r] = xb[nn + MS * r];
+      }
+    } else {
+      const auto xs = iq_row<SC16>(a.iq, a.iq_scale, row);
+#pragma unroll
+      for (int r = 0; r < 8; r++) {
+        const int64_t m = b0 + nn + MS * r;
+        const bool in = m >= 0 && m < (int64_t)a.frame_len;
+        const float2 v = xs.at(in ? m : 0);
+        x[r] = in ? v2f{v.x, v.y} : v2f{0.0f, 0.0f};
+      }
+    }
+  };
+  // c_q[n] of the pair's antenna into the image
+  auto pass0 = [&](const v2f (&x)[8], v2f *im, int j) {
+    v2f c = x[7];
+#pragma unroll
+    for (int r = 6; r >= 0; r--) c = cmac_pk(x[r], c, w8);   // c = x_r + c W_8^q
+    c = cmul_pk(c, wnl[(uint32_t)opq((int)n)]);
+    im[(2 * (uint32_t)j + ga) * RS + (uint32_t)opq((int)n)] = c;
+  };
+
+  load_w(f);
+  v2f xa[8], xb[8];                                   // antenna pairs in flight (named slots)
+  load_pair(xa, f, s, 0);
+  uint32_t n_out_f = pfx[f + 1] - pfx[f];
+  for (uint32_t i = i_begin; i < i_end; i++) {
+    const uint32_t buf = i & 1u;
+    v2f *im = img + buf * NA * RS;
+    // the item after this one (uniform)
+    uint32_t fn = f, sn = s + 1;
+    const bool more = i + 1 < i_end;
+    if (more && sn >= n_out_f) {
+      do { fn++; } while (pfx[fn + 1] == pfx[fn]);
+      sn = 0;
+    }
+    fn = __builtin_amdgcn_readfirstlane(fn);
+    sn = __builtin_amdgcn_readfirstlane(sn);
+    // stage A: four antenna pairs, the next one's loads in flight
+    load_pair(xb, f, s, 1);
+    pass0(xa, im, 0);
+    load_pair(xa, f, s, 2);
+    pass0(xb, im, 1);
+    load_pair(xb, f, s, 3);
+    pass0(xa, im, 2);
+    if (more) load_pair(xa, fn, sn, 0);               // the next symbol's first pair
+    pass0(xb, im, 3);
+    __syncthreads();                                  // every c_q of the symbol in the image
+    // stage B: antenna g's 512-point transform on wave g
+    if (wv < (uint32_t)NA) {
+      v2f w1[2];
+      w1[0] = w1l[2 * lane];
+      w1[1] = w1l[2 * lane + 1];
+      wave512_fwd(im + wv * RS, w1, lane);
+    }
+    __syncthreads();                                  // X_g[8 k' + q] at im[g][k']
+    // stage C: apply (antenna by antenna into four accumulators), demap, EVM, stores
+    v2f acc[4] = {v2f{0.0f, 0.0f}, v2f{0.0f, 0.0f}, v2f{0.0f, 0.0f}, v2f{0.0f, 0.0f}};
+    {
+      const v2f *xp = im + (uint32_t)opq((int)kq);
+      const v2f *wp = wl + (uint32_t)opq(tid);
+#pragma unroll
+      for (int g = 0; g < NA; g++) {
+        const v2f Xg = xp[g * RS];
+#pragma unroll
+        for (int j = 0; j < 3; j++) acc[j] = cmac_pk(acc[j], Wr[j][g], Xg);
+        acc[3] = cmac_pk(acc[3], wp[g * T], Xg);
+      }
+    }
+    const uint64_t frame_id = a.frame_id0 + a.info[f].ref;
+    const uint64_t rowstep = (uint64_t)a.max_out * a.M_occ;
+    const uint64_t ob0 = rfl64((((uint64_t)f * NA) * a.max_out + s) * a.M_occ);
+    const auto osym = sgpr_ptr(reinterpret_cast<v2f *>(a.out_sym) + ob0);
+    const auto oidx = sgpr_ptr(a.out_idx + ob0);
+    const auto rref = sgpr_ptr(a.ref_idx + rfl64((uint64_t)a.info[f].ref * NA * rowstep + (uint64_t)s * a.M_occ));
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      const uint32_t t = 4 * h + (uint32_t)j;
+      const uint32_t off = t * (uint32_t)rowstep + k;   // < 2^32: checked at launch
+      const v2f y = acc[j];
+      const uint32_t d = gidx[qam_level_pair_pk(y, inv_sc, Lf, Lm1, a.qam.L)];
+      uint32_t refi;
+      if constexpr (REF == 1) refi = rref[off];
+      else if constexpr (REF == 2)
+        refi = (uint32_t)(hash5(a.ref_seed, DOM_DATA, frame_id, t, (uint64_t)s * a.M_occ + k) &
+                          (uint64_t)(a.qam.L * a.qam.L - 1));
+      else refi = d;
+      const unsigned long long bal = __builtin_amdgcn_ballot_w64(refi != d);
+      n_err[0][j] += (uint32_t)__builtin_popcountll(bal & 0x5555555555555555ull);
+      n_err[1][j] += (uint32_t)__builtin_popcountll(bal & 0xAAAAAAAAAAAAAAAAull);
+      const v2f sp = ptab[refi];
+      const v2f er = y - sp;
+      e_num[j] = __builtin_fmaf(er.x, er.x, __builtin_fmaf(er.y, er.y, e_num[j]));
+      e_den[j] = __builtin_fmaf(sp.x, sp.x, __builtin_fmaf(sp.y, sp.y, e_den[j]));
+      if constexpr (OUTS & 1) osym[off] = y;
+      if constexpr (OUTS & 2) oidx[off] = (uint8_t)d;
+    }
+    if (!more || fn != f) {
+      flush(f);
+      if (more) {
+        n_out_f = pfx[fn + 1] - pfx[fn];
+        load_w(fn);
+      }
+    }
+    f = fn;
+    s = sn;
+  }
+}
+
+// the residue-class decode's LDS and grid: two images; 64 workgroups per 8 XCDs x 8 classes
+static size_t res8_lds_bytes() { return sizeof(float2) * (2 * 8 * kR8RS + 8 * kR8T + kR8MS + 128); }
+static uint32_t res8_grid(uint32_t n_cu) { return 64u * std::max(1u, n_cu / 64u); }
+
+bool decode_res8_accepts(const DecodeArgs &a, int log2M, uint32_t n_frames) {
+  static const bool off = [] { const char *e = getenv("RMIMO_DECODE_RES"); return e && e[0] == '0'; }();
+  return !off && a.N == 8 && log2M == 12 && a.detector != 3 && a.all_occ &&
+         n_frames <= kStreamMaxFrames && a.qam.L * a.qam.L <= kStreamMaxQam && a.cpe == 0;
+}
+
+// EVM records per frame the residue decode may write (the classes of every group)
+uint32_t res8_records(uint32_t n_cu) { return res8_grid(n_cu); }
+
+uint32_t launch_decode_res8(const DecodeArgs &a, int log2M, uint32_t n_frames, hipStream_t s) {
+  if (!a.nrec || !decode_res8_accepts(a, log2M, n_frames)) return 0;
+  if (res8_records(a.n_cu) > a.rec_stride) return 0;  // EVM space
+  if ((uint64_t)a.N * a.max_out * a.M_occ >= (1ull << 32)) return 0;   // 32-bit lane offsets
+  const int outs = (a.out_sym ? 1 : 0) | (a.out_idx ? 2 : 0);
+  void (*kern)(DecodeArgs) = nullptr;
+#define R8K(R, S)                                                              \
+  (outs == 3 ? decode_res8_kernel<R, 3, S> : outs == 2 ? decode_res8_kernel<R, 2, S> \
+   : outs == 1 ? decode_res8_kernel<R, 1, S> : decode_res8_kernel<R, 0, S>)
+  if (a.sc16) kern = a.ref_mode == 1 ? R8K(1, true) : a.ref_mode == 2 ? R8K(2, true) : R8K(0, true);
+  else kern = a.ref_mode == 1 ? R8K(1, false) : a.ref_mode == 2 ? R8K(2, false) : R8K(0, false);
+#undef R8K
+  const size_t shm = res8_lds_bytes();
+  if (hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+                          (int)shm) != hipSuccess)
+    return 0;
+  hipLaunchKernelGGL(kern, dim3(res8_grid(a.n_cu)), dim3(kR8T), shm, s, a);
+  return kR8T / 64;
+}
+
 bool decode_split_accepts(const DecodeArgs &a, int log2M) {
   // (the apply reads 16 bytes of reference indices per lane)
   return a.N == 8 && a.detector != 3 && a.all_occ && log2M >= 9 && log2M <= 12 &&

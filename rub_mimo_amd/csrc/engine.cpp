@@ -666,12 +666,14 @@ int run_decode(mimo_rx *h, const float2 *iq, uint64_t stride, uint32_t F, uint64
   d.rec_stride = max_out;
   // (the split records' stride only where the split kernels can run: RMIMO_DEC_EXPT forces
   // the per-symbol kernels, whose records are max_out apart)
+  if (d.expt == 0 && decode_res8_accepts(d, h->log2M, F))   // residue-class records per frame
+    d.rec_stride = std::max(d.rec_stride, res8_records(h->n_cu));
   if (!no_split && d.expt == 0 && decode_split_accepts(d, h->log2M)) {
     // [F][M/64][group][N][64] complex64 spectra of the 8x8 split decode (one symbol group)
     if (h->spec.ensure((size_t)F * split_group_symbols(max_out) * h->N * h->M) != hipSuccess)
       return fail(MIMO_ERR_NOMEM, "split decode scratch");
     d.spec = h->spec.p;
-    d.rec_stride = std::max(max_out, split_plan(max_out, h->log2M, nullptr, nullptr));
+    d.rec_stride = std::max(d.rec_stride, split_plan(max_out, h->log2M, nullptr, nullptr));
   }
   {
     const int rc0 = ensure_workspace(h, F, 0, (uint64_t)F * d.rec_stride * h->N * 3 * kMaxEvmParts);
@@ -703,7 +705,8 @@ int run_decode(mimo_rx *h, const float2 *iq, uint64_t stride, uint32_t F, uint64
   ea.chunk_part = h->evm_chunk.p;
   ea.counter = h->evm_cnt.p;
   ea.nrec = per_frame ? h->nrec.p : nullptr;
-  ea.few = path == MIMO_DECODE_STREAM ? 1 : 0;   // per workgroup segment, not per chunk x range
+  // per workgroup segment (streaming, residue-class), not per chunk x range
+  ea.few = (path == MIMO_DECODE_STREAM || path == MIMO_DECODE_RESIDUE) ? 1 : 0;
   e = h->timer.begin(s);
   launch_evm(ea, F, s);
   h->timer.end(6, e, s);
@@ -1349,6 +1352,7 @@ static int run_batch(mimo_rx *h, const mimo_batch *b, hipStream_t s) {
     static const bool no_split = [] { const char *e = getenv("RMIMO_DECODE_SPLIT"); return e && e[0] == '0'; }();
     const bool fused = sc_screen_ok(h->M) && h->search_ls && !h->cfo && decode_expt() == 0 &&
                        (decode_stream_accepts(probe, h->log2M, slots) ||
+                        decode_res8_accepts(probe, h->log2M, slots) ||
                         (!no_split && decode_split_accepts(probe, h->log2M)));
     if (fused) {
       h->cur_sc16 = 1;

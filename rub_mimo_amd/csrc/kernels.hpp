@@ -300,6 +300,11 @@ bool decode_stream_cpe(const DecodeArgs &a);
 // alternating over symbol groups); 0 when the configuration is not handled or a.spec is null.
 // The scratch holds split_group_symbols(max_out) symbols per frame.
 uint32_t launch_decode_split(const DecodeArgs &a, int log2M, uint32_t n_frames, hipStream_t s);
+// one-pass 8x8 decode by residue class (M = 4096): accepts / launches (0: not handled), and
+// the EVM records per frame it may write (rec_stride must hold them)
+bool decode_res8_accepts(const DecodeArgs &a, int log2M, uint32_t n_frames);
+uint32_t launch_decode_res8(const DecodeArgs &a, int log2M, uint32_t n_frames, hipStream_t s);
+uint32_t res8_records(uint32_t n_cu);
 bool decode_split_accepts(const DecodeArgs &a, int log2M);
 uint32_t split_group_symbols(uint32_t max_out);
 // the split decode's symbol groups, symbol ranges per (group, chunk) and EVM records per frame

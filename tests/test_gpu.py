@@ -578,20 +578,83 @@ def test_c3_4x4_mmse_2048_64qam_full_frame():
 
 
 def test_c4_8x8_mmse_4096_256qam_reduced_codes():
-    """C4 geometry with 2 access codes so the brute-force oracle stays within ~30 s. PID 12 is
-    below M/64, so this takes the per-symbol decode_kernel<12, 8>."""
+    """C4 geometry with 2 access codes so the brute-force oracle stays within ~30 s. PID 12:
+    the one-pass residue-class decode with fewer symbols than its 32 workgroup groups."""
     _c_frame_parity(4096, 304, 8, 2, 12, 256, _lib.DET_MMSE, 35.0, seed=41, bias=False,
-                    path=_lib.DECODE_SYMBOL)
+                    path=_lib.DECODE_RESIDUE)
 
 
-def test_c4_split_decode_matches_oracle():
-    """The production C4 decode: with max_out >= M/64 the 8x8 frame takes the split form
-    (spectra_kernel<12> writes every symbol's spectra, apply_split_kernel<8> applies W, demaps
-    and sums EVM per 64-subcarrier chunk; decode_stream.hip). PID 66 (not a multiple of the
-    apply's four symbols in flight, symbol ranges of 16/17) against the brute-force oracle
-    with 2 access codes: symbols within the EVM tolerance, indices, errors and EVM-dB."""
+def test_c4_residue_decode_matches_oracle():
+    """The production C4 decode: decode_res8_kernel (decode_stream.hip), eight workgroups per
+    symbol, each the 512-point transforms of one subcarrier residue class of all eight
+    antennas and the 8x8 apply of those subcarriers. PID 66 (22 groups of 3 symbols, EVM
+    records of every class) against the brute-force oracle with 2 access codes: symbols within
+    the EVM tolerance, indices, errors and EVM-dB."""
     _c_frame_parity(4096, 304, 8, 2, 66, 256, _lib.DET_MMSE, 35.0, seed=48, bias=False,
-                    path=_lib.DECODE_SPLIT, out_idx=True)
+                    path=_lib.DECODE_RESIDUE, out_idx=True)
+
+
+def test_c4_split_and_symbol_decodes_in_child():
+    """The two-pass split decode (spectra_kernel<12> + apply_split2_kernel<8>) and the
+    per-symbol decode_kernel<12, 8> remain behind RMIMO_DECODE_RES=0 (read once per process):
+    a child interpreter runs the C4 parity cases on them."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = ("import sys; sys.path.insert(0, %r); sys.path.insert(0, %r)\n"
+            "import test_gpu as t\nfrom rub_mimo_amd import _lib\n"
+            "t._c_frame_parity(4096, 304, 8, 2, 66, 256, _lib.DET_MMSE, 35.0, seed=48,"
+            " bias=False, path=_lib.DECODE_SPLIT, out_idx=True)\n"
+            "t._c_frame_parity(4096, 304, 8, 2, 12, 256, _lib.DET_MMSE, 35.0, seed=41,"
+            " bias=False, path=_lib.DECODE_SYMBOL)\nprint('split/symbol parity ok')\n"
+            % (root, os.path.join(root, "tests")))
+    env = dict(os.environ, RMIMO_DECODE_RES="0")
+    out = subprocess.run([sys.executable, "-c", code], env=env, cwd=root, timeout=110,
+                         capture_output=True, text=True)
+    assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-4000:]
+    assert "split/symbol parity ok" in out.stdout
+
+
+def test_c4_residue_batch_equals_single_frames():
+    """decode_res8_kernel on a batch: its workgroup groups' symbol ranges straddle frames
+    (3 frames x PID 67 over 32 groups), yet each frame's symbols and indices equal a
+    one-frame batch bit for bit; the indices are the hard decisions of the symbols and the
+    EVM / symbol-error sums equal a float64 recount (ref_mode 1)."""
+    import torch
+    M, cp, N, nac, pid, qam, F = 4096, 304, 8, 2, 67, 256, 3
+    sp = SynthParams(M=M, cp_len=cp, num_streams=N, num_access_codes=nac, pid=pid,
+                     qam_order=qam, seed=58, snr_db=35.0)
+    syn = Synthesizer(sp)
+    L = sp.max_frame_len()
+    iq = torch.empty((F, N, L), dtype=torch.complex64, device="cuda")
+    tx = torch.empty((F, N, pid, M), dtype=torch.uint8, device="cuda")
+    syn.generate(iq, L, L, F, frame_id0=0, tx_idx=tx)
+    P = RxParams(M=M, cp_len=cp, num_streams=N, num_access_codes=nac, pid_max=pid,
+                 detector=_lib.DET_MMSE, qam_order=qam, keep_identity_bias=False)
+    rx = Receiver(P)
+    sym = torch.zeros((F, N, pid, M), dtype=torch.complex64, device="cuda")
+    idx = torch.zeros((F, N, pid, M), dtype=torch.uint8, device="cuda")
+    rx.process(iq, L, L, F, max_out=pid, out_sym=sym, out_idx=idx, ref_mode=1, ref_idx=tx)
+    torch.cuda.synchronize()
+    assert rx.decode_path() == _lib.DECODE_RESIDUE
+    res = rx.results(F)
+    ok = [f for f in range(F) if res[f]["status"] == _lib.FRAME_OK]
+    assert len(ok) >= 1, [r["status"] for r in res]
+    for f in ok:
+        s1 = torch.zeros((1, N, pid, M), dtype=torch.complex64, device="cuda")
+        i1 = torch.zeros((1, N, pid, M), dtype=torch.uint8, device="cuda")
+        r1 = Receiver(P)
+        r1.process(iq[f:f + 1], L, L, 1, max_out=pid, out_sym=s1, out_idx=i1, ref_mode=1,
+                   ref_idx=tx[f:f + 1])
+        torch.cuda.synchronize()
+        assert torch.equal(s1[0], sym[f]) and torch.equal(i1[0], idx[f]), f
+        ys = sym[f].cpu().numpy()
+        dec, num, den, err = ref.demap_evm(ys.transpose(1, 0, 2), qam, tx[f].cpu().numpy())
+        assert np.array_equal(dec, idx[f].cpu().numpy()), f
+        r = res[f]
+        assert np.array_equal(r["errors"], err.astype(np.int64)), (r["errors"], err)
+        assert np.allclose(r["evm_num"], num, rtol=1e-4), (r["evm_num"], num)
+        assert np.allclose(r["evm_den"], den, rtol=1e-5), (r["evm_den"], den)
 
 
 @pytest.mark.parametrize("det", [_lib.DET_ZF, _lib.DET_MMSE])
@@ -970,7 +1033,7 @@ def test_cfo_folded_matches_oracle_and_is_frame_deterministic(tmp_path):
         idx = torch.zeros((F, N, pid, M), dtype=torch.uint8, device="cuda")
         rxo.process(rot, L, L, F, max_out=pid, out_sym=sym, out_idx=idx, ref_mode=1, ref_idx=tx)
         torch.cuda.synchronize()
-        assert rxo.decode_path() == DECODE_STREAM and rxo.cfo_mode() == 2
+        assert rxo.decode_path() == _lib.DECODE_STREAM and rxo.cfo_mode() == 2
         res = rxo.results(F)
         orc = _oracle_frames(tmp_path, list(rot.cpu().numpy()), M, cp, N, nac, pid, qam, 2)
         ok = 0
