@@ -632,6 +632,8 @@ void search_ls_wave_kernel(SearchArgs a) {
   constexpr bool LSREG = 2 * (M / 8) == T && LOG2M >= 9;
   if constexpr (LSREG) {
     using PM = RegPlan<LOG2M, 8>;
+    constexpr int PBX = reg_image_len<LOG2M, 8>();     // conflict-free exchange layouts
+    static_assert(2 * PBX <= lds_padded_len(F), "both LS images in the search's buffer");
     const uint32_t u = (uint32_t)tid / PM::T, lt = (uint32_t)tid % PM::T;   // u uniform per wave
     const bool valid = u ? valid1 : valid0;
     const int64_t wb = u ? w1v : w0;
@@ -655,7 +657,7 @@ void search_ls_wave_kernel(SearchArgs a) {
     v2f wm[PM::NTW > 0 ? PM::NTW : 1];
     reg_twiddles<LOG2M, 8>(wm, a.tw, (int)lt);
     reg_compute<LOG2M, 8, 0, false>(xw, wm);
-    reg_rest<LOG2M, 8, 1, false>(buf + u * PBM, xw, wm, (int)lt);
+    reg_rest_lay<LOG2M, 8, 1, false>(buf + u * PBX, xw, wm, (int)lt);
     if (!valid) return;                               // uniform per wave
     const uint32_t ac = s0 + u - 1, code = ac / a.N, tx = ac % a.N;
     const int8_t *sg = a.s1sign + ((size_t)tx * a.nac + code) * M;

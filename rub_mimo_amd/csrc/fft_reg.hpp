@@ -160,6 +160,104 @@ MIMO_DEV void reg_rest(v2f *buf, v2f *v, const v2f *w1, int tid) {
   }
 }
 
+// Exchange layouts of an 8-point-per-thread plan (PTS = 8, radix 8 first), one per exchange
+// (each is a store then a load, so each may place elements as it likes): with lds_pad the
+// radix-8 stores of the first two exchanges (elements 8 j + r, and 64 (j/8) + j%8 + 8 r) are
+// 2-way bank-conflicted on gfx950 (8-byte stores: 16-lane groups over 32 banks) -- 31% of
+// the LDS cycles of the search's 2048-point LS transform (tools/lds/). Both become
+// conflict-free:
+//   1 (after pass 0): i = 32 a + b at 33 a + (b ^ 4 ((b >> 4) & 1)) -- the store from two bases
+//     per thread (the XOR swaps r < 4 and r >= 4 where j & 2), the load j + r NB from one;
+//   2 (after pass 1, radix 8 over NS = 8): i + 2 (i >> 5) + 4 (i >> 6) -- x2(o + 8 r) =
+//     x2(o) + 8 r + 2 (r >> 2), x2(j + r NB) = x2(j) + 9 r NB / 8 (NB a multiple of 64);
+//     footprint N + N/8 (the image stride reg_image_len);
+//   0: lds_pad (later exchanges).
+template <int LOG2N, int PTS>
+constexpr int reg_ex_layout(int e) {
+  using PL = RegPlan<LOG2N, PTS>;
+  if (PTS != 8 || PL::RM != 8 || PL::radix(0) != 8) return 0;
+  if (e == 0) return (PL::N / PL::radix(1)) % 32 == 0 ? 1 : 0;
+  if (e == 1 && PL::NP > 2 && PL::radix(1) == 8 && PL::ns(1) == 8 &&
+      (PL::N / PL::radix(2)) % 64 == 0)
+    return 2;
+  return 0;
+}
+template <int LOG2N, int PTS>
+constexpr int reg_image_len() {   // entries per transform image of the layouts above
+  return (reg_ex_layout<LOG2N, PTS>(1) == 2) ? (1 << LOG2N) + (1 << LOG2N) / 8
+                                              : (1 << LOG2N) + (1 << LOG2N) / 32;
+}
+MIMO_DEV constexpr int reg_x2(int i) { return i + 2 * (i >> 5) + 4 * (i >> 6); }
+
+template <int LOG2N, int PTS, int P, int LAY>
+MIMO_DEV void reg_store_lay(v2f *buf, const v2f *v, int tid) {
+  using PL = RegPlan<LOG2N, PTS>;
+  constexpr int R = PL::radix(P);
+  if constexpr (LAY == 1) {
+    static_assert(P == 0 && R == 8 && PL::bt(P) == 1, "x1: pass 0, one radix-8 butterfly");
+    const int j = tid;
+    const int m = ((j >> 1) & 1) << 2;
+    const int B = 33 * (j >> 2) + 8 * (j & 3);
+    v2f *lo = buf + B + m, *hi = buf + B - m;
+#pragma unroll
+    for (int r = 0; r < 4; r++) lo[r] = v[r];
+#pragma unroll
+    for (int r = 4; r < 8; r++) hi[r] = v[r];
+  } else if constexpr (LAY == 2) {
+    static_assert(P == 1 && R == 8 && PL::ns(P) == 8 && PL::bt(P) == 1, "x2: pass 1, radix 8");
+    const int j = tid;
+    v2f *bp = buf + 64 * (j >> 3) + (j & 7) + 8 * (j >> 3);
+#pragma unroll
+    for (int r = 0; r < 8; r++) bp[8 * r + 2 * (r >> 2)] = v[r];
+  } else {
+    reg_store<LOG2N, PTS, P>(buf, v, tid);
+  }
+}
+
+template <int LOG2N, int PTS, int P, int LAY>
+MIMO_DEV void reg_load_lay(const v2f *buf, v2f *v, int tid) {
+  using PL = RegPlan<LOG2N, PTS>;
+  constexpr int R = PL::radix(P), NB = PL::N / R;
+  if constexpr (LAY == 1) {
+    static_assert(NB % 32 == 0, "x1 loads");
+#pragma unroll
+    for (int i = 0; i < PL::bt(P); i++) {
+      const int j = tid + i * PL::T;
+      const v2f *bp = buf + 33 * (j >> 5) + ((j & 31) ^ (((j >> 4) & 1) << 2));
+#pragma unroll
+      for (int r = 0; r < R; r++) v[i * R + r] = bp[33 * r * (NB / 32)];
+    }
+  } else if constexpr (LAY == 2) {
+    static_assert(NB % 64 == 0, "x2 loads");
+#pragma unroll
+    for (int i = 0; i < PL::bt(P); i++) {
+      const int j = tid + i * PL::T;
+      const v2f *bp = buf + reg_x2(j);
+#pragma unroll
+      for (int r = 0; r < R; r++) v[i * R + r] = bp[9 * r * (NB / 8)];
+    }
+  } else {
+    reg_load<LOG2N, PTS, P>(buf, v, tid);
+  }
+}
+
+// reg_rest with the exchange layouts above (images of reg_image_len entries)
+template <int LOG2N, int PTS, int P, bool INV>
+MIMO_DEV void reg_rest_lay(v2f *buf, v2f *v, const v2f *w1, int tid) {
+  using PL = RegPlan<LOG2N, PTS>;
+  if constexpr (P < PL::NP) {
+    int t = tid;
+    asm volatile("" : "+v"(t));
+    constexpr int LAY = reg_ex_layout<LOG2N, PTS>(P - 1);
+    __syncthreads();
+    reg_store_lay<LOG2N, PTS, P - 1, LAY>(buf, v, t);
+    __syncthreads();
+    reg_load_lay<LOG2N, PTS, P, LAY>(buf, v, t);
+    reg_compute<LOG2N, PTS, P, INV>(v, w1);
+    reg_rest_lay<LOG2N, PTS, P + 1, INV>(buf, v, w1, tid);
+  }
+}
+
 // LDS writes of this wave visible to its own reads; no code motion across
 MIMO_DEV void wave_lds_sync() {
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
