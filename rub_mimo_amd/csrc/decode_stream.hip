@@ -377,26 +377,6 @@ MIMO_DEV void dma16(uint32_t voff, __attribute__((address_space(1))) const void 
                : "=&s"(keep) : "v"(voff), "s"(sbase), "s"(lds) : "memory");
 }
 
-// a wave-uniform global pointer held in SGPRs (address arithmetic feeding it may sit in
-// VGPRs); global address space, so accesses through it are global_* with an SGPR base and a
-// 32-bit lane offset, not flat_* (flat stores also count on lgkmcnt: every LDS wait would
-// drain them)
-MIMO_DEV uint64_t rfl64(uint64_t v) {   // a uniform 64-bit value, held in SGPRs
-  return (uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)v) |
-         ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32)) << 32);
-}
-
-template <typename P>
-using gptr = __attribute__((address_space(1))) P *;
-typedef float v4f __attribute__((ext_vector_type(4)));
-template <typename P>
-MIMO_DEV gptr<P> sgpr_ptr(P *p) {
-  const uint64_t v = (uint64_t)p;
-  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
-  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
-  return (gptr<P>)(((uint64_t)hi << 32) | lo);
-}
-
 constexpr size_t kStreamStaticLds = 8192;   // pfx, fbody, fcr, ptab, gidx, cpe_part, cfo_tab (+ slack)
 
 // dynamic LDS of the kernel: FFT images, staging, reference staging, twiddle table

@@ -638,12 +638,21 @@ void search_ls_wave_kernel(SearchArgs a) {
     const bool valid = u ? valid1 : valid0;
     const int64_t wb = u ? w1v : w0;
     v2f xw[8];
+    if (valid && wb >= 0 && wb + M <= L) {            // uniform per wave: one row base
+      const auto xr = xs.row((uint64_t)wb);
 #pragma unroll
-    for (int e = 0; e < 8; e++) {
-      const int64_t n = wb + reg_index<LOG2M, 8>((int)lt, e);
-      const bool ok = valid && n >= 0 && n < L;
-      const float2 t = xs.at(n < 0 ? 0 : (n >= L ? L - 1 : n));
-      xw[e] = ok ? v2f{t.x, t.y} : v2f{0.0f, 0.0f};
+      for (int e = 0; e < 8; e++) {
+        const float2 t = xr.at(reg_index<LOG2M, 8>((int)lt, e));
+        xw[e] = v2f{t.x, t.y};
+      }
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; e++) {
+        const int64_t n = wb + reg_index<LOG2M, 8>((int)lt, e);
+        const bool ok = valid && n >= 0 && n < L;
+        const float2 t = xs.at(n < 0 ? 0 : (n >= L ? L - 1 : n));
+        xw[e] = ok ? v2f{t.x, t.y} : v2f{0.0f, 0.0f};
+      }
     }
     if constexpr (CFO) {   // window sample lt + e M/8, relative to base: wb - base + ...
       v2f rb = phasor_cycles(nu * (double)(wb - I.base + (int64_t)lt));
@@ -660,14 +669,16 @@ void search_ls_wave_kernel(SearchArgs a) {
     reg_rest_lay<LOG2M, 8, 1, false>(buf + u * PBX, xw, wm, (int)lt);
     if (!valid) return;                               // uniform per wave
     const uint32_t ac = s0 + u - 1, code = ac / a.N, tx = ac % a.N;
-    const int8_t *sg = a.s1sign + ((size_t)tx * a.nac + code) * M;
-    float2 *q = a.lsq + ((((uint64_t)f * a.N + r) * a.N + tx) * a.nac + code) * M;
+    // (code row bases uniform per wave: SGPR pointers, 32-bit lane offsets; X S1 as a product
+    // with the sign: exact for +-1, and a null subcarrier's 0 term is dropped by the combine)
+    const auto sg = sgpr_ptr(a.s1sign + ((size_t)tx * a.nac + code) * M);
+    const auto q = sgpr_ptr(reinterpret_cast<v2f *>(a.lsq) +
+                            ((((uint64_t)f * a.N + r) * a.N + tx) * a.nac + code) * M);
 #pragma unroll
     for (int e = 0; e < 8; e++) {
-      const int k = reg_index<LOG2M, 8>((int)lt, e);
-      const int sgn = sg[k];
-      const float2 Xk = make_float2(xw[e].x, xw[e].y);
-      q[k] = sgn > 0 ? Xk : (sgn < 0 ? cneg(Xk) : make_float2(0.0f, 0.0f));
+      const uint32_t k = (uint32_t)reg_index<LOG2M, 8>((int)lt, e);
+      const float sgn = (float)sg[k];
+      q[k] = xw[e] * v2f{sgn, sgn};
     }
     return;
   } else {

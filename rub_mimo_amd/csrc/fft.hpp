@@ -27,6 +27,27 @@ typedef float v2f __attribute__((ext_vector_type(2)));
 // The same operations as single VOP3P instructions with the swizzle and the sign folded into
 // op_sel / neg modifiers (the compiler materialises {-b.y, b.x} with a v_xor and a v_mov
 // first). Results are bitwise those of vmul / rot_mi forms above.
+// a wave-uniform global pointer held in SGPRs (address arithmetic feeding it may sit in
+// VGPRs); global address space, so accesses through it are global_* with an SGPR base and a
+// 32-bit lane offset, not flat_* (flat stores also count on lgkmcnt: every LDS wait would
+// drain them)
+MIMO_DEV uint64_t rfl64(uint64_t v) {   // a uniform 64-bit value, held in SGPRs
+  return (uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)v) |
+         ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32)) << 32);
+}
+
+template <typename P>
+using gptr = __attribute__((address_space(1))) P *;
+typedef float v4f __attribute__((ext_vector_type(4)));
+template <typename P>
+MIMO_DEV gptr<P> sgpr_ptr(P *p) {
+  const uint64_t v = (uint64_t)p;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+  return (gptr<P>)(((uint64_t)hi << 32) | lo);
+}
+
+
 MIMO_DEV v2f cmul_pk(v2f a, v2f b) {     // a * b: (a.x b.x - a.y b.y, a.x b.y + a.y b.x)
   v2f r;
   // one asm block: the compiler pads between separate inline-asm VALU blocks with s_nop
