@@ -1608,10 +1608,14 @@ void sc_exact_kernel(ScArgs a) {
   }
   const int64_t ib_lo = w0 + (int64_t)it_lo * kScIt;
   if (active) {
-  // the first block's loads, then the history [ib_lo - M, ib_lo) -> its ring slots: both in
-  // flight together (the window sums below wait for the history only)
-  float4 pre[kScIt / (2 * kScT)];
+  // the first two blocks' loads, then the history [ib_lo - M, ib_lo) -> its ring slots: all in
+  // flight together (the window sums below wait for the history only). Block it_lo + j goes
+  // through register set j & 1 (pre, pre2): each iteration refills the set it consumed two
+  // blocks ahead, so an iteration's ring fill no longer waits one memory latency on the load
+  // the previous iteration issued (the second iteration of a pass did, ~5 us)
+  float4 pre[kScIt / (2 * kScT)], pre2[kScIt / (2 * kScT)];
   bool pf = fetch_block(pre, x, ib_lo, L, vec);
+  bool pf2 = it_hi > it_lo ? fetch_block(pre2, x, ib_lo + kScIt, L, vec) : false;
   const int wb = (kScIt * it_lo) % RING;
   if (vec && ib_lo - M >= 0 && ib_lo <= L) {
     // all history pairs in flight together, then the ring writes
@@ -1675,15 +1679,25 @@ void sc_exact_kernel(ScArgs a) {
   for (int it = it_lo; it <= it_hi; it++) {
     const int64_t ib = w0 + (int64_t)it * kScIt;
     const unsigned long long tq0 = a.prof ? (unsigned long long)wall_clock64() : 0ull;
-    const bool pf_used = pf;
+    const bool odd = ((it - it_lo) & 1) != 0;                  // uniform: register set
+    const bool pf_used = odd ? pf2 : pf;
     {
       const int sl0 = (M + it * kScIt) % RING + 2 * tid;
-      if (pf) {
+      if (pf_used) {
+        if (odd) {
 #pragma unroll
-        for (int j = 0; j < kScIt / (2 * kScT); j++) {
-          int sl = sl0 + 2 * kScT * j;
-          if (sl >= RING) sl -= RING;
-          *reinterpret_cast<float4 *>(ring + ring_pad(sl)) = pre[j];
+          for (int j = 0; j < kScIt / (2 * kScT); j++) {
+            int sl = sl0 + 2 * kScT * j;
+            if (sl >= RING) sl -= RING;
+            *reinterpret_cast<float4 *>(ring + ring_pad(sl)) = pre2[j];
+          }
+        } else {
+#pragma unroll
+          for (int j = 0; j < kScIt / (2 * kScT); j++) {
+            int sl = sl0 + 2 * kScT * j;
+            if (sl >= RING) sl -= RING;
+            *reinterpret_cast<float4 *>(ring + ring_pad(sl)) = pre[j];
+          }
         }
       } else {   // frame edges: guarded loads straight into the ring
 #pragma unroll 1
@@ -1697,7 +1711,10 @@ void sc_exact_kernel(ScArgs a) {
     }
     __syncthreads();
     const unsigned long long tq1 = a.prof ? (unsigned long long)wall_clock64() : 0ull;
-    if (it + 1 <= it_hi) pf = fetch_block(pre, x, ib + kScIt, L, vec);
+    if (it + 2 <= it_hi) {                        // two blocks ahead, into the set just used
+      if (odd) pf2 = fetch_block(pre2, x, ib + 2 * kScIt, L, vec);
+      else pf = fetch_block(pre, x, ib + 2 * kScIt, L, vec);
+    }
     const float2 *xn = ring + ring_pad((M + it * kScIt + kScS * tid) % RING);
     const float2 *xr = ring + ring_pad((RL + it * kScIt + kScS * tid) % RING);
     const float2 *xm = ring + ring_pad((it * kScIt + kScS * tid) % RING);
