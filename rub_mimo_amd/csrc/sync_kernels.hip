@@ -649,7 +649,7 @@ __global__ __launch_bounds__(kScT) __attribute__((amdgpu_waves_per_eu(2))) void 
   __shared__ long long s_lo[kMaxStreams];
   __shared__ unsigned long long s_smin, s_smax;
 
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int tid = threadIdx.x;
   const int64_t L = (int64_t)a.frame_len, cp = a.cp;
   const int64_t K = (int64_t)a.chunk_len, H = (int64_t)kScSpan - K;
   const uint64_t total = (a.chunk_hi - a.chunk_lo) * n_frames;
@@ -683,7 +683,6 @@ __global__ __launch_bounds__(kScT) __attribute__((amdgpu_waves_per_eu(2))) void 
     SC_PROF(const long long w_item = wall_clock64();)
     SC_PROF(long long t_rows = 0, t_words = 0, t_ph[5] = {0, 0, 0, 0, 0};)
     const int64_t w0 = c0 - H;                 // first evaluated position
-    const int64_t org = w0 - M;                // ring slot 0 at the start of the item
     const int64_t cend = std::min<int64_t>(c0 + K, L);
     int any = 1;
     uint32_t n_done = 0;
@@ -1387,15 +1386,36 @@ __global__ __launch_bounds__(64) void stream_fixup_kernel(PlateauArgs a) {
 // ======================================================================================
 
 // one step of the transposing butterfly: of v[0 .. N) a lane keeps the half selected by its
-// lane bit OFF and adds the partner's copy of that half (compile-time indices throughout)
+// lane bit OFF and adds the partner's copy of that half (compile-time indices throughout), with
+// no LDS traffic. Offsets 32 and 16 pair lanes l and l ^ OFF through v_permlane32/16_swap: one
+// swap of (v[i], v[i + N/2]) leaves a lane its own kept value and the partner's copy of it, so
+// the kept sum is the two results added. Offsets 8 and 4 pair lanes through DPP row_mirror
+// (l <-> 15 - l in a row) and row_half_mirror (l <-> 7 - l in 8), which flip the same lane bit:
+// a lane then holds the sum over lanes l ^ {0, 7, 8, 15} of every row, and the quad sums that
+// follow (l ^ {0, 1, 2, 3}) cover each of the 64 lanes once.
+template <int CTRL>
+MIMO_DEV float dpp_mov(float x) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), CTRL, 0xf, 0xf, false));
+}
 template <int OFF, int N>
 MIMO_DEV void tr_reduce_step(float *v, int lane) {
-  const bool up = (lane & OFF) != 0;
+  static_assert(OFF == 32 || OFF == 16 || OFF == 8 || OFF == 4, "lane bits 5..2");
+  if constexpr (OFF >= 16) {
 #pragma unroll
-  for (int i = 0; i < N / 2; i++) {
-    const float send = up ? v[i] : v[i + N / 2];
-    const float keep = up ? v[i + N / 2] : v[i];
-    v[i] = keep + __shfl_xor(send, OFF);
+    for (int i = 0; i < N / 2; i++) {
+      const uint32_t a = __float_as_uint(v[i]), b = __float_as_uint(v[i + N / 2]);
+      const auto r = OFF == 32 ? __builtin_amdgcn_permlane32_swap(a, b, false, false)
+                               : __builtin_amdgcn_permlane16_swap(a, b, false, false);
+      v[i] = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+    }
+  } else {
+    const bool up = (lane & OFF) != 0;
+#pragma unroll
+    for (int i = 0; i < N / 2; i++) {
+      const float send = up ? v[i] : v[i + N / 2];
+      const float keep = up ? v[i + N / 2] : v[i];
+      v[i] = keep + dpp_mov<OFF == 8 ? 0x140 : 0x141>(send);   // row_mirror / row_half_mirror
+    }
   }
 }
 
@@ -1441,7 +1461,7 @@ __global__ __launch_bounds__(kScrT) __attribute__((amdgpu_waves_per_eu(6))) void
     // per-lane partials v[4 b + c] (c: Re P, Im P, |x|^2, |Re p| + |Im p|), then a transposing
     // butterfly: at offsets 32, 16, 8, 4 a lane keeps half of its values and adds the
     // partner's copy of them (8 + 4 + 2 + 1 exchanges for 16 sums instead of 16 x 6); lanes
-    // then hold value (lane >> 2) summed over their 16-lane group, and offsets 2, 1 finish it
+    // then hold value (lane >> 2) summed over 16 lanes, and the quad sums finish it
     float v[4 * kScrBPI];
 #pragma unroll
     for (int b = 0; b < kScrBPI; b++) {
@@ -1459,8 +1479,8 @@ __global__ __launch_bounds__(kScrT) __attribute__((amdgpu_waves_per_eu(6))) void
     tr_reduce_step<8, 4>(v, lane);
     tr_reduce_step<4, 2>(v, lane);
     float tot = v[0];
-    tot += __shfl_xor(tot, 2);
-    tot += __shfl_xor(tot, 1);
+    tot += dpp_mov<0x4E>(tot);   // quad_perm [2, 3, 0, 1]: lane ^ 2
+    tot += dpp_mov<0xB1>(tot);   // quad_perm [1, 0, 3, 2]: lane ^ 1
     {
       const int q = lane >> 2, b = q >> 2, c = q & 3;   // value q = 4 b + c
       if ((lane & 3) == 0 && j0 + b < NB) reinterpret_cast<float *>(&recs[j0 + b])[c] = tot;
