@@ -1029,11 +1029,10 @@ static int maybe_trim(mimo_rx *h) {
   const uint64_t need = H + 2 * (uint64_t)h->SL + 2 * (uint64_t)h->M + K;
   if (c_lo * K < need + K) return MIMO_OK;            // nothing to drop yet
   const uint64_t D = (c_lo * K - need) / K * K;
-  const uint64_t keep = h->total - D;
-  // high-water mark: only once the droppable prefix is at least as long as the kept tail, so a
-  // probe (and its host round trip) comes once per that many samples of stream, and the tail
-  // moves in one copy whose source and destination do not overlap
-  if (D < keep) return MIMO_OK;
+  // high-water mark: only once the droppable prefix reaches half a window (pieces are half a
+  // window too), so a probe and its host round trip come once per half window of stream, not
+  // once per S&C chunk, and the capture stays within about a window plus the S&C reach
+  if (D < std::max<uint64_t>(K, h->win_len / 2)) return MIMO_OK;
   const int64_t lo = (int64_t)(D + h->SL + h->M), hi = (int64_t)(c_lo * K - H);
   if (hi - lo < (int64_t)K / 2) return MIMO_OK;
   // the probe's span moves only when the S&C reaches a new chunk: a caller feeding small pieces
@@ -1050,10 +1049,15 @@ static int maybe_trim(mimo_rx *h) {
   HIPCHK(hipStreamSynchronize(h->stream));
   for (uint32_t a = 0; a < h->N; a++)
     if (!ok[a]) return MIMO_OK;                       // a run may reach back: keep everything
-  // move [D, total) to the front (D >= keep: disjoint ranges)
-  HIPCHK(hipMemcpy2DAsync(h->capbuf.p, sizeof(float2) * h->cap_len, h->capbuf.p + D,
-                          sizeof(float2) * h->cap_len, sizeof(float2) * keep, h->N,
-                          hipMemcpyDeviceToDevice, h->stream));
+  // move [D, total) to the front in pieces of D samples (each piece's source is read before
+  // any later piece writes over it: copies on one stream run in order; one piece when D >= keep)
+  const uint64_t keep = h->total - D;
+  for (uint64_t o = 0; o < keep; o += D) {
+    const uint64_t m = std::min<uint64_t>(D, keep - o);
+    HIPCHK(hipMemcpy2DAsync(h->capbuf.p + o, sizeof(float2) * h->cap_len,
+                            h->capbuf.p + D + o, sizeof(float2) * h->cap_len,
+                            sizeof(float2) * m, h->N, hipMemcpyDeviceToDevice, h->stream));
+  }
   h->origin += D;
   h->total = keep;
   return MIMO_OK;
