@@ -251,7 +251,7 @@ struct mimo_rx {
   // the stream since construction/reset (positions inside it are capture-relative).
   DevBuf<float2> capbuf;
   uint64_t cap_len = 0, total = 0, origin = 0;
-  uint64_t trim_clo = ~0ull;   // the S&C chunk position of the last trim probe (maybe_trim)
+  uint64_t trim_clo = ~0ull;   // stream position of the S&C chunk of the last trim probe
   DevBuf<uint32_t> probe;               // trim probe: per antenna, a proven metric zero
   // DEBUG_LOG files of the streaming execute (framing.cc:390-402, 598-600, 675-696, 873-883)
   std::string dbg_dir;
@@ -1036,9 +1036,11 @@ static int maybe_trim(mimo_rx *h) {
   const int64_t lo = (int64_t)(D + h->SL + h->M), hi = (int64_t)(c_lo * K - H);
   if (hi - lo < (int64_t)K / 2) return MIMO_OK;
   // the probe's span moves only when the S&C reaches a new chunk: a caller feeding small pieces
-  // pays one probe (and its host round trip) per chunk of stream, not one per call
-  if (c_lo == h->trim_clo) return MIMO_OK;
-  h->trim_clo = c_lo;
+  // pays one probe (and its host round trip) per chunk of stream, not one per call. (The stream
+  // position of that chunk, not its capture-relative index: a trim re-bases the capture.)
+  const uint64_t c_abs = h->origin + c_lo * K;
+  if (c_abs == h->trim_clo) return MIMO_OK;
+  h->trim_clo = c_abs;
   HIPCHK(h->probe.ensure(h->N));
   hipLaunchKernelGGL(trim_probe_kernel, dim3(h->N), dim3(64), 0, h->stream, h->capbuf.p,
                      h->cap_len, h->M, lo, hi, h->thr, sc_band(h->M), h->probe.p);
