@@ -106,7 +106,9 @@ inline std::vector<unsigned char> draw_s1(std::vector<msequence> const &ms, unsi
 class framegen {
  private:
   mimo_tx *h_ = nullptr;
-  unsigned int M, cp_len, symbol_len, num_streams, num_access_codes;
+  unsigned int M, cp_len;
+  [[maybe_unused]] unsigned int symbol_len;   // the reference's member (M + cp_len)
+  unsigned int num_streams, num_access_codes;
   std::vector<unsigned char> p;
   unsigned int M_null = 0, M_pilot = 0, M_data = 0;
 
@@ -172,7 +174,9 @@ class framegen {
 class framesync {
  private:
   mimo_rx *h_ = nullptr;
-  unsigned int M, cp_len, symbol_len, num_streams, num_access_codes;
+  unsigned int M, cp_len;
+  [[maybe_unused]] unsigned int symbol_len;   // the reference's member (M + cp_len)
+  unsigned int num_streams, num_access_codes;
   std::vector<unsigned char> p;
   unsigned int M_null = 0, M_pilot = 0, M_data = 0, M_occupied = 0;
   mimo_callback callback;

@@ -428,7 +428,7 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
   constexpr int SB = SC16 ? 4 : 8;                // bytes per staged sample
   constexpr int RS = M + SPC;
   constexpr int NBLK = (RS / SPC + 63) / 64;      // wave DMA instructions per staged row
-  constexpr int NWI = (NA * NBLK + T / 64 - 1) / (T / 64);   // ... per wave and symbol
+  [[maybe_unused]] constexpr int NWI = (NA * NBLK + T / 64 - 1) / (T / 64);   // ... per wave and symbol
   constexpr int LASTC = RS / SPC - (NBLK - 1) * 64;          // chunks in a row's last block
   static_assert(RS % SPC == 0 && LASTC >= 1 && LASTC <= 64 && 64 * SPC * SB == 1024,
                 "row DMA blocks of 1 KB");
@@ -555,8 +555,7 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
     const int64_t b0 = fbody[ff];
     const uint32_t cr = __builtin_amdgcn_readfirstlane(fcr[ff]);
     FrameBase fb;
-    fb.body = (int64_t)((((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)b0)) |
-                         ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)((uint64_t)b0 >> 32)) << 32)));
+    fb.body = (int64_t)rfl64((uint64_t)b0);
     fb.row0 = (int64_t)(cr & 0xFFFFu) * NA * (int64_t)a.stride;
     fb.ref = (uint64_t)(cr >> 16) * NA * a.max_out * a.M_occ;
     return fb;
@@ -813,6 +812,7 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
       // times the in-body part)
       if (a.cpe == 2) {
         v2f c = cmul_pk(cfo_tab[(opq(tid) % W8) % CTN], cfo_rot(s));
+
         if constexpr (W8 > CTN) c = cmul_pk(c, cfo_hi);
 #pragma unroll
         for (int r = 0; r < 8; r++) {

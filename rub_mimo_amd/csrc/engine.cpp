@@ -686,6 +686,15 @@ int run_decode(mimo_rx *h, const float2 *iq, uint64_t stride, uint32_t F, uint64
   h->timer.end(5, e, s);
   h->last_decode_path = path;
   h->last_cfo_mode = !h->cfo ? 0 : (path == MIMO_DECODE_STREAM && decode_stream_cpe(d) ? 2 : 1);
+  static const bool cfo_dbg = [] { const char *e = getenv("RMIMO_CFO_DEBUG"); return e && e[0] == '1'; }();
+  if (cfo_dbg && h->cfo) {   // diagnostics: the per-frame CFO state the decode read
+    std::vector<FrameInfo> fi(F);
+    HIPCHK(hipMemcpyAsync(fi.data(), h->info.p, sizeof(FrameInfo) * F, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    for (uint32_t f = 0; f < F; f++)
+      fprintf(stderr, "cfo_dbg f %u status %d base %lld i0 %u eps %.9f E %lld\n", f, (int)fi[f].status,
+              (long long)fi[f].base, fi[f].i0, (double)fi[f].cfo_eps, (long long)fi[f].cfo_E);
+  }
   if (!parts)   // run_batch widens every sc16 batch the streaming decode does not take
     return fail(MIMO_ERR_UNSUPPORTED, "no decode kernel takes this configuration");
   if (dprof) {   // diagnostics: per-item cycle split of the decode kernel

@@ -32,8 +32,11 @@ typedef float v2f __attribute__((ext_vector_type(2)));
 // 32-bit lane offset, not flat_* (flat stores also count on lgkmcnt: every LDS wait would
 // drain them)
 MIMO_DEV uint64_t rfl64(uint64_t v) {   // a uniform 64-bit value, held in SGPRs
-  return (uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)v) |
-         ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32)) << 32);
+  // (the builtin returns int: each half goes through uint32_t, or a low half with bit 31 set
+  // would sign-extend over the high half)
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)v);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+  return (uint64_t)lo | ((uint64_t)hi << 32);
 }
 
 template <typename P>
