@@ -460,6 +460,12 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
   __shared__ v2f cpe_part[CPE ? T / 64 : 1];                       // per-wave phase sums
   constexpr int CTN = W8 < 256 ? W8 : 256;
   __shared__ v2f cfo_tab[CPE ? CTN : 1];                           // folded CFO, in-body phasors
+  struct CfoState {
+    uint64_t E, j0;   // nu 2^64 (two's complement), i0 + cp: symbol 0's body
+    v2f w, rot;       // exp(-j2pi nu W8), the next symbol's body-start phasor
+  };
+  __shared__ CfoState cfo_st_s[1];
+  CfoState *cfo_st = cfo_st_s;
   const int tid = threadIdx.x;
   const uint32_t wv = __builtin_amdgcn_readfirstlane((uint32_t)tid >> 6);
   for (uint32_t e = tid; e < a.qam.L * a.qam.L; e += T) {
@@ -633,19 +639,32 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
         }
       }
     }
+    return odds;
+  };
+  // the reference indices of symbol (fb, ss) into rstg ([NA][M] bytes), by waves RW0 .. RW0 +
+  // NREF/64 - 1 (with DS_ROW_DMA the waves after the row waves, which stage no samples): issued
+  // after a symbol's top barrier (every wave is done with the previous symbol's), waited for
+  // by those waves before the barrier that precedes the apply, and read there straight from
+  // LDS -- the indices are not carried in registers through the transform
+  constexpr int RW0 = (WPR && NA * WPR + NREF / 64 <= T / 64) ? NA * WPR : 0;
+  static_assert(NREF % 64 == 0 && RW0 + NREF / 64 <= T / 64, "reference DMA waves");
+  const bool ref_wave = REF == 1 && wv >= (uint32_t)RW0 && wv < (uint32_t)(RW0 + NREF / 64);
+  auto fetch_ref = [&](const FrameBase &fb, uint32_t ss) {
     if constexpr (REF == 1) {
-      // (waves RW0 .. RW0 + NREF/64 - 1: with DS_ROW_DMA the waves after the row waves)
-      constexpr int RW0 = (WPR && NA * WPR + NREF / 64 <= T / 64) ? NA * WPR : 0;
-      static_assert(NREF % 64 == 0 && RW0 + NREF / 64 <= T / 64, "reference DMA waves");
-      const int tr = t0 - RW0 * 64;
-      if (tr >= 0 && tr < NREF) {
+      if (ref_wave) {
+        const int tr = opq(tid) - RW0 * 64;
         const uint32_t dst = __builtin_amdgcn_readfirstlane(rstg_base + (uint32_t)((wv - RW0) * 64) * 16u);
         const uint32_t t = (uint32_t)tr / (M / 16), q = (uint32_t)tr % (M / 16);
         const auto rb = sgpr_ptr(a.ref_idx + fb.ref + (uint64_t)ss * a.M_occ);
         dma16(t * (uint32_t)(a.max_out * a.M_occ) + 16 * q, rb, dst);
       }
     }
-    return odds;
+  };
+  // ... and the wait (the reference waves' only loads in flight: with RW0 = 0 they also stage
+  // samples, whose DMA this waits for as well)
+  auto wait_ref = [&]() {
+    if constexpr (REF == 1)
+      if (ref_wave) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   };
 
   // this frame's weights * gain * dn for the thread's subcarriers k = tid + q T
@@ -716,10 +735,19 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
   // (the thread's in-body phasor exp(-j2pi nu t0%W8) comes from an LDS table of the frame,
   // cfo_tab[n] = exp(-j2pi nu n) for n < CTN, times a wave-uniform exp(-j2pi nu CTN hi) when
   // W8 > CTN)
+  // (the frame's E, i0 + cp, exp(-j2pi nu W8) and the next symbol's body-start phasor live in
+  // LDS, written by thread 0: registers are the scarce resource of this kernel. The phasor of
+  // symbol s is formed at the tail of symbol s - 1 (or at the start) and read at pass 0 of
+  // symbol s; pass 0 ends at a barrier every wave passes before thread 0 reaches the tail, so
+  // one slot serves)
   v2f cfo_hi = v2f{1.0f, 0.0f};
-  v2f cfo_w = v2f{1.0f, 0.0f};                              // exp(-j2pi nu W8)
-  uint64_t cfo_E = 0;                                       // nu 2^64 (two's complement)
-  uint64_t cfo_j0 = 0;                                      // i0 + cp: symbol 0's body
+  auto cfo_ph = [](double cyc) {
+    double p = -2.0 * cyc;
+    p -= 2.0 * rint(p * 0.5);
+    float sn, cs;
+    sincospif((float)p, &sn, &cs);
+    return v2f{cs, sn};
+  };
   auto cfo_frame = [&](uint32_t ff) {
     if constexpr (CPE) {
       if (a.cpe == 2) {
@@ -728,33 +756,33 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
         const FrameInfo &J = a.info[ff];
         const int64_t e64 = J.cfo_E;
         const double nu = ldexp((double)e64, -64);
-        auto ph = [](double cyc) {
-          double p = -2.0 * cyc;
-          p -= 2.0 * rint(p * 0.5);
-          float sn, cs;
-          sincospif((float)p, &sn, &cs);
-          return v2f{cs, sn};
-        };
         // (every reader of the previous frame's table passed this symbol's barriers; the next
         // top barrier publishes the new one)
-        for (int e = tid; e < CTN; e += T) cfo_tab[e] = ph(nu * (double)e);
-        if constexpr (W8 > CTN) cfo_hi = uni(ph(nu * (double)((opq(tid) % W8) / CTN * CTN)));
-        cfo_w = uni(ph(nu * (double)W8));
-        cfo_E = rfl64((uint64_t)e64);
-        cfo_j0 = rfl64((uint64_t)J.i0 + a.cp);
+        for (int e = tid; e < CTN; e += T) cfo_tab[e] = cfo_ph(nu * (double)e);
+        if constexpr (W8 > CTN) cfo_hi = uni(cfo_ph(nu * (double)((opq(tid) % W8) / CTN * CTN)));
+        if (tid == 0) {
+          cfo_st->E = (uint64_t)e64;
+          cfo_st->j0 = (uint64_t)J.i0 + a.cp;
+          cfo_st->w = cfo_ph(nu * (double)W8);
+        }
       }
     }
   };
-  // the body start's phasor of symbol ss of the current frame
-  auto cfo_rot = [&](uint32_t ss) -> v2f {
-    const uint64_t P = cfo_E * (cfo_j0 + (uint64_t)ss * a.SL);   // turns x 2^64, wrapped
-    const float turns = (float)(int32_t)(uint32_t)(P >> 32) * 0x1p-32f;   // [-1/2, 1/2)
-    float sn, cs;
-    sincospif(-2.0f * turns, &sn, &cs);
-    return uni(v2f{cs, sn});
+  // thread 0: the body-start phasor of symbol ss of the current frame into LDS
+  auto cfo_next = [&](uint32_t ss) {
+    if constexpr (CPE) {
+      if (a.cpe == 2 && tid == 0) {
+        const uint64_t P = cfo_st->E * (cfo_st->j0 + (uint64_t)ss * a.SL);   // turns x 2^64, wrapped
+        const float turns = (float)(int32_t)(uint32_t)(P >> 32) * 0x1p-32f;   // [-1/2, 1/2)
+        float sn, cs;
+        sincospif(-2.0f * turns, &sn, &cs);
+        cfo_st->rot = v2f{cs, sn};
+      }
+    }
   };
   load_w(f);
   cfo_frame(f);
+  cfo_next(s);
   FrameBase fbase = frame_base(f);
   uint32_t odd = fetch(fbase, s);
   // the first symbol's staging (issued after the weight loads: the counted wait in the loop
@@ -786,34 +814,14 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
         for (int r = 0; r < 8; r++) v[r] = x[r * W8];
       }
     }
-    uint32_t cref[(NA * S + 3) / 4];                  // reference indices, byte (t S + q)
-    if constexpr (REF == 1) {
-      const int t0 = opq(tid);
-#pragma unroll
-      for (int w = 0; w < (NA * S + 3) / 4; w++) cref[w] = 0;
-      if constexpr (KADJ) {   // the thread's S = 2 bytes of stream t are adjacent
-#pragma unroll
-        for (int t = 0; t < NA; t++) {
-          const int e = t * S;
-          cref[e / 4] |= (uint32_t)reinterpret_cast<const uint16_t *>(rstg + t * M)[t0] << (8 * (e % 4));
-        }
-      } else {
-#pragma unroll
-        for (int t = 0; t < NA; t++)
-#pragma unroll
-          for (int q = 0; q < S; q++) {
-            const int e = t * S + q;
-            cref[e / 4] |= (uint32_t)rstg[t * M + t0 + q * T] << (8 * (e % 4));
-          }
-      }
-    }
+    fetch_ref(fbase, s);
     if constexpr (CPE) {
       // folded CFO: the symbol's derotation on its time samples (the body start's phasor
       // times the in-body part)
       if (a.cpe == 2) {
-        v2f c = cmul_pk(cfo_tab[(opq(tid) % W8) % CTN], cfo_rot(s));
-
+        v2f c = cmul_pk(cfo_tab[(opq(tid) % W8) % CTN], cfo_st->rot);
         if constexpr (W8 > CTN) c = cmul_pk(c, cfo_hi);
+        const v2f cfo_w = cfo_st->w;                  // exp(-j2pi nu W8)
 #pragma unroll
         for (int r = 0; r < 8; r++) {
           v[r] = cmul_pk(v[r], c);
@@ -875,6 +883,7 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
         dft_fwd_pk<8>(v);
         wave_passes<LOG2M - 3, 1, WP::PADK>(rg, v, twl + WP::TW0, s);
       }
+      wait_ref();
       __syncthreads();                                // every spectrum in its region
     } else {
       st_store<LOG2M, NA, 0, 0, ex_layout<PL::NP>(0)>(img, v, (uint32_t)opq(tid));
@@ -884,9 +893,11 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
         const uint32_t t = (uint32_t)opq(tid);
         __syncthreads();
         st_store<LOG2M, NA, PL::NP - 1>(img, v, t);
+        wait_ref();
         __syncthreads();
       }
 #else
+      wait_ref();
       __syncthreads();
 #endif
     }
@@ -911,7 +922,7 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
 #endif
       const uint32_t d = gidx[qam_level_pair_pk(acc, inv_sc, Lf, Lm1, a.qam.L)];
       uint32_t refi;
-      if constexpr (REF == 1) refi = (cref[(t * S + q) / 4] >> (8 * ((t * S + q) % 4))) & 0xFFu;
+      if constexpr (REF == 1) refi = rstg[t * M + k];
       else if constexpr (REF == 2)
         refi = (uint32_t)(hash5(a.ref_seed, DOM_DATA, frame_id, t, (uint64_t)s * a.M_occ + k) &
                           (uint64_t)(a.qam.L * a.qam.L - 1));
@@ -926,21 +937,38 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
     };
     // CPE: the symbol's common phase c = sum conj(Q(y)) y over every stream's outputs at even
     // subcarriers (per thread in stream-then-slot order, per wave by the xor tree, the waves
-    // in order), then every output of the symbol turned by conj(c) / |c|. (Every stream: each
-    // carries its own static phase error from its column of G, which one stream's estimate
-    // would impose on the others.)
-    auto cpe_turn = [&](v2f (&y)[NA][S]) {
+    // in order), then every output of the symbol turned by u = conj(c) / |c| before its
+    // decision. (Every stream: each carries its own static phase error from its column of G,
+    // which one stream's estimate would impose on the others.) The even outputs are formed
+    // twice -- once here for c, once in the apply below -- rather than held across the
+    // workgroup reduction: the symbol's outputs and the weights do not fit the registers
+    // together (the held form spilled).
+    v2f u = v2f{1.0f, 0.0f};
+    if constexpr (CPE) {
       v2f c = v2f{0.0f, 0.0f};
       // KADJ: k = S tid + q, even for q = 0; else k = tid + q T (T even), even on even threads
       const bool even_thread = KADJ || ((opq(tid) & 1) == 0);
       if (even_thread) {
 #pragma unroll
-        for (int t = 0; t < NA; t++)
+        for (int q = 0; q < (KADJ ? 1 : S); q++) {
+          const uint32_t kk = KADJ ? (uint32_t)opq(tid) * S : (uint32_t)opq(tid) + q * T;
+          v2f X[NA];
+          if constexpr (WF) {
+            const v2f *xp = img + (kk & 7u) * QS + (WP::X256 ? (int)(kk >> 3) : padk<WP::PADK>((int)(kk >> 3)));
 #pragma unroll
-          for (int q = 0; q < (KADJ ? 1 : S); q++) {
-            const v2f pt = qam_dec_point_pk(y[t][q], inv_sc, Lf, Lm1, a.qam.scale);
-            c = cmac_pk(c, v2f{pt.x, -pt.y}, y[t][q]);
+            for (int r = 0; r < NA; r++) X[r] = xp[r * GS];
+          } else {
+            const v2f *xp = img + lds_pad((int)(uint32_t)opq(tid)) + q * (T + T / 32);
+#pragma unroll
+            for (int r = 0; r < NA; r++) X[r] = xp[r * PB];
           }
+#pragma unroll
+          for (int t = 0; t < NA; t++) {
+            const v2f y = apply1(t, q, X);
+            const v2f pt = qam_dec_point_pk(y, inv_sc, Lf, Lm1, a.qam.scale);
+            c = cmac_pk(c, v2f{pt.x, -pt.y}, y);
+          }
+        }
       }
 #pragma unroll
       for (int off = 32; off > 0; off >>= 1) {
@@ -955,32 +983,35 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
       const float m2 = c.x * c.x + c.y * c.y;
       if (m2 > 0.0f) {
         const float inv = 1.0f / sqrtf(m2);
-        const v2f u = v2f{c.x * inv, -c.y * inv};
-#pragma unroll
-        for (int t = 0; t < NA; t++)
-#pragma unroll
-          for (int q = 0; q < S; q++) y[t][q] = cmul_pk(y[t][q], u);
+        u = uni(v2f{c.x * inv, -c.y * inv});
       }
+    }
+    // one output: the apply, turned by the common phase (CPE)
+    auto out1 = [&](int t, int q, const v2f *X) -> v2f {
+      const v2f y = apply1(t, q, X);
+      if constexpr (CPE) return cmul_pk(y, u);
+      else return y;
     };
-    v2f yc[CPE ? NA : 1][CPE ? S : 1];                // CPE: the symbol's outputs, turned
     if constexpr (KADJ) {
       // the thread's S adjacent subcarriers k = S tid + q: every antenna's X of both, then per
       // stream both outputs and one 16-byte symbol store and one 2-byte index store (per stream
       // the EVM terms accumulate in the same q order as the strided form)
       v2f X[S][NA];
+      // (CPE: the q = 0 outputs of every stream first, then X of q = 1 -- X of both slots and
+      // the outputs are not held together: the turned apply has fewer registers to spare)
+      v2f yq0[CPE ? NA : 1];
 #pragma unroll
       for (int q = 0; q < S; q++) {
         const uint32_t kk = (uint32_t)opq(tid) * S + q;
         const v2f *xp = img + (kk & 7u) * QS + (WP::X256 ? (int)(kk >> 3) : padk<WP::PADK>((int)(kk >> 3)));
 #pragma unroll
         for (int r = 0; r < NA; r++) X[q][r] = xp[r * GS];
-      }
-      if constexpr (CPE) {
+        if constexpr (CPE) {
+          if (q == 0) {
 #pragma unroll
-        for (int t = 0; t < NA; t++)
-#pragma unroll
-          for (int q = 0; q < S; q++) yc[t][q] = apply1(t, q, X[q]);
-        cpe_turn(yc);
+            for (int t = 0; t < NA; t++) yq0[t] = out1(t, 0, X[0]);
+          }
+        }
       }
 #pragma unroll
       for (int t = 0; t < NA; t++) {
@@ -988,14 +1019,10 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
         const auto osym = sgpr_ptr(reinterpret_cast<v2f *>(a.out_sym + ob));
         const auto oidx = sgpr_ptr(a.out_idx + ob);
         const uint32_t kb = (uint32_t)opq(tid) * S;
-        v2f y0, y1;
-        if constexpr (CPE) {
-          y0 = yc[t][0];
-          y1 = yc[t][1];
-        } else {
-          y0 = apply1(t, 0, X[0]);
-          y1 = apply1(t, 1, X[1]);
-        }
+        v2f y0;
+        if constexpr (CPE) y0 = yq0[t];
+        else y0 = out1(t, 0, X[0]);
+        const v2f y1 = out1(t, 1, X[1]);
         const uint32_t d0 = finish(t, 0, kb, y0);
         const uint32_t d1 = finish(t, 1, kb + 1, y1);
 #ifndef DS_ABL_NOSTORE   // timing ablation: no symbol / index stores
@@ -1017,30 +1044,18 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
           for (int r = 0; r < NA; r++) X[r] = xp[r * PB];
         }
       };
-      if constexpr (CPE) {
-#pragma unroll
-        for (int q = 0; q < S; q++) {
-          v2f X[NA];
-          load_x(q, X);
-#pragma unroll
-          for (int t = 0; t < NA; t++) yc[t][q] = apply1(t, q, X);
-        }
-        cpe_turn(yc);
-      }
 #pragma unroll
       for (int q = 0; q < S; q++) {
         const uint32_t k = (uint32_t)opq(tid) + q * T;
         v2f X[NA];
-        if constexpr (!CPE) load_x(q, X);
+        load_x(q, X);
 #pragma unroll
         for (int t = 0; t < NA; t++) {
           // uniform row bases (SGPRs): the stores take a 32-bit per-lane offset
           const uint64_t ob = ob0 + (uint64_t)t * rowstep;
           const auto osym = sgpr_ptr(reinterpret_cast<v2f *>(a.out_sym + ob));
           const auto oidx = sgpr_ptr(a.out_idx + ob);
-          v2f acc;
-          if constexpr (CPE) acc = yc[t][q];
-          else acc = apply1(t, q, X);
+          const v2f acc = out1(t, q, X);
           const uint32_t d = finish(t, q, k, acc);
 #ifndef DS_ABL_NOSTORE   // timing ablation: no symbol / index stores
           if constexpr (OUTS & 1)
@@ -1062,6 +1077,7 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
         cfo_frame(fn);
       }
     }
+    if (!last) cfo_next(sn);
     MARK(";@@G next");
     f = __builtin_amdgcn_readfirstlane(fn);
     s = __builtin_amdgcn_readfirstlane(sn);
@@ -1808,8 +1824,10 @@ static size_t res8_lds_bytes() { return sizeof(float2) * (2 * 8 * kR8RS + 8 * kR
 static uint32_t res8_grid(uint32_t n_cu) { return 64u * std::max(1u, n_cu / 64u); }
 
 bool decode_res8_accepts(const DecodeArgs &a, int log2M, uint32_t n_frames) {
-  static const bool off = [] { const char *e = getenv("RMIMO_DECODE_RES"); return e && e[0] == '0'; }();
-  return !off && a.N == 8 && log2M == 12 && a.detector != 3 && a.all_occ &&
+  // opt-in (RMIMO_DECODE_RES=1): measured 2.58 ms per C4 step against the split form's 1.35
+  // (profiles/r04/pmc_c4.json: waves parked 74% on its register-staged loads, VALU 6%)
+  static const bool on = [] { const char *e = getenv("RMIMO_DECODE_RES"); return e && e[0] == '1'; }();
+  return on && a.N == 8 && log2M == 12 && a.detector != 3 && a.all_occ &&
          n_frames <= kStreamMaxFrames && a.qam.L * a.qam.L <= kStreamMaxQam && a.cpe == 0;
 }
 

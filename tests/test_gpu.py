@@ -578,48 +578,57 @@ def test_c3_4x4_mmse_2048_64qam_full_frame():
 
 
 def test_c4_8x8_mmse_4096_256qam_reduced_codes():
-    """C4 geometry with 2 access codes so the brute-force oracle stays within ~30 s. PID 12:
-    the one-pass residue-class decode with fewer symbols than its 32 workgroup groups."""
+    """C4 geometry with 2 access codes so the brute-force oracle stays within ~30 s. PID 12 is
+    below M/64, so this takes the per-symbol decode_kernel<12, 8>."""
     _c_frame_parity(4096, 304, 8, 2, 12, 256, _lib.DET_MMSE, 35.0, seed=41, bias=False,
-                    path=_lib.DECODE_RESIDUE)
+                    path=_lib.DECODE_SYMBOL)
 
 
-def test_c4_residue_decode_matches_oracle():
-    """The production C4 decode: decode_res8_kernel (decode_stream.hip), eight workgroups per
-    symbol, each the 512-point transforms of one subcarrier residue class of all eight
-    antennas and the 8x8 apply of those subcarriers. PID 66 (22 groups of 3 symbols, EVM
-    records of every class) against the brute-force oracle with 2 access codes: symbols within
-    the EVM tolerance, indices, errors and EVM-dB."""
+def test_c4_split_decode_matches_oracle():
+    """The production C4 decode: with max_out >= M/64 the 8x8 frame takes the split form
+    (spectra_persist_kernel<12> writes every symbol's spectra, apply_split2_kernel<8> applies
+    W, demaps and sums EVM; decode_stream.hip). PID 66 against the brute-force oracle with 2
+    access codes: symbols within the EVM tolerance, indices, errors and EVM-dB."""
     _c_frame_parity(4096, 304, 8, 2, 66, 256, _lib.DET_MMSE, 35.0, seed=48, bias=False,
-                    path=_lib.DECODE_RESIDUE, out_idx=True)
+                    path=_lib.DECODE_SPLIT, out_idx=True)
 
 
-def test_c4_split_and_symbol_decodes_in_child():
-    """The two-pass split decode (spectra_kernel<12> + apply_split2_kernel<8>) and the
-    per-symbol decode_kernel<12, 8> remain behind RMIMO_DECODE_RES=0 (read once per process):
-    a child interpreter runs the C4 parity cases on them."""
+def test_c4_residue_decode_in_child():
+    """The one-pass residue-class decode (decode_res8_kernel, opt-in behind RMIMO_DECODE_RES=1,
+    read once per process; eight workgroups per symbol, each the 512-point transforms of one
+    subcarrier residue class of all eight antennas and the 8x8 apply of those subcarriers): a
+    child interpreter runs the oracle parity cases (PID 66 with indices: 22 groups of 3
+    symbols, EVM records of every class; PID 12: fewer symbols than its 32 groups) and the
+    batch = single-frame equality on it."""
     import subprocess
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     code = ("import sys; sys.path.insert(0, %r); sys.path.insert(0, %r)\n"
             "import test_gpu as t\nfrom rub_mimo_amd import _lib\n"
             "t._c_frame_parity(4096, 304, 8, 2, 66, 256, _lib.DET_MMSE, 35.0, seed=48,"
-            " bias=False, path=_lib.DECODE_SPLIT, out_idx=True)\n"
+            " bias=False, path=_lib.DECODE_RESIDUE, out_idx=True)\n"
             "t._c_frame_parity(4096, 304, 8, 2, 12, 256, _lib.DET_MMSE, 35.0, seed=41,"
-            " bias=False, path=_lib.DECODE_SYMBOL)\nprint('split/symbol parity ok')\n"
+            " bias=False, path=_lib.DECODE_RESIDUE)\n"
+            "t._c4_batch_equals_single_frames(_lib.DECODE_RESIDUE)\n"
+            "print('residue parity ok')\n"
             % (root, os.path.join(root, "tests")))
-    env = dict(os.environ, RMIMO_DECODE_RES="0")
-    out = subprocess.run([sys.executable, "-c", code], env=env, cwd=root, timeout=110,
+    env = dict(os.environ, RMIMO_DECODE_RES="1")
+    out = subprocess.run([sys.executable, "-c", code], env=env, cwd=root, timeout=150,
                          capture_output=True, text=True)
     assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-4000:]
-    assert "split/symbol parity ok" in out.stdout
+    assert "residue parity ok" in out.stdout
 
 
-def test_c4_residue_batch_equals_single_frames():
-    """decode_res8_kernel on a batch: its workgroup groups' symbol ranges straddle frames
-    (3 frames x PID 67 over 32 groups), yet each frame's symbols and indices equal a
-    one-frame batch bit for bit; the indices are the hard decisions of the symbols and the
-    EVM / symbol-error sums equal a float64 recount (ref_mode 1)."""
+def test_c4_batch_equals_single_frames():
+    """The production C4 decode on a batch equals one-frame batches bit for bit."""
+    _c4_batch_equals_single_frames(_lib.DECODE_SPLIT)
+
+
+def _c4_batch_equals_single_frames(path):
+    """A C4 decode on a batch: its workgroups' symbol ranges straddle frames (3 frames x PID
+    67), yet each frame's symbols and indices equal a one-frame batch bit for bit; the indices
+    are the hard decisions of the symbols and the EVM / symbol-error sums equal a float64
+    recount (ref_mode 1)."""
     import torch
     M, cp, N, nac, pid, qam, F = 4096, 304, 8, 2, 67, 256, 3
     sp = SynthParams(M=M, cp_len=cp, num_streams=N, num_access_codes=nac, pid=pid,
@@ -636,7 +645,7 @@ def test_c4_residue_batch_equals_single_frames():
     idx = torch.zeros((F, N, pid, M), dtype=torch.uint8, device="cuda")
     rx.process(iq, L, L, F, max_out=pid, out_sym=sym, out_idx=idx, ref_mode=1, ref_idx=tx)
     torch.cuda.synchronize()
-    assert rx.decode_path() == _lib.DECODE_RESIDUE
+    assert rx.decode_path() == path
     res = rx.results(F)
     ok = [f for f in range(F) if res[f]["status"] == _lib.FRAME_OK]
     assert len(ok) >= 1, [r["status"] for r in res]
