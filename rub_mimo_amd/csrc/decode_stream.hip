@@ -333,6 +333,22 @@ MIMO_DEV void sub256_fwd(v2f *rg, v2f *v, const v2f *twl, uint32_t s) {
 }
 
 // a wave-uniform complex value held in SGPRs
+// the sum over the 64 lanes, in every lane, with no LDS traffic: v_permlane32/16_swap pair lanes
+// l and l ^ 32 / l ^ 16, then DPP row_mirror (l ^ 15), row_half_mirror (l ^ 7) and quad_perm
+// (l ^ 2, l ^ 1), whose partner sets together cover the 16 lanes of a row
+MIMO_DEV float wave_sum_f(float x) {
+  const uint32_t b = __float_as_uint(x);
+  const auto s32 = __builtin_amdgcn_permlane32_swap(b, b, false, false);
+  x = __uint_as_float(s32[0]) + __uint_as_float(s32[1]);
+  const uint32_t b16 = __float_as_uint(x);
+  const auto s16 = __builtin_amdgcn_permlane16_swap(b16, b16, false, false);
+  x = __uint_as_float(s16[0]) + __uint_as_float(s16[1]);
+  x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x140, 0xf, 0xf, false));
+  x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x141, 0xf, 0xf, false));
+  x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x4E, 0xf, 0xf, false));
+  x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0xB1, 0xf, 0xf, false));
+  return x;
+}
 MIMO_DEV v2f uni(v2f v) {
   return v2f{__int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v.x))),
              __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v.y)))};
@@ -573,6 +589,33 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
 #pragma unroll
   for (int g = 0; g < NA; g++) ptn |= (((uint32_t)g * (uint32_t)a.stride) & (SPC - 1)) << (4 * g);
   ptn = __builtin_amdgcn_readfirstlane(ptn);
+  // the reference indices of symbol (fb, ss) into rstg ([NA][M] bytes), by waves RW0 .. RW0 +
+  // NREF/64 - 1 (with DS_ROW_DMA the waves after the row waves, which stage no samples). Plain
+  // kernels: issued with the next symbol's samples and copied to registers (cref) at the top of
+  // the symbol. CPE kernels (fewer registers to spare): issued after a symbol's top barrier
+  // (every wave is done with the previous symbol's), waited for by those waves before the
+  // barrier that precedes the apply, and read there straight from LDS
+  constexpr int RW0 = (WPR && NA * WPR + NREF / 64 <= T / 64) ? NA * WPR : 0;
+  static_assert(NREF % 64 == 0 && RW0 + NREF / 64 <= T / 64, "reference DMA waves");
+  const bool ref_wave = REF == 1 && wv >= (uint32_t)RW0 && wv < (uint32_t)(RW0 + NREF / 64);
+  auto fetch_ref = [&](const FrameBase &fb, uint32_t ss) {
+    if constexpr (REF == 1) {
+      if (ref_wave) {
+        const int tr = opq(tid) - RW0 * 64;
+        const uint32_t dst = __builtin_amdgcn_readfirstlane(rstg_base + (uint32_t)((wv - RW0) * 64) * 16u);
+        const uint32_t t = (uint32_t)tr / (M / 16), q = (uint32_t)tr % (M / 16);
+        const auto rb = sgpr_ptr(a.ref_idx + fb.ref + (uint64_t)ss * a.M_occ);
+        dma16(t * (uint32_t)(a.max_out * a.M_occ) + 16 * q, rb, dst);
+      }
+    }
+  };
+  // ... and the wait (the reference waves' only loads in flight: with RW0 = 0 they also stage
+  // samples, whose DMA this waits for as well)
+  auto wait_ref = [&]() {
+    if constexpr (REF == 1 && CPE)
+      if (ref_wave) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  };
+
   auto fetch = [&](const FrameBase &fb, uint32_t ss) -> uint32_t {
     const int64_t abs0 = fb.body + (int64_t)((uint64_t)ss * a.SL);
     const int64_t row0 = fb.row0;
@@ -639,34 +682,9 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
         }
       }
     }
+    if constexpr (REF == 1 && !CPE) fetch_ref(fb, ss);   // the next symbol's, with its samples
     return odds;
   };
-  // the reference indices of symbol (fb, ss) into rstg ([NA][M] bytes), by waves RW0 .. RW0 +
-  // NREF/64 - 1 (with DS_ROW_DMA the waves after the row waves, which stage no samples): issued
-  // after a symbol's top barrier (every wave is done with the previous symbol's), waited for
-  // by those waves before the barrier that precedes the apply, and read there straight from
-  // LDS -- the indices are not carried in registers through the transform
-  constexpr int RW0 = (WPR && NA * WPR + NREF / 64 <= T / 64) ? NA * WPR : 0;
-  static_assert(NREF % 64 == 0 && RW0 + NREF / 64 <= T / 64, "reference DMA waves");
-  const bool ref_wave = REF == 1 && wv >= (uint32_t)RW0 && wv < (uint32_t)(RW0 + NREF / 64);
-  auto fetch_ref = [&](const FrameBase &fb, uint32_t ss) {
-    if constexpr (REF == 1) {
-      if (ref_wave) {
-        const int tr = opq(tid) - RW0 * 64;
-        const uint32_t dst = __builtin_amdgcn_readfirstlane(rstg_base + (uint32_t)((wv - RW0) * 64) * 16u);
-        const uint32_t t = (uint32_t)tr / (M / 16), q = (uint32_t)tr % (M / 16);
-        const auto rb = sgpr_ptr(a.ref_idx + fb.ref + (uint64_t)ss * a.M_occ);
-        dma16(t * (uint32_t)(a.max_out * a.M_occ) + 16 * q, rb, dst);
-      }
-    }
-  };
-  // ... and the wait (the reference waves' only loads in flight: with RW0 = 0 they also stage
-  // samples, whose DMA this waits for as well)
-  auto wait_ref = [&]() {
-    if constexpr (REF == 1)
-      if (ref_wave) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  };
-
   // this frame's weights * gain * dn for the thread's subcarriers k = tid + q T
   v2f Wr[NA][NA][S];
   auto load_w = [&](uint32_t ff) {
@@ -814,7 +832,28 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
         for (int r = 0; r < 8; r++) v[r] = x[r * W8];
       }
     }
-    fetch_ref(fbase, s);
+    uint32_t cref[(NA * S + 3) / 4];                  // reference indices, byte (t S + q)
+    if constexpr (REF == 1 && !CPE) {
+      const int t0 = opq(tid);
+#pragma unroll
+      for (int w = 0; w < (NA * S + 3) / 4; w++) cref[w] = 0;
+      if constexpr (KADJ) {   // the thread's S = 2 bytes of stream t are adjacent
+#pragma unroll
+        for (int t = 0; t < NA; t++) {
+          const int e = t * S;
+          cref[e / 4] |= (uint32_t)reinterpret_cast<const uint16_t *>(rstg + t * M)[t0] << (8 * (e % 4));
+        }
+      } else {
+#pragma unroll
+        for (int t = 0; t < NA; t++)
+#pragma unroll
+          for (int q = 0; q < S; q++) {
+            const int e = t * S + q;
+            cref[e / 4] |= (uint32_t)rstg[t * M + t0 + q * T] << (8 * (e % 4));
+          }
+      }
+    }
+    if constexpr (CPE) fetch_ref(fbase, s);
     if constexpr (CPE) {
       // folded CFO: the symbol's derotation on its time samples (the body start's phasor
       // times the in-body part)
@@ -922,7 +961,8 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
 #endif
       const uint32_t d = gidx[qam_level_pair_pk(acc, inv_sc, Lf, Lm1, a.qam.L)];
       uint32_t refi;
-      if constexpr (REF == 1) refi = rstg[t * M + k];
+      if constexpr (REF == 1 && CPE) refi = rstg[t * M + k];
+      else if constexpr (REF == 1) refi = (cref[(t * S + q) / 4] >> (8 * ((t * S + q) % 4))) & 0xFFu;
       else if constexpr (REF == 2)
         refi = (uint32_t)(hash5(a.ref_seed, DOM_DATA, frame_id, t, (uint64_t)s * a.M_occ + k) &
                           (uint64_t)(a.qam.L * a.qam.L - 1));
@@ -970,11 +1010,8 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
           }
         }
       }
-#pragma unroll
-      for (int off = 32; off > 0; off >>= 1) {
-        c.x += __shfl_xor(c.x, off);
-        c.y += __shfl_xor(c.y, off);
-      }
+      c.x = wave_sum_f(c.x);
+      c.y = wave_sum_f(c.y);
       if ((tid & 63) == 0) cpe_part[wv] = c;
       __syncthreads();
       c = cpe_part[0];
