@@ -749,8 +749,9 @@ static void emit_symbol(ref_framesync *fs, const ref_cf32 *X /* [N][M_occ] */) {
  *     k + M inside the window (i0 = corr[N-1][last] + M, framing.cc:857);
  *  4. each access code's LS terms X/S1 turned by exp(-j 2 pi delta (c + M/2) / M), c its window;
  *  5. the decode reads x[j] exp(-j 2 pi (eps0 + delta) j / M);
- *  6. cfo_mode 2: per symbol, c = sum conj(Q(y)) y over the outputs y of every stream at even
- *     occupied index j (Q the hard decision's point), and every output of the symbol turned
+ *  6. cfo_mode 2: per symbol, c = sum conj(Q(y)) y over the outputs y of every stream at the
+ *     occupied indices j with j even and bit 9 of j clear (Q the hard decision's point; the
+ *     GPU's rule: it halves that pass on whole waves), and every output of the symbol turned
  *     by conj(c) / |c|. (Every stream: each stream's output carries its own static phase error
  *     from its column of G, and one stream's would turn the others by it.)
  * ==================================================================================== */
@@ -766,8 +767,8 @@ static ref_cf32 cfo_turn(ref_cf32 v, double nu, uint64_t j) {
 
 static void cfo_common_phase(const ref_framesync *fs, ref_cf32 *out /* [N][M_occ] */) {
   double cr = 0.0, ci = 0.0;
-  for (size_t i = 0; i < (size_t)fs->N * fs->M_occ; i++) { /* every stream, even j */
-    if ((i % fs->M_occ) & 1) continue;
+  for (size_t i = 0; i < (size_t)fs->N * fs->M_occ; i++) { /* every stream, the j above */
+    if (((i % fs->M_occ) & 1) || (((i % fs->M_occ) >> 9) & 1)) continue;
     ref_cf32 y = out[i];
     ref_cf32 p = ref_qam_point(ref_qam_demap(y, fs->cfg.qam), fs->cfg.qam);
     cr += (double)p.re * y.re + (double)p.im * y.im; /* conj(p) y */

@@ -114,7 +114,8 @@ def receive(rx, M, cp, N, nac, pid_max, s0_bits, s1_bits, p=None, detector="zf2"
     cfo=True: the opt-in CFO stages (eps0 from the S&C window at the trigger, search and LS on
     the window turned by eps0, delta from the data prefixes, LS terms turned by delta at their
     window centres, decode of the window turned by eps0 + delta) and, with qam, the per-symbol
-    common phase from the decisions of every stream at even occupied index."""
+    common phase from the decisions of every stream at the even occupied indices with bit 9
+    clear."""
     if p is None:
         p = np.full(M, 2, np.uint8)
     SL = M + cp
@@ -221,7 +222,8 @@ def receive(rx, M, cp, N, nac, pid_max, s0_bits, s1_bits, p=None, detector="zf2"
         Y = np.einsum("ktr,rk->tk", W[occ], X[:, occ])
         syms[s] = Y * gain[None, :]
         if cfo and qam:
-            ev = syms[s][:, 0::2]          # every stream, even occupied index
+            j = np.arange(syms[s].shape[1])
+            ev = syms[s][:, ((j & 1) == 0) & (((j >> 9) & 1) == 0)]   # every stream; j even, bit 9 clear
             c = np.sum(np.conj(qam_decision_point(ev, qam)) * ev)
             if c != 0:
                 syms[s] *= np.conj(c) / abs(c)

@@ -975,10 +975,11 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
       e_den[t] = __builtin_fmaf(sp.x, sp.x, __builtin_fmaf(sp.y, sp.y, e_den[t]));
       return d;
     };
-    // CPE: the symbol's common phase c = sum conj(Q(y)) y over every stream's outputs at even
-    // subcarriers (per thread in stream-then-slot order, per wave by the xor tree, the waves
-    // in order), then every output of the symbol turned by u = conj(c) / |c| before its
-    // decision. (Every stream: each carries its own static phase error from its column of G,
+    // CPE: the symbol's common phase c = sum conj(Q(y)) y over every stream's outputs at the
+    // subcarriers k with k even and bit 9 of k clear (per thread in stream-then-slot order, per
+    // wave by a lane sum, the waves in order), then every output of the symbol turned by u =
+    // conj(c) / |c| before its decision. (The bit-9 rule halves the pass on whole waves: at C3,
+    // k = 2 tid, so waves w with w & 4 clear -- two of the four on each SIMD.) (Every stream: each carries its own static phase error from its column of G,
     // which one stream's estimate would impose on the others.) The even outputs are formed
     // twice -- once here for c, once in the apply below -- rather than held across the
     // workgroup reduction: the symbol's outputs and the weights do not fit the registers
@@ -992,6 +993,7 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
 #pragma unroll
         for (int q = 0; q < (KADJ ? 1 : S); q++) {
           const uint32_t kk = KADJ ? (uint32_t)opq(tid) * S : (uint32_t)opq(tid) + q * T;
+          if ((kk >> 9) & 1u) continue;               // (uniform per wave when KADJ)
           v2f X[NA];
           if constexpr (WF) {
             const v2f *xp = img + (kk & 7u) * QS + (WP::X256 ? (int)(kk >> 3) : padk<WP::PADK>((int)(kk >> 3)));
