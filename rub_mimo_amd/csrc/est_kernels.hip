@@ -215,6 +215,36 @@ MIMO_DEV v2f phasor_cycles(double cyc) {
   return v2f{(float)cs, (float)sn};
 }
 
+// the same from an exactly reduced phase with the fp32 sincos (per-thread start phasors of the
+// folded CFO; the per-workgroup values below keep the fp64 one)
+MIMO_DEV v2f phasor_cycles32(double cyc) {
+  double ph = -2.0 * cyc;                             // units of pi
+  ph -= 2.0 * rint(ph * 0.5);
+  float sn, cs;
+  sincospif((float)ph, &sn, &cs);
+  return v2f{cs, sn};
+}
+
+// folded CFO of a search workgroup: the frame's stage-1 frequency nu (cycles per sample) and the
+// workgroup-uniform step phasors exp(-j 2 pi nu d), formed once by thread 0 (the stage partials'
+// sum, its atan2 and the fp64 sincospi were per thread) and read by every thread from LDS
+struct CfoSearchLds {
+  double nu;
+  v2f step[3];
+};
+MIMO_DEV double cfo_search_setup(CfoSearchLds &c, const double *part, uint32_t f, uint32_t M,
+                                 double d0, double d1, double d2) {
+  if (threadIdx.x == 0) {
+    const double nu = cfo_stage_eps(part, f, 1) / (double)M;
+    c.nu = nu;
+    c.step[0] = phasor_cycles(nu * d0);
+    c.step[1] = phasor_cycles(nu * d1);
+    c.step[2] = phasor_cycles(nu * d2);
+  }
+  __syncthreads();
+  return c.nu;
+}
+
 MIMO_DEV uint32_t key_index(unsigned long long k) {
   return k ? (0xFFFFFFFFu - (uint32_t)(k & 0xFFFFFFFFull)) : 0u;
 }
@@ -238,6 +268,7 @@ void search_ls_kernel(SearchArgs a) {
   extern __shared__ __attribute__((aligned(16))) float2 lds_raw[];
   v2f *buf = reinterpret_cast<v2f *>(lds_raw);
   __shared__ unsigned long long s_key[2];
+  __shared__ CfoSearchLds cfo_lds;                    // (folded CFO only)
   // (frame, rx, pair) of this workgroup. xcd_order: workgroups are dispatched round-robin over
   // the 8 XCDs (hardware id b -> XCD b mod 8); each XCD is given a contiguous range of the
   // order (pair, frame, rx), so the workgroups resident on one XCD at a time share the two
@@ -286,9 +317,9 @@ void search_ls_kernel(SearchArgs a) {
   if constexpr (CFO) {
     // sample tid + e F/16 of the segment, relative to base: SL s0 + tid + e F/16
     static_assert(PTS == 16 && PL::RM == 16, "reg_index = tid + e F/16");
-    nu = cfo_stage_eps(a.cfo_part, f, 1) / (double)M;
-    v2f rb = phasor_cycles(nu * (double)((int64_t)a.SL * s0 + tid));
-    const v2f st = phasor_cycles(nu * (double)(F / 16));
+    nu = cfo_search_setup(cfo_lds, a.cfo_part, f, M, (double)(F / 16), (double)(M / 8), 0.0);
+    v2f rb = phasor_cycles32(nu * (double)((int64_t)a.SL * s0 + tid));
+    const v2f st = cfo_lds.step[0];
 #pragma unroll
     for (int e = 0; e < PTS; e++) {
       v[e] = vmul(v[e], rb);
@@ -374,8 +405,8 @@ void search_ls_kernel(SearchArgs a) {
       xw[e] = ok ? v2f{t.x, t.y} : v2f{0.0f, 0.0f};
     }
     if constexpr (CFO) {   // window sample lt + e M/8, relative to base
-      v2f rb = phasor_cycles(nu * (double)(wb - I.base + (int64_t)lt));
-      const v2f st = phasor_cycles(nu * (double)(M / 8));
+      v2f rb = phasor_cycles32(nu * (double)(wb - I.base + (int64_t)lt));
+      const v2f st = cfo_lds.step[1];
 #pragma unroll
       for (int e = 0; e < 8; e++) {
         xw[e] = vmul(xw[e], rb);
@@ -458,6 +489,7 @@ void search_ls_wave_kernel(SearchArgs a) {
   extern __shared__ __attribute__((aligned(16))) float2 lds_raw[];
   v2f *buf = reinterpret_cast<v2f *>(lds_raw);
   __shared__ unsigned long long s_key[2];
+  __shared__ CfoSearchLds cfo_lds;                    // (folded CFO only)
   uint32_t f = blockIdx.y, bx = blockIdx.x;
   if (a.xcd_order) {   // as search_ls_kernel: slot pair slowest within each XCD's range
     const uint32_t G = gridDim.x * gridDim.y, b = blockIdx.y * gridDim.x + blockIdx.x;
@@ -511,10 +543,10 @@ void search_ls_wave_kernel(SearchArgs a) {
   }
   double nu = 0.0;                                    // CFO: eps0 / M, cycles per sample
   if constexpr (CFO) {
-    nu = cfo_stage_eps(a.cfo_part, f, 1) / (double)M;
+    nu = cfo_search_setup(cfo_lds, a.cfo_part, f, M, (double)T, 1024.0, (double)(M / 8));
     // sample n_i + 1024 rr, n_i = tid + T i, relative to base: SL s0 + n_i + 1024 rr
-    v2f ri = phasor_cycles(nu * (double)((int64_t)a.SL * s0 + tid));
-    const v2f sa = phasor_cycles(nu * (double)T), sb = phasor_cycles(nu * 1024.0);
+    v2f ri = phasor_cycles32(nu * (double)((int64_t)a.SL * s0 + tid));
+    const v2f sa = cfo_lds.step[0], sb = cfo_lds.step[1];
 #pragma unroll
     for (int i = 0; i < NB; i++) {
       v2f rb = ri;
@@ -655,8 +687,8 @@ void search_ls_wave_kernel(SearchArgs a) {
       }
     }
     if constexpr (CFO) {   // window sample lt + e M/8, relative to base: wb - base + ...
-      v2f rb = phasor_cycles(nu * (double)(wb - I.base + (int64_t)lt));
-      const v2f st = phasor_cycles(nu * (double)(M / 8));
+      v2f rb = phasor_cycles32(nu * (double)(wb - I.base + (int64_t)lt));
+      const v2f st = cfo_lds.step[2];
 #pragma unroll
       for (int e = 0; e < 8; e++) {
         xw[e] = vmul(xw[e], rb);
