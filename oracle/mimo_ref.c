@@ -744,9 +744,8 @@ static void emit_symbol(ref_framesync *fs, const ref_cf32 *X /* [N][M_occ] */) {
  *  1. eps0 = arg(sum_r sum_{n<M/2} conj(x[t0+n]) x[t0+n+M/2]) / pi, t0 = trigger - M + 1: the S&C
  *     window that ends at the trigger lies in the M/2-periodic S0 on every antenna;
  *  2. search and LS read x1[j] = x[j] exp(-j 2 pi eps0 j / M);
- *  3. delta = arg(P1) / (2 pi), P1 = exp(-j 2 pi eps0) sum over the data symbols s < PID+2
- *     with s a multiple of 4, antennas and prefix interiors (n in [4, cp-4)) of
- *     conj(x[k]) x[k+M], k = i0 + s SL + n,
+ *  3. delta = arg(P1) / (2 pi), P1 = exp(-j 2 pi eps0) sum over the data symbols s < PID+2,
+ *     antennas and prefix interiors (n in [4, cp-4)) of conj(x[k]) x[k+M], k = i0 + s SL + n,
  *     k + M inside the window (i0 = corr[N-1][last] + M, framing.cc:857);
  *  4. each access code's LS terms X/S1 turned by exp(-j 2 pi delta (c + M/2) / M), c its window;
  *  5. the decode reads x[j] exp(-j 2 pi (eps0 + delta) j / M);
@@ -807,7 +806,7 @@ static double cfo_stage3(const ref_framesync *fs, const ref_cf32 *buf, uint64_t 
   const uint32_t M = fs->M, N = fs->N, cp = fs->cp, SL = fs->SL, margin = 4;
   const uint32_t inner = cp > 2 * margin ? cp - 2 * margin : 0;
   double re = 0.0, im = 0.0;
-  for (uint32_t s = 0; s < fs->cfg.pid_max + 2; s += 4) /* every fourth symbol, as the GPU */
+  for (uint32_t s = 0; s < fs->cfg.pid_max + 2; s++)
     for (uint32_t r = 0; r < N; r++)
       for (uint32_t n = 0; n < inner; n++) {
         uint64_t k = i0 + (uint64_t)s * SL + margin + n;

@@ -175,7 +175,7 @@ def receive(rx, M, cp, N, nac, pid_max, s0_bits, s1_bits, p=None, detector="zf2"
     if cfo:
         i0 = corr_idx[N - 1, nacN - 1] + M
         ks = []
-        for s in range(0, pid_max + 2, 4):   # every fourth data symbol's prefix
+        for s in range(pid_max + 2):
             k = i0 + s * SL + 4 + np.arange(max(cp - 8, 0))
             ks.append(k[k + M < win_len])
         k = np.concatenate(ks)

@@ -75,8 +75,7 @@ __global__ __launch_bounds__(kCfoThreads) void cfo_derotate_kernel(float2 *__res
 //     eps0 into a scratch capture that search, LS, weights and decode read.
 //  2. fine, after the search: one S0 leaves a residual of ~1e-4 subcarrier spacings at 30 dB,
 //     ~0.3-1 rad of drift over 1000 symbols (and a phase spread across the access codes that
-//     the MMSE noise estimate would read as noise). The cyclic prefixes of every fourth data
-//     symbol --
+//     the MMSE noise estimate would read as noise). The cyclic prefixes of the data symbols --
 //     their positions known from the search (base + i0 + s SL, framing.cc:857) -- correlate
 //     conj(x[k]) x[k + M] over each prefix's interior: delta = arg(P) / (2 pi) on the coarse-
 //     corrected samples. The LS terms are rotated by delta at their code windows
@@ -84,7 +83,6 @@ __global__ __launch_bounds__(kCfoThreads) void cfo_derotate_kernel(float2 *__res
 // Blocks sum fixed symbol subsets into partials, combined in fixed order by the rotation
 // kernels (bitwise reproducible).
 constexpr uint32_t kCfoMargin = 4;   // prefix samples skipped at each end
-constexpr uint32_t kCfoSymStride = 4;   // stage 2 reads the prefixes of symbols 0, 4, 8, ...
 
 MIMO_DEV bool cfo_live(const FrameInfo &I) { return I.status == 0 || I.status == 2; }
 
@@ -129,12 +127,7 @@ __global__ __launch_bounds__(kCfoThreads) void cfo_batch_est_kernel(CfoBatchArgs
     // (the reads stay inside the framesync's window, as the reference's ring holds it: the
     // capture may hold more, the window does not)
     const int64_t wend = std::min<int64_t>(L, I.base + (int64_t)a.win);
-    // every kCfoSymStride-th data symbol (s = kCfoSymStride m, block b taking m = b + kCfoBlocks j):
-    // each prefix is an independent estimate of the same phase advance, and a quarter of them
-    // keep the estimate's spread well inside the common-phase step's reach at a quarter of the
-    // reads (all symbols: 135 us per C3x64 step, the largest CFO stage)
-    const uint32_t nd = (a.n_data + kCfoSymStride - 1) / kCfoSymStride;
-    const uint32_t nsym = nd > b ? (nd - b + kCfoBlocks - 1) / kCfoBlocks : 0u;
+    const uint32_t nsym = a.n_data > b ? (a.n_data - b + kCfoBlocks - 1) / kCfoBlocks : 0u;
     const uint32_t runs = nsym * a.N;
     const float2 *cap = src + (uint64_t)I.cap * a.N * a.stride;
     constexpr int U = 8;
@@ -147,7 +140,7 @@ __global__ __launch_bounds__(kCfoThreads) void cfo_batch_est_kernel(CfoBatchArgs
         for (int e = 0; e < U; e++) {
           const uint32_t p = p0 + (uint32_t)e;          // uniform: run (symbol, antenna)
           const uint32_t js = p / a.N, r = p % a.N;
-          const int64_t k = d0 + (int64_t)(b + js * kCfoBlocks) * kCfoSymStride * a.SL + kCfoMargin + n;
+          const int64_t k = d0 + (int64_t)(b + js * kCfoBlocks) * a.SL + kCfoMargin + n;
           ok[e] = p < runs && n < inner && k >= 0 && k + a.M < wend;
           const float2 *row = cap + (uint64_t)(p < runs ? r : 0u) * a.stride;
           const int64_t kk = ok[e] ? k : 0;
