@@ -1421,7 +1421,7 @@ MIMO_DEV void tr_reduce_step(float *v, int lane) {
 
 // block sums of antenna 0 over a span, the screen test, and the chunk list
 template <bool S>
-__global__ __launch_bounds__(kScrT) __attribute__((amdgpu_waves_per_eu(4))) void sc_screen_kernel(ScreenArgs a) {
+__global__ __launch_bounds__(kScrT) __attribute__((amdgpu_waves_per_eu(6))) void sc_screen_kernel(ScreenArgs a) {
   constexpr int B = kScrB;
   __shared__ float4 recs[kScrSpan / B + 2 * (kScrMaxD)];
   const uint32_t f = blockIdx.y;
@@ -1439,10 +1439,10 @@ __global__ __launch_bounds__(kScrT) __attribute__((amdgpu_waves_per_eu(4))) void
   const auto x = iq_row<S>(a.iq, a.iq_scale, (uint64_t)f * a.N * a.stride);   // antenna 0
   const bool vec = x.pair_ok();
   // block sums: a wave per block, two positions per lane (B = 128); kScrBPI blocks per wave
-  // iteration with all their loads issued before the first use, and the next iteration's
-  // loads issued before this one's sums (software-pipelined: a wave keeps two iterations of
-  // loads in flight instead of waiting one memory latency per iteration)
-  auto load_blocks = [&](int j0, float4 (&cur)[kScrBPI], float4 (&del)[kScrBPI]) {
+  // iteration with all their loads issued before the first use (one memory latency per
+  // iteration instead of per block)
+  for (int j0 = wv * kScrBPI; j0 < NB; j0 += (kScrT / 64) * kScrBPI) {
+    float4 cur[kScrBPI], del[kScrBPI];
     const int64_t nb = h0 + (int64_t)j0 * B;
     if (vec && nb - RL >= 0 && nb + (int64_t)kScrBPI * B <= LF && j0 + kScrBPI <= NB) {
 #pragma unroll
@@ -1458,13 +1458,6 @@ __global__ __launch_bounds__(kScrT) __attribute__((amdgpu_waves_per_eu(4))) void
         del[b] = ld_pair(x, n - RL, LF, vec);
       }
     }
-  };
-  constexpr int JSTEP = (kScrT / 64) * kScrBPI;
-  float4 cur[kScrBPI], del[kScrBPI];
-  if (wv * kScrBPI < NB) load_blocks(wv * kScrBPI, cur, del);
-  for (int j0 = wv * kScrBPI; j0 < NB; j0 += JSTEP) {
-    float4 ncur[kScrBPI], ndel[kScrBPI];
-    if (j0 + JSTEP < NB) load_blocks(j0 + JSTEP, ncur, ndel);   // uniform
     // per-lane partials v[4 b + c] (c: Re P, Im P, |x|^2, |Re p| + |Im p|), then a transposing
     // butterfly: at offsets 32, 16, 8, 4 a lane keeps half of its values and adds the
     // partner's copy of them (8 + 4 + 2 + 1 exchanges for 16 sums instead of 16 x 6); lanes
@@ -1491,11 +1484,6 @@ __global__ __launch_bounds__(kScrT) __attribute__((amdgpu_waves_per_eu(4))) void
     {
       const int q = lane >> 2, b = q >> 2, c = q & 3;   // value q = 4 b + c
       if ((lane & 3) == 0 && j0 + b < NB) reinterpret_cast<float *>(&recs[j0 + b])[c] = tot;
-    }
-#pragma unroll
-    for (int b = 0; b < kScrBPI; b++) {
-      cur[b] = ncur[b];
-      del[b] = ndel[b];
     }
   }
   __syncthreads();
