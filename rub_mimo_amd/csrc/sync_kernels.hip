@@ -1424,10 +1424,18 @@ template <bool S>
 __global__ __launch_bounds__(kScrT) __attribute__((amdgpu_waves_per_eu(6))) void sc_screen_kernel(ScreenArgs a) {
   constexpr int B = kScrB;
   __shared__ float4 recs[kScrSpan / B + 2 * (kScrMaxD)];
+  // per chunk the test can touch (chunk_len >= kScrSpan / 2: at most three), the first and last
+  // unproven position, gathered before the global list update
+  constexpr int kScrChunks = 4;
+  __shared__ unsigned long long s_cmin[kScrChunks], s_cmax[kScrChunks];
   const uint32_t f = blockIdx.y;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int D = (int)(a.M / 2) / B, RL = (int)a.M / 2;
   if (a.trig && a.trig[f] != ~0ull) return;           // triggered in an earlier phase
+  if (tid < kScrChunks) {
+    s_cmin[tid] = ~0ull;
+    s_cmax[tid] = 0ull;
+  }
   const int64_t L = a.chunk_hi ? std::min<int64_t>((int64_t)a.frame_len,
                                                    (int64_t)(a.chunk_hi * a.chunk_len))
                                : (int64_t)a.frame_len;   // end of this phase's positions
@@ -1489,6 +1497,7 @@ __global__ __launch_bounds__(kScrT) __attribute__((amdgpu_waves_per_eu(6))) void
   __syncthreads();
   const int64_t K = (int64_t)a.chunk_len;
   const int64_t lo_all = (int64_t)a.chunk_lo * K;
+  const int64_t c_base = q0 / K;                       // the first chunk the test can touch
   for (int j = 2 * D + tid; j < NB; j += kScrT) {
     const int64_t n0 = h0 + (int64_t)j * B;
     if (n0 >= L) break;
@@ -1498,42 +1507,53 @@ __global__ __launch_bounds__(kScrT) __attribute__((amdgpu_waves_per_eu(6))) void
     // it for the first block, whose energy lower bound is zero, and every capture's chunk 0
     // used to become an exact-pass item for that block alone.)
     if (a.empty_history && n0 + B <= (int64_t)RL) continue;
+    // (one pass over the 2D records: each read once; the same sums in the same order)
     double pr = 0.0, pi = 0.0, apw = 0.0, rz = 0.0, azw = 0.0;
-    for (int u = 1; u <= D; u++) {
+    for (int u = 1; u <= 2 * D; u++) {
       const float4 r = recs[j - u];
-      pr += (double)r.x;
-      pi += (double)r.y;
-      apw += (double)r.w;
+      if (u <= D) {
+        pr += (double)r.x;
+        pi += (double)r.y;
+        apw += (double)r.w;
+      }
+      if (u < 2 * D) rz += (double)r.z;
+      azw += (double)r.z;
     }
-    for (int u = 1; u < 2 * D; u++) rz += (double)recs[j - u].z;
-    for (int u = 1; u <= 2 * D; u++) azw += (double)recs[j - u].z;
     const double ab = (double)recs[j].w, ad = (double)recs[j - D].w;
     const double pup = sqrt(pr * pr + pi * pi) + ab + ad + 1e-4 * (apw + ab + ad);
     const double rlow = 0.5 * (rz - 1e-4 * (azw + (double)recs[j].z));
     const bool proven = rlow > 0.0 && pup * pup < a.thr_screen * (rlow * rlow);
     if (proven) continue;
-    // unproven block: its positions in [lo_all, L) may be candidates
+    // unproven block: its positions in [lo_all, L) may be candidates -- gathered per chunk in
+    // LDS first, so each chunk the workgroup touches costs one set of global atomics (a chain
+    // of returning atomics per unproven block kept a workgroup alive ~20 us)
     const int64_t s0 = n0 < lo_all ? lo_all : n0;
     const int64_t s1 = (n0 + B < L ? n0 + B : L) - 1;
     if (s1 < s0) continue;
     for (int64_t c = s0 / K; c <= s1 / K; c++) {
-      const uint64_t ci = (uint64_t)f * a.nchunks + (uint64_t)c;
       const int64_t u0 = s0 > c * K ? s0 : c * K, u1 = s1 < (c + 1) * K - 1 ? s1 : (c + 1) * K - 1;
-      atomicMin(&a.fmin[ci], (unsigned long long)u0);
-      atomicMax(&a.fmax[ci], (unsigned long long)u1);
-      if (atomicOr(&a.flag[ci], 1u) == 0u) {
-        const uint32_t slot = atomicAdd(a.count, 1u);
-        if (slot < a.cap) {
-          ScHot *hp = a.hot + slot;
-          hp->f = f;
-          hp->n_done = a.N;
-          hp->namb = 0;
-          hp->arrived = 0;
-          hp->chunk = (uint64_t)c;
-          hp->c0 = c * K;
-          hp->w0 = c * K - ((int64_t)kScSpan - K);
-          hp->cend = (c + 1) * K < L ? (c + 1) * K : L;
-        }
+      atomicMin(&s_cmin[c - c_base], (unsigned long long)u0);
+      atomicMax(&s_cmax[c - c_base], (unsigned long long)u1);
+    }
+  }
+  __syncthreads();
+  if (tid < kScrChunks && s_cmin[tid] != ~0ull) {
+    const int64_t c = c_base + tid;
+    const uint64_t ci = (uint64_t)f * a.nchunks + (uint64_t)c;
+    atomicMin(&a.fmin[ci], s_cmin[tid]);
+    atomicMax(&a.fmax[ci], s_cmax[tid]);
+    if (atomicOr(&a.flag[ci], 1u) == 0u) {
+      const uint32_t slot = atomicAdd(a.count, 1u);
+      if (slot < a.cap) {
+        ScHot *hp = a.hot + slot;
+        hp->f = f;
+        hp->n_done = a.N;
+        hp->namb = 0;
+        hp->arrived = 0;
+        hp->chunk = (uint64_t)c;
+        hp->c0 = c * K;
+        hp->w0 = c * K - ((int64_t)kScSpan - K);
+        hp->cend = (c + 1) * K < L ? (c + 1) * K : L;
       }
     }
   }
