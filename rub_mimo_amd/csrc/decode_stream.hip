@@ -854,30 +854,6 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
       }
     }
     if constexpr (CPE) fetch_ref(fbase, s);
-    // the staging is consumed (every wave holds its samples, and its reference indices): the
-    // next symbol's staging DMA goes out now, ahead of pass 0's arithmetic, so it has pass 0 as
-    // well as the transforms and the apply to land (it used to follow pass 0's region stores,
-    // behind the same barrier)
-    __syncthreads();                                  // staging consumed by every wave
-    DSP(const unsigned long long ds_2 = __builtin_amdgcn_s_memtime(); ds_t[5] += ds_2 - ds_1;)
-    MARK(";@@C fetch");
-    // the item after this one (uniform) and its staging, in flight during this symbol
-    uint32_t fn = f, sn = s + 1, n_out_n = n_out_f;
-    uint32_t odd_n = 0;
-    FrameBase fbase_n = fbase;
-    if (i + 1 < i_end) {
-      if (sn >= n_out_f) {
-        do { fn++; } while (pfx[fn + 1] == pfx[fn]);
-        sn = 0;
-        n_out_n = pfx[fn + 1] - pfx[fn];
-        fn = __builtin_amdgcn_readfirstlane(fn);
-        fbase_n = frame_base(fn);
-      }
-      fn = __builtin_amdgcn_readfirstlane(fn);
-      sn = __builtin_amdgcn_readfirstlane(sn);
-      n_out_n = __builtin_amdgcn_readfirstlane(n_out_n);
-      odd_n = fetch(fbase_n, sn);
-    }
     if constexpr (CPE) {
       // folded CFO: the symbol's derotation on its time samples (the body start's phasor
       // times the in-body part)
@@ -904,12 +880,31 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
       v2f *e = img + g * GS + (WP::X256 ? (int)n : padk<WP::PADK>((int)n));
 #pragma unroll
       for (int q = 0; q < 8; q++) e[q * QS] = v[q];
-      __syncthreads();                                // every c_q[n] in its region
     }
-    DSP(const unsigned long long ds_2b = __builtin_amdgcn_s_memtime(); ds_t[6] += ds_2b - ds_2;)
+    __syncthreads();                                  // staging consumed by every wave
+    DSP(const unsigned long long ds_2 = __builtin_amdgcn_s_memtime(); ds_t[5] += ds_2 - ds_1;)
+    MARK(";@@C fetch");
+    // the item after this one (uniform) and its staging, in flight during this symbol
+    uint32_t fn = f, sn = s + 1, n_out_n = n_out_f;
+    uint32_t odd_n = 0;
+    FrameBase fbase_n = fbase;
+    if (i + 1 < i_end) {
+      if (sn >= n_out_f) {
+        do { fn++; } while (pfx[fn + 1] == pfx[fn]);
+        sn = 0;
+        n_out_n = pfx[fn + 1] - pfx[fn];
+        fn = __builtin_amdgcn_readfirstlane(fn);
+        fbase_n = frame_base(fn);
+      }
+      fn = __builtin_amdgcn_readfirstlane(fn);
+      sn = __builtin_amdgcn_readfirstlane(sn);
+      n_out_n = __builtin_amdgcn_readfirstlane(n_out_n);
+      odd_n = fetch(fbase_n, sn);
+    }
     // passes 1 .. NP-1 through the LDS images (pass 1 needs no leading barrier: the previous
     // symbol's image readers finished before the barrier at the top), then the exchange that
     // leaves the spectra in natural order
+    DSP(const unsigned long long ds_2b = __builtin_amdgcn_s_memtime(); ds_t[6] += ds_2b - ds_2;)
     MARK(";@@D subfft");
     if constexpr (WF) {
       // sub-transform (g, q) on lane group t0 / LG, inside one wave
