@@ -1552,6 +1552,51 @@ constexpr int kR8MS = 512;                    // points of a residue transform
 constexpr int kR8RS = 576;                    // region stride (entries): the x2 layout's 570
 constexpr int kR8Groups = 8;                  // residue classes = workgroups per symbol
 
+// the wave-local 512-point forward transform of region rg (RegPlan<9, 8>: radix 8, 8, 8) with
+// the streaming decode's exchange layouts (x1 after pass 0, x2 after pass 1; lds_pad left both
+// radix-8 stores 2-way bank-conflicted); input and output in natural order, element lane + 64 e
+MIMO_DEV void wave512_fwd(v2f *rg, const v2f *w1, int lane) {
+  using PL = RegPlan<9, 8>;
+  static_assert(PL::NP == 3 && PL::RM == 8 && PL::T == 64, "plan 8, 8, 8 on one wave");
+  v2f v[8];
+  int t = lane;
+  asm volatile("" : "+v"(t));
+#pragma unroll
+  for (int r = 0; r < 8; r++) v[r] = rg[t + 64 * r];
+  reg_compute<9, 8, 0, false>(v, w1);
+  {   // x1: element 8 t + r at 33 (t >> 2) + 8 (t & 3) + (r ^ m), m = 4 ((t >> 1) & 1)
+    const int m = ((t >> 1) & 1) << 2;
+    const int B = 33 * (t >> 2) + 8 * (t & 3);
+    v2f *lo = rg + B + m, *hi = rg + B - m;
+#pragma unroll
+    for (int r = 0; r < 4; r++) lo[r] = v[r];
+#pragma unroll
+    for (int r = 4; r < 8; r++) hi[r] = v[r];
+  }
+  wave_lds_sync();
+  {   // pass 1 loads elements t + 64 r
+    const v2f *p = rg + 33 * (t >> 5) + ((t & 31) ^ (((t >> 4) & 1) << 2));
+#pragma unroll
+    for (int r = 0; r < 8; r++) v[r] = p[66 * r];
+  }
+  reg_compute<9, 8, 1, false>(v, w1);
+  {   // x2: element 64 (t/8) + t%8 + 8 r
+    v2f *q = rg + 64 * (t >> 3) + (t & 7) + 8 * (t >> 3);
+#pragma unroll
+    for (int r = 0; r < 8; r++) q[8 * r + 2 * (r >> 2)] = v[r];
+  }
+  wave_lds_sync();
+  {   // pass 2 loads elements t + 64 r
+    const v2f *p = rg + x2pad(t);
+#pragma unroll
+    for (int r = 0; r < 8; r++) v[r] = p[72 * r];
+  }
+  reg_compute<9, 8, 2, false>(v, w1);
+  wave_lds_sync();
+#pragma unroll
+  for (int r = 0; r < 8; r++) rg[t + 64 * r] = v[r];
+}
+
 template <int REF, int OUTS, bool SC16>
 __global__ __launch_bounds__(kR8T) void decode_res8_kernel(DecodeArgs a) {
   constexpr int NA = 8, M = 4096, MS = kR8MS, RS = kR8RS, T = kR8T;

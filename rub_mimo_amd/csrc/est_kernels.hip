@@ -19,10 +19,6 @@
 namespace mimo {
 
 constexpr int kEstT = 256;
-// the search's LS windows in the wave-local form (1) or the workgroup register plan (0, A/B)
-#ifndef SL_LS_WAVE
-#define SL_LS_WAVE 1
-#endif
 
 // ------------------------------------------------------------------------------------
 template <int LOG2M, int LOG2F>
@@ -234,17 +230,16 @@ MIMO_DEV v2f phasor_cycles32(double cyc) {
 // sum, its atan2 and the fp64 sincospi were per thread) and read by every thread from LDS
 struct CfoSearchLds {
   double nu;
-  v2f step[4];
+  v2f step[3];
 };
 MIMO_DEV double cfo_search_setup(CfoSearchLds &c, const double *part, uint32_t f, uint32_t M,
-                                 double d0, double d1, double d2, double d3 = 0.0) {
+                                 double d0, double d1, double d2) {
   if (threadIdx.x == 0) {
     const double nu = cfo_stage_eps(part, f, 1) / (double)M;
     c.nu = nu;
     c.step[0] = phasor_cycles(nu * d0);
     c.step[1] = phasor_cycles(nu * d1);
     c.step[2] = phasor_cycles(nu * d2);
-    c.step[3] = phasor_cycles(nu * d3);
   }
   __syncthreads();
   return c.nu;
@@ -548,7 +543,7 @@ void search_ls_wave_kernel(SearchArgs a) {
   }
   double nu = 0.0;                                    // CFO: eps0 / M, cycles per sample
   if constexpr (CFO) {
-    nu = cfo_search_setup(cfo_lds, a.cfo_part, f, M, (double)T, 1024.0, (double)(M / 8), 512.0);
+    nu = cfo_search_setup(cfo_lds, a.cfo_part, f, M, (double)T, 1024.0, (double)(M / 8));
     // sample n_i + 1024 rr, n_i = tid + T i, relative to base: SL s0 + n_i + 1024 rr
     v2f ri = phasor_cycles32(nu * (double)((int64_t)a.SL * s0 + tid));
     const v2f sa = cfo_lds.step[0], sb = cfo_lds.step[1];
@@ -667,85 +662,7 @@ void search_ls_wave_kernel(SearchArgs a) {
   const int64_t w0 = I.base + (int64_t)key_index(s_key[0]);
   const int64_t w1v = I.base + (int64_t)key_index(s_key[1]);
   constexpr bool LSREG = 2 * (M / 8) == T && LOG2M >= 9;
-  // wave-local form (M = 2^10 .. 2^12): M = BL 512, one radix-BL pass across the window's BL
-  // waves (one workgroup barrier), then each wave one 512-point transform of its region in
-  // registers with in-wave exchanges (wave512_fwd_v): X[BL k + q] in wave q, k = lane + 64 e.
-  // The register plan above exchanges three times across the workgroup (six barriers).
-  constexpr int BL = M / 512;
-  constexpr bool LSWAVE = LSREG && SL_LS_WAVE && (BL == 2 || BL == 4 || BL == 8);
-  if constexpr (LSWAVE) {
-    constexpr int TWL = M / 8, NBL = 8 / BL, RSL = 576;   // RSL: the x2 layout's 570 entries
-    static_assert(2 * BL * RSL <= lds_padded_len(F), "both LS windows' regions in the buffer");
-    const uint32_t u = (uint32_t)tid / TWL, lt = (uint32_t)tid % TWL;   // u uniform per wave
-    const bool valid = u ? valid1 : valid0;
-    const int64_t wb = u ? w1v : w0;
-    // loads in the block pass's order: xw[i BL + rr] = x[n_i + 512 rr], n_i = lt + TWL i
-    v2f xw[8];
-    if (valid && wb >= 0 && wb + M <= L) {            // uniform per wave: one row base
-      const auto xr = xs.row((uint64_t)wb);
-#pragma unroll
-      for (int i = 0; i < NBL; i++)
-#pragma unroll
-        for (int rr = 0; rr < BL; rr++) {
-          const float2 t = xr.at((int)lt + TWL * i + 512 * rr);
-          xw[i * BL + rr] = v2f{t.x, t.y};
-        }
-    } else {
-#pragma unroll
-      for (int i = 0; i < NBL; i++)
-#pragma unroll
-        for (int rr = 0; rr < BL; rr++) {
-          const int64_t n = wb + (int64_t)lt + TWL * i + 512 * rr;
-          const bool ok = valid && n >= 0 && n < L;
-          const float2 t = xs.at(n < 0 ? 0 : (n >= L ? L - 1 : n));
-          xw[i * BL + rr] = ok ? v2f{t.x, t.y} : v2f{0.0f, 0.0f};
-        }
-    }
-    if constexpr (CFO) {   // sample n_i + 512 rr, relative to base: wb - base + lt + TWL i + ...
-      v2f ri = phasor_cycles32(nu * (double)(wb - I.base + (int64_t)lt));
-      const v2f sa = cfo_lds.step[2], sb = cfo_lds.step[3];   // TWL = M/8, 512
-#pragma unroll
-      for (int i = 0; i < NBL; i++) {
-        v2f rb = ri;
-#pragma unroll
-        for (int rr = 0; rr < BL; rr++) {
-          xw[i * BL + rr] = vmul(xw[i * BL + rr], rb);
-          rb = vmul(rb, sb);
-        }
-        ri = vmul(ri, sa);
-      }
-    }
-    // radix-BL block pass: c_q[n] = W_M^{n q} sum_rr x[n + 512 rr] W_BL^{rr q} -> region q at n
-    v2f *im = buf + u * (BL * RSL);
-#pragma unroll
-    for (int i = 0; i < NBL; i++) {
-      dft_small<BL, false>(xw + i * BL);
-      const int n = (int)lt + TWL * i;
-      v2f w[BL];
-      twiddle_powers<BL>(w, twiddle<false>(a.tw, n * (kTwN / M)));
-#pragma unroll
-      for (int q = 1; q < BL; q++) xw[i * BL + q] = vmul(xw[i * BL + q], w[q]);
-#pragma unroll
-      for (int q = 0; q < BL; q++) im[q * RSL + n] = xw[i * BL + q];
-    }
-    __syncthreads();                                  // every c_q complete
-    if (!valid) return;                               // uniform per wave
-    const uint32_t qw = lt >> 6;                      // this wave's class q (uniform; lane = lt & 63)
-    v2f wl[2];
-    reg_twiddles<9, 8>(wl, a.tw, lane);
-    wave512_fwd_v(im + qw * RSL, xw, wl, lane);
-    const uint32_t ac = s0 + u - 1, code = ac / a.N, tx = ac % a.N;
-    const auto sg = sgpr_ptr(a.s1sign + ((size_t)tx * a.nac + code) * M);
-    const auto q = sgpr_ptr(reinterpret_cast<v2f *>(a.lsq) +
-                            ((((uint64_t)f * a.N + r) * a.N + tx) * a.nac + code) * M);
-#pragma unroll
-    for (int e = 0; e < 8; e++) {
-      const uint32_t k = (uint32_t)BL * ((uint32_t)lane + 64u * e) + qw;
-      const float sgn = (float)sg[k];
-      q[k] = xw[e] * v2f{sgn, sgn};
-    }
-    return;
-  } else if constexpr (LSREG) {
+  if constexpr (LSREG) {
     using PM = RegPlan<LOG2M, 8>;
     constexpr int PBX = reg_image_len<LOG2M, 8>();     // conflict-free exchange layouts
     static_assert(2 * PBX <= lds_padded_len(F), "both LS images in the search's buffer");

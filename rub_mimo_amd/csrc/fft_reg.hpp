@@ -320,56 +320,6 @@ MIMO_DEV void wave1024_rest(v2f *buf, v2f *v, const v2f *w1, int lane) {
   reg_rest_wave<10, 16, 2, INV>(buf, v, w1, lane);
 }
 
-// the wave-local 512-point forward transform of region rg (RegPlan<9, 8>: radix 8, 8, 8) with
-// the exchange layouts above (x1 after pass 0, x2 after pass 1; lds_pad left both
-// radix-8 stores 2-way bank-conflicted); input in natural order (element lane + 64 e of the
-// region), output in v[e] = X[lane + 64 e]
-MIMO_DEV void wave512_fwd_v(v2f *rg, v2f (&v)[8], const v2f *w1, int lane) {
-  using PL = RegPlan<9, 8>;
-  static_assert(PL::NP == 3 && PL::RM == 8 && PL::T == 64, "plan 8, 8, 8 on one wave");
-  int t = lane;
-  asm volatile("" : "+v"(t));
-#pragma unroll
-  for (int r = 0; r < 8; r++) v[r] = rg[t + 64 * r];
-  reg_compute<9, 8, 0, false>(v, w1);
-  {   // x1: element 8 t + r at 33 (t >> 2) + 8 (t & 3) + (r ^ m), m = 4 ((t >> 1) & 1)
-    const int m = ((t >> 1) & 1) << 2;
-    const int B = 33 * (t >> 2) + 8 * (t & 3);
-    v2f *lo = rg + B + m, *hi = rg + B - m;
-#pragma unroll
-    for (int r = 0; r < 4; r++) lo[r] = v[r];
-#pragma unroll
-    for (int r = 4; r < 8; r++) hi[r] = v[r];
-  }
-  wave_lds_sync();
-  {   // pass 1 loads elements t + 64 r
-    const v2f *p = rg + 33 * (t >> 5) + ((t & 31) ^ (((t >> 4) & 1) << 2));
-#pragma unroll
-    for (int r = 0; r < 8; r++) v[r] = p[66 * r];
-  }
-  reg_compute<9, 8, 1, false>(v, w1);
-  {   // x2: element 64 (t/8) + t%8 + 8 r
-    v2f *q = rg + 64 * (t >> 3) + (t & 7) + 8 * (t >> 3);
-#pragma unroll
-    for (int r = 0; r < 8; r++) q[8 * r + 2 * (r >> 2)] = v[r];
-  }
-  wave_lds_sync();
-  {   // pass 2 loads elements t + 64 r
-    const v2f *p = rg + reg_x2(t);
-#pragma unroll
-    for (int r = 0; r < 8; r++) v[r] = p[72 * r];
-  }
-  reg_compute<9, 8, 2, false>(v, w1);
-}
-// ... with the result back in the region (natural order)
-MIMO_DEV void wave512_fwd(v2f *rg, const v2f *w1, int lane) {
-  v2f v[8];
-  wave512_fwd_v(rg, v, w1, lane);
-  wave_lds_sync();
-#pragma unroll
-  for (int r = 0; r < 8; r++) rg[lane + 64 * r] = v[r];
-}
-
 // element index held in v[s] after the last pass (and read by pass 0): j + r*N/R, R the main
 // radix (the first and the last pass)
 template <int LOG2N, int PTS>
