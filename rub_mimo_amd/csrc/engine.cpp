@@ -447,24 +447,15 @@ int run_sync(mimo_rx *h, const float2 *iq, uint64_t stride, uint32_t F, uint64_t
       // capture may begin mid-stream after a trim (its history is not empty)
       sa.empty_history = reset_trig ? 1u : 0u;
       if (a.diag & 32) a.diag |= 16;   // diagnostics: finalize as a separate kernel
-      // Two phases for one frame per capture: the first 1/64 of every capture's chunks (at
-      // least two; a frame's S0 plateau sits near its capture's start), then the rest only for
-      // captures with no trigger yet. A trigger found in phase 1 is the capture's first (every
-      // earlier chunk was evaluated) and phase 2 evaluates exactly the chunks one pass would have
-      // for the others, so results are those of one pass; the screen's reads of antenna 0 past
-      // the trigger of a synced capture are skipped, and so are the exact passes over the
-      // near-threshold access-code region behind it (with a first eighth as phase 1, C3x64 had
-      // ~140 phase-1 items, 560 passes over 512 resident workgroups: two rounds).
-      // RMIMO_SC_PHASES=1: one pass; RMIMO_SC_PHASE1_DIV: phase 1 = nchunks / DIV.
+      // Two phases for one frame per capture: the first eighth of every capture's chunks (a
+      // frame's S0 plateau sits near its capture's start), then the rest only for captures with
+      // no trigger yet. A trigger found in phase 1 is the capture's first (every earlier chunk
+      // was evaluated) and phase 2 evaluates exactly the chunks one pass would have for the
+      // others, so results are those of one pass; the screen's reads of antenna 0 past the
+      // trigger of a synced capture are skipped. RMIMO_SC_PHASES=1: one pass.
       static const bool one_phase = [] { const char *e = getenv("RMIMO_SC_PHASES"); return e && e[0] == '1'; }();
-      static const uint64_t p1_div = [] {
-        const char *e = getenv("RMIMO_SC_PHASE1_DIV");
-        const long v = e ? atol(e) : 0;
-        return (uint64_t)(v > 0 ? v : 64);
-      }();
       const uint64_t c1 = (!stream && chunk_lo == 0 && !one_phase && nchunks >= 16)
-                              ? std::min<uint64_t>(nchunks, std::max<uint64_t>(2, nchunks / p1_div))
-                              : nchunks;
+                              ? std::max<uint64_t>(2, nchunks / 8) : nchunks;
       sa.chunk_hi = c1;
       launch_sc_screen(sa, F, s);
       ScArgs a1 = a;
