@@ -1068,6 +1068,15 @@ MIMO_DEV bool trigger_run_starts(const PlateauArgs &a, uint32_t cap, const ScRec
 // (framing.cc:612-623): sync index, window base, completeness and num_samples_processed, all
 // relative to origin as that framesync counts them; FrameInfo keeps absolute positions.
 // Uniform on every lane; lane 0 writes. Returns the status.
+// the fields the estimation stages fill in later (weights_kernel, the CFO stages): zero until
+// then, so a frame they skip reports zeros, not the slot's previous contents
+MIMO_DEV void frame_clear_estimates(FrameInfo &I) {
+  I.noise_var = 0.0f;
+  I.i0 = 0;
+  I.cfo_eps = 0.0f;
+  I.cfo_E = 0;
+}
+
 MIMO_DEV int frame_from_trigger(const PlateauArgs &a, FrameInfo &I, uint32_t cap, uint32_t ref,
                                 int64_t origin, int64_t n, const int64_t (&st)[kMaxStreams],
                                 bool need_base_in_view, uint64_t &nsp_rel) {
@@ -1101,6 +1110,7 @@ MIMO_DEV int frame_from_trigger(const PlateauArgs &a, FrameInfo &I, uint32_t cap
     I.cap = cap;
     I.ref = ref;
     if (status != 0) I.n_sym = 0;
+    frame_clear_estimates(I);
     for (uint32_t s = 0; s < a.N; s++) {
       I.plateau_start[s] = (uint64_t)st[s];
       I.plateau_end[s] = (uint64_t)n;
@@ -1162,6 +1172,11 @@ MIMO_DEV void frame_empty(FrameInfo &I, int status, uint32_t cap, uint32_t ref, 
   I.origin = (uint64_t)origin;
   I.cap = cap;
   I.ref = ref;
+  frame_clear_estimates(I);
+  for (uint32_t s = 0; s < kMaxStreams; s++) {
+    I.plateau_start[s] = 0;
+    I.plateau_end[s] = 0;
+  }
 }
 
 // one frame per capture: run starts (from the trigger chunk's record, exact backward scan

@@ -673,18 +673,15 @@ def test_split_decode_m512_matches_oracle(det):
                     path=_lib.DECODE_SPLIT, out_idx=True)
 
 
-def test_two_phase_screen_finds_late_frames():
-    """The S&C screen runs in two phases (the first eighth of every capture's chunks, then the
-    rest for captures with no trigger yet). Frames placed past the first phase -- at 30%, 55%
-    and 80% of a noisy capture -- sync exactly as the oracle does on the whole capture, beside
-    one early frame; symbols within the EVM tolerance."""
+def _late_frames_capture(F=4, offs_frac=(0.02, 0.30, 0.55, 0.80), noise_only=()):
+    """Noisy captures of five frame lengths with one frame each at the given fraction of the
+    capture (past the S&C's first phase from 0.30 on); captures in noise_only hold no frame."""
     import torch
     M, cp, N, nac, pid, qam = 1024, 76, 2, 4, 40, 16
     sp = SynthParams(M=M, cp_len=cp, num_streams=N, num_access_codes=nac, pid=pid,
                      qam_order=qam, seed=21, snr_db=25.0)
     S = Synthesizer(sp)
     Lf = sp.max_frame_len()
-    F = 4
     frames = torch.zeros((F, N, Lf), dtype=torch.complex64, device="cuda")
     tx = torch.empty((F, N, pid, M), dtype=torch.uint8, device="cuda")
     S.generate(frames, Lf, Lf, F, tx_idx=tx)
@@ -692,9 +689,51 @@ def test_two_phase_screen_finds_late_frames():
     rng = np.random.default_rng(7)
     noise = (rng.standard_normal((F, N, L)) + 1j * rng.standard_normal((F, N, L))) * 1e-3
     cap = torch.from_numpy(noise.astype(np.complex64)).cuda()
-    offs = [int(0.02 * L), int(0.30 * L), int(0.55 * L), int(0.80 * L)]
+    offs = [int(offs_frac[f % len(offs_frac)] * L) for f in range(F)]
     for f in range(F):
-        cap[f, :, offs[f]:offs[f] + Lf] += frames[f]
+        if f not in noise_only:
+            cap[f, :, offs[f]:offs[f] + Lf] += frames[f]
+    geom = (M, cp, N, nac, pid, qam)
+    return geom, cap, tx, L, offs
+
+
+def _late_frames_run(F=7, calls=3):
+    """Batch receive of _late_frames_capture(F) (capture 5 noise only), repeated `calls` times
+    on one receiver (the second call is captured into a graph, the third replays it); returns
+    every call's symbols and per-frame results."""
+    import torch
+    (M, cp, N, nac, pid, qam), cap, tx, L, offs = _late_frames_capture(F, noise_only=(5,))
+    rxo = Receiver(RxParams(M=M, cp_len=cp, num_streams=N, num_access_codes=nac, pid_max=pid,
+                            detector=_lib.DET_ZF2, qam_order=qam))
+    out = []
+    sym = torch.empty((F, N, pid, M), dtype=torch.complex64, device="cuda")   # one buffer:
+    for _ in range(calls):                                                    # graph replays
+        sym.zero_()
+        torch.cuda.synchronize()
+        rxo.process(cap, L, L, F, max_out=pid, out_sym=sym, ref_mode=1, ref_idx=tx)
+        torch.cuda.synchronize()
+        res = rxo.results(F)
+        keys = ("status", "trigger", "sync_index", "num_samples_processed", "plateau_start",
+                "noise_var", "evm_num", "evm_den", "errors")
+        out.append((sym.cpu().numpy(), [{k: np.asarray(r[k]) for k in keys} for r in res]))
+    return out
+
+
+def _same_runs(a, b):
+    assert np.array_equal(a[0], b[0])
+    for f, (ra, rb) in enumerate(zip(a[1], b[1])):
+        for k in ra:
+            assert np.array_equal(ra[k], rb[k]), (f, k, ra[k], rb[k])
+
+
+def test_two_phase_screen_finds_late_frames():
+    """The S&C screen runs in two phases (the first eighth of every capture's chunks, then the
+    rest for captures with no trigger yet). Frames placed past the first phase -- at 30%, 55%
+    and 80% of a noisy capture -- sync exactly as the oracle does on the whole capture, beside
+    one early frame; symbols within the EVM tolerance."""
+    import torch
+    F = 4
+    (M, cp, N, nac, pid, qam), cap, tx, L, offs = _late_frames_capture(F)
     rxo = Receiver(RxParams(M=M, cp_len=cp, num_streams=N, num_access_codes=nac, pid_max=pid,
                             detector=_lib.DET_ZF2, qam_order=qam))
     sym = torch.zeros((F, N, pid, M), dtype=torch.complex64, device="cuda")
@@ -720,6 +759,44 @@ def test_two_phase_screen_finds_late_frames():
         assert evm_delta(ours, o.symbols()[:pid]) <= SYM_TOL, f
         late += 1 if f > 0 else 0
     assert synced >= 2 and late >= 1
+
+
+def test_two_phase_screen_equals_one_pass():
+    """Early, late and frame-less captures in one batch: the two-phase S&C (engine.cpp
+    run_sync) returns what one pass over every chunk returns (RMIMO_SC_PHASES=1, read once per
+    process: a child interpreter), bit for bit, on every call -- direct launches, the captured
+    graph and its replay. A capture without a frame reports zeros in the fields the estimation
+    stages fill in (the first call of a process whose device memory held other data: those
+    fields used to keep the slot's previous contents)."""
+    import subprocess
+    import sys
+    import tempfile
+    runs = _late_frames_run()
+    for r in runs[1:]:
+        _same_runs(runs[0], r)
+    res = runs[0][1]
+    st = [int(r["status"]) for r in res]
+    assert st[5] == _lib.FRAME_NO_SYNC
+    assert float(res[5]["noise_var"]) == 0.0 and not np.any(res[5]["plateau_start"])
+    assert sum(1 for f in (1, 2, 3, 4) if st[f] == _lib.FRAME_OK) >= 2, st
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    with tempfile.TemporaryDirectory() as td:
+        dst = os.path.join(td, "one_pass.npz")
+        code = ("import sys; sys.path.insert(0, %r); sys.path.insert(0, %r)\n"
+                "import numpy as np, test_gpu as t\n"
+                "sym, res = t._late_frames_run(calls=1)[0]\n"
+                "flat = {'sym': sym}\n"
+                "for f, r in enumerate(res):\n"
+                "    for k, v in r.items(): flat['%%d_%%s' %% (f, k)] = v\n"
+                "np.savez(%r, **flat)\nprint('one pass ok')\n"
+                % (root, os.path.join(root, "tests"), dst))
+        env = dict(os.environ, RMIMO_SC_PHASES="1")
+        out = subprocess.run([sys.executable, "-c", code], env=env, cwd=root, timeout=100,
+                             capture_output=True, text=True)
+        assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-4000:]
+        z = np.load(dst)
+        one = (z["sym"], [{k: z["%d_%s" % (f, k)] for k in r} for f, r in enumerate(res)])
+    _same_runs(runs[0], one)
 
 
 def test_captures_starting_at_the_frame_origin():
