@@ -453,9 +453,14 @@ int run_sync(mimo_rx *h, const float2 *iq, uint64_t stride, uint32_t F, uint64_t
       // was evaluated) and phase 2 evaluates exactly the chunks one pass would have for the
       // others, so results are those of one pass; the screen's reads of antenna 0 past the
       // trigger of a synced capture are skipped. RMIMO_SC_PHASES=1: one pass.
+      // Phase 1 ends one chunk past the S0 pair of a frame that starts its capture as the
+      // reference's tx_worker lays frames out (main.cc:937-1153: SL (N nac + 1) + u zeros,
+      // u < SL, then the two S0 symbols), the M-sample metric delay included.
       static const bool one_phase = [] { const char *e = getenv("RMIMO_SC_PHASES"); return e && e[0] == '1'; }();
+      const uint64_t s0_end = (uint64_t)h->SL * ((uint64_t)h->N * h->nac + 4) + h->M;
       const uint64_t c1 = (!stream && chunk_lo == 0 && !one_phase && nchunks >= 16)
-                              ? std::max<uint64_t>(2, nchunks / 8) : nchunks;
+                              ? std::min<uint64_t>(nchunks, std::max<uint64_t>(2, (s0_end + K - 1) / K + 1))
+                              : nchunks;
       sa.chunk_hi = c1;
       launch_sc_screen(sa, F, s);
       ScArgs a1 = a;
