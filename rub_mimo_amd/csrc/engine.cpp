@@ -447,7 +447,7 @@ int run_sync(mimo_rx *h, const float2 *iq, uint64_t stride, uint32_t F, uint64_t
       // capture may begin mid-stream after a trim (its history is not empty)
       sa.empty_history = reset_trig ? 1u : 0u;
       if (a.diag & 32) a.diag |= 16;   // diagnostics: finalize as a separate kernel
-      // Two phases for one frame per capture: the first eighth of every capture's chunks (a
+      // Two phases for one frame per capture: the first chunks of every capture (a
       // frame's S0 plateau sits near its capture's start), then the rest only for captures with
       // no trigger yet. A trigger found in phase 1 is the capture's first (every earlier chunk
       // was evaluated) and phase 2 evaluates exactly the chunks one pass would have for the

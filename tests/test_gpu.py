@@ -727,7 +727,7 @@ def _same_runs(a, b):
 
 
 def test_two_phase_screen_finds_late_frames():
-    """The S&C screen runs in two phases (the first eighth of every capture's chunks, then the
+    """The S&C screen runs in two phases (every capture's chunks through a leading frame's S0, then the
     rest for captures with no trigger yet). Frames placed past the first phase -- at 30%, 55%
     and 80% of a noisy capture -- sync exactly as the oracle does on the whole capture, beside
     one early frame; symbols within the EVM tolerance."""
