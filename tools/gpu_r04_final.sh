@@ -4,15 +4,21 @@
 set -o pipefail
 R=$(cd "$(dirname "$0")/.." && pwd)
 tag=${1:-r04}
+part=${2:-all}          # all | bench (tests + bench lines) | prof (PMC, stats, CFO)
 O=$R/gpurun_out/$tag
 mkdir -p $O
 cd $R
+if [ $part != prof ]; then
 timeout -k 10 500 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/gpu_tests.log 2>&1 || { echo "gpu tests failed"; tail -30 $O/gpu_tests.log; exit 1; }
 tail -1 $O/gpu_tests.log
+timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $O/smoke.log 2>&1 || { echo "smoke failed"; tail -20 $O/smoke.log; exit 1; }
+tail -1 $O/smoke.log
 timeout -k 10 300 python bench.py > $O/bench_c3.json 2> $O/bench_c3.err || { echo "bench c3 failed"; tail -20 $O/bench_c3.err; exit 1; }
 for w in c2 c4 c5; do
   timeout -k 10 200 python bench.py --workload $w --cpu-baseline 0 > $O/bench_$w.json 2> $O/bench_$w.err || { echo "bench $w failed"; tail -20 $O/bench_$w.err; exit 1; }
 done
+fi
+[ $part = bench ] && exit 0
 export PMC_KERNEL="decode|spectra|apply_split"
 for w in c3 c4; do
   "$R/tools/pmc_run.sh" "${tag}_${w}_fetch" "FETCH_SIZE" --workload $w || exit 1
