@@ -1435,10 +1435,11 @@ MIMO_DEV void tr_reduce_step(float *v, int lane) {
 }
 
 // block sums of antenna 0 over a span, the screen test, and the chunk list
-template <bool S>
+template <bool S, int SPAN>
 __global__ __launch_bounds__(kScrT) __attribute__((amdgpu_waves_per_eu(6))) void sc_screen_kernel(ScreenArgs a) {
   constexpr int B = kScrB;
-  __shared__ float4 recs[kScrSpan / B + 2 * (kScrMaxD)];
+  static_assert(SPAN <= kScrSpan && SPAN % (kScrB * kScrBPI * (kScrT / 64)) == 0, "screen span");
+  __shared__ float4 recs[SPAN / B + 2 * (kScrMaxD)];
   // per chunk the test can touch (chunk_len >= kScrSpan / 2: at most three), the first and last
   // unproven position, gathered before the global list update
   constexpr int kScrChunks = 4;
@@ -1455,9 +1456,9 @@ __global__ __launch_bounds__(kScrT) __attribute__((amdgpu_waves_per_eu(6))) void
                                                    (int64_t)(a.chunk_hi * a.chunk_len))
                                : (int64_t)a.frame_len;   // end of this phase's positions
   const int64_t LF = (int64_t)a.frame_len;
-  const int64_t q0 = (int64_t)a.chunk_lo * (int64_t)a.chunk_len + (int64_t)blockIdx.x * kScrSpan;
+  const int64_t q0 = (int64_t)a.chunk_lo * (int64_t)a.chunk_len + (int64_t)blockIdx.x * SPAN;
   if (q0 >= L) return;
-  const int NB = kScrSpan / B + 2 * D;
+  const int NB = SPAN / B + 2 * D;
   const int64_t h0 = q0 - (int64_t)2 * D * B;     // first block of the history
   const auto x = iq_row<S>(a.iq, a.iq_scale, (uint64_t)f * a.N * a.stride);   // antenna 0
   const bool vec = x.pair_ok();
@@ -2080,12 +2081,23 @@ void launch_sc_screen(const ScreenArgs &a, uint32_t n_frames, hipStream_t s) {
   const uint64_t end = a.chunk_hi ? std::min<uint64_t>(a.frame_len, a.chunk_hi * a.chunk_len)
                                   : (uint64_t)a.frame_len;
   const uint64_t span = end - std::min<uint64_t>(end, a.chunk_lo * a.chunk_len);
-  const uint32_t gx = (uint32_t)((span + kScrSpan - 1) / kScrSpan);
+  // positions per workgroup: 8192 up to M = 2048 (twice the workgroups; a phase-1 screen of
+  // 64 C3 captures is ~830 workgroups at 16384, under one per SIMD), 16384 above (the 2D-block
+  // history, M positions, would be half of an 8192 span); RMIMO_SCR_SPAN=8192 | 16384 forces one
+  static const int span_env = [] { const char *e = getenv("RMIMO_SCR_SPAN"); return e ? atoi(e) : 0; }();
+  const int sp = span_env == 8192 ? 8192 : span_env == 16384 ? kScrSpan : a.M <= 2048 ? 8192 : kScrSpan;
+  const uint32_t gx = (uint32_t)((span + sp - 1) / sp);
   if (!gx) return;
-  if (a.sc16)
-    hipLaunchKernelGGL(sc_screen_kernel<true>, dim3(gx, n_frames), dim3(kScrT), 0, s, a);
-  else
-    hipLaunchKernelGGL(sc_screen_kernel<false>, dim3(gx, n_frames), dim3(kScrT), 0, s, a);
+  if (sp == 8192) {
+    if (a.sc16)
+      hipLaunchKernelGGL((sc_screen_kernel<true, 8192>), dim3(gx, n_frames), dim3(kScrT), 0, s, a);
+    else
+      hipLaunchKernelGGL((sc_screen_kernel<false, 8192>), dim3(gx, n_frames), dim3(kScrT), 0, s, a);
+  } else if (a.sc16) {
+    hipLaunchKernelGGL((sc_screen_kernel<true, kScrSpan>), dim3(gx, n_frames), dim3(kScrT), 0, s, a);
+  } else {
+    hipLaunchKernelGGL((sc_screen_kernel<false, kScrSpan>), dim3(gx, n_frames), dim3(kScrT), 0, s, a);
+  }
 }
 
 void launch_sc_exact(const ScArgs &a, hipStream_t s) {
