@@ -710,7 +710,7 @@ void search_ls_wave_kernel(SearchArgs a) {
     for (int e = 0; e < 8; e++) {
       const uint32_t k = (uint32_t)reg_index<LOG2M, 8>((int)lt, e);
       const float sgn = (float)sg[k];
-      q[k] = xw[e] * v2f{sgn, sgn};
+      __builtin_nontemporal_store(xw[e] * v2f{sgn, sgn}, &q[k]);   // read once, by the combine
     }
     return;
   } else {
@@ -804,8 +804,10 @@ __global__ __launch_bounds__(256) void ls_combine_q_kernel(LsArgs a) {
     for (uint32_t c0 = 0; c0 < a.nac; c0 += CB) {
       float2 vb[CB];
 #pragma unroll
-      for (uint32_t j = 0; j < CB; j++)
-        vb[j] = q[(uint64_t)min(c0 + j, a.nac - 1) * M];   // clamped: every load unconditional
+      for (uint32_t j = 0; j < CB; j++) {   // clamped: every load unconditional; read once
+        const v2f t = __builtin_nontemporal_load(reinterpret_cast<const v2f *>(q) + (uint64_t)min(c0 + j, a.nac - 1) * M);
+        vb[j] = make_float2(t.x, t.y);
+      }
 #pragma unroll
       for (uint32_t j = 0; j < CB; j++) {
         const uint32_t c = c0 + j;
