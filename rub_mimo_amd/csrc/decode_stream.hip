@@ -389,7 +389,7 @@ MIMO_DEV void dma16(uint32_t voff, __attribute__((address_space(1))) const void 
   // s_nop 4 first: sbase may come straight from a v_readfirstlane (VALU-written SGPR read as
   // a VMEM base needs wait states the compiler does not insert inside an asm statement)
   asm volatile("s_nop 4\n\ts_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t"
-               "global_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
+               "global_load_lds_dwordx4 %1, %2 nt\n\ts_mov_b32 m0, %0"
                : "=&s"(keep) : "v"(voff), "s"(sbase), "s"(lds) : "memory");
 }
 
@@ -1065,9 +1065,12 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
         const uint32_t d0 = finish(t, 0, kb, y0);
         const uint32_t d1 = finish(t, 1, kb + 1, y1);
 #ifndef DS_ABL_NOSTORE   // timing ablation: no symbol / index stores
+        // (outputs are written once and not read back here: non-temporal stores)
         if constexpr (OUTS & 1)
-          *(gptr<v4f>)((gptr<char>)osym + kb * (uint32_t)sizeof(v2f)) = v4f{y0.x, y0.y, y1.x, y1.y};
-        if constexpr (OUTS & 2) *(gptr<uint16_t>)((gptr<char>)oidx + kb) = (uint16_t)(d0 | (d1 << 8));
+          __builtin_nontemporal_store(v4f{y0.x, y0.y, y1.x, y1.y},
+                                      (gptr<v4f>)((gptr<char>)osym + kb * (uint32_t)sizeof(v2f)));
+        if constexpr (OUTS & 2)
+          __builtin_nontemporal_store((uint16_t)(d0 | (d1 << 8)), (gptr<uint16_t>)((gptr<char>)oidx + kb));
 #endif
       }
     } else {
@@ -1098,8 +1101,8 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
           const uint32_t d = finish(t, q, k, acc);
 #ifndef DS_ABL_NOSTORE   // timing ablation: no symbol / index stores
           if constexpr (OUTS & 1)
-            *(gptr<v2f>)((gptr<char>)osym + k * (uint32_t)sizeof(v2f)) = acc;
-          if constexpr (OUTS & 2) oidx[k] = (uint8_t)d;
+            __builtin_nontemporal_store(acc, (gptr<v2f>)((gptr<char>)osym + k * (uint32_t)sizeof(v2f)));
+          if constexpr (OUTS & 2) __builtin_nontemporal_store((uint8_t)d, &oidx[k]);
 #endif
         }
       }
@@ -1502,6 +1505,7 @@ __global__ __launch_bounds__(64 * NA) void apply_split2_kernel(DecodeArgs a) {
       e_den = __builtin_fmaf(pt.x, pt.x, __builtin_fmaf(pt.y, pt.y, e_den));
     }
     const uint64_t o = (((uint64_t)f * NA + w) * a.max_out + s) * a.M_occ + kb;
+    // (plain stores: non-temporal ones measured +3.7% on this kernel at C4)
     if (a.out_sym)
       *reinterpret_cast<v4f *>(reinterpret_cast<v2f *>(a.out_sym) + o) =
           v4f{acc[0].x, acc[0].y, acc[1].x, acc[1].y};
