@@ -1190,6 +1190,46 @@ void ref_framesync_get_cfo(const ref_framesync *fs, double *eps2) {
   eps2[1] = fs->cfo_delta;
 }
 
+/* Test helper (not a reference entry point): advance a fresh framesync over samples [0, p0)
+ * with the S&C state updates of framing.cc:626-637 (window ring, wdelaycf read-before-push,
+ * the two firfilt histories) but without the per-sample dot products and the plateau rule on
+ * samples [0, p0 - 1); sample p0 - 1 then runs through execute_sc_sync in full. The metric of
+ * every later sample depends only on those histories, so it equals the full run's bit for bit.
+ * The plateau state at p0 equals the full run's when no antenna is in a run after sample
+ * p0 - 1 (its y at or below the threshold), which is checked (-2 otherwise): a run open at
+ * p0 - 1 would carry a start this walk never saw. What it cannot see is a trigger before p0,
+ * which the full run would have taken; callers start p0 where the capture holds no frame. */
+int ref_framesync_fast_forward(ref_framesync *fs, const ref_cf32 *const *in, uint64_t p0) {
+  if (fs->state != REF_STATE_SEEK_PLATEAU || fs->nsp != 0 || p0 == 0 || fs->cfg.trace_sc) return -1;
+  ref_cf32 x[64];
+  const uint32_t M = fs->M, M2 = fs->M2;
+  for (uint64_t i = 0; i + 1 < p0; i++) {
+    for (uint32_t s = 0; s < fs->N; s++) x[s] = in[s][i];
+    win_push(fs, x);
+    for (uint32_t s = 0; s < fs->N; s++) {
+      ref_cf32 *dly = fs->dly + (size_t)s * M2, *xc = fs->xc + (size_t)s * M2;
+      float *nz = fs->nz + (size_t)s * M;
+      const ref_cf32 d = dly[fs->dly_pos];
+      dly[fs->dly_pos] = x[s];
+      ref_cf32 pv;
+      pv.re = d.re * x[s].re - (-d.im) * x[s].im;
+      pv.im = d.re * x[s].im + (-d.im) * x[s].re;
+      xc[fs->xc_pos] = pv;
+      nz[fs->nz_pos] = x[s].re * x[s].re + x[s].im * x[s].im;
+    }
+    fs->dly_pos = (fs->dly_pos + 1) % M2;
+    fs->xc_pos = (fs->xc_pos + 1) % M2;
+    fs->nz_pos = (fs->nz_pos + 1) % M;
+    fs->nsp++;
+  }
+  for (uint32_t s = 0; s < fs->N; s++) x[s] = in[s][p0 - 1];
+  execute_sc_sync(fs, x);
+  fs->nsp++;
+  for (uint32_t s = 0; s < fs->N; s++)
+    if (fs->in_plateau[s]) return -2;
+  return fs->state == REF_STATE_SEEK_PLATEAU ? 0 : -2;
+}
+
 /* CPU-baseline helper (not a reference entry point): put a fresh framesync in the state the
  * plateau rule leaves it in when it fires at sample `trigger` with `sync_index`
  * (framing.cc:617-623): the window ring holds samples up to `trigger` (zeros before 0), the

@@ -134,6 +134,7 @@ void     ref_framesync_destroy(ref_framesync *fs);
 int      ref_framesync_execute(ref_framesync *fs, const ref_cf32 *const *in, uint32_t n);
 void     ref_framesync_reset(ref_framesync *fs);
 /* CPU-baseline helper: state after the plateau rule fired at `trigger` (see mimo_ref.c) */
+int      ref_framesync_fast_forward(ref_framesync *fs, const ref_cf32 *const *in, uint64_t p0);
 int      ref_framesync_skip_to_sync(ref_framesync *fs, const ref_cf32 *const *in,
                                     uint64_t trigger, uint64_t sync_index);
 uint64_t ref_framesync_get_sync_index(const ref_framesync *fs);

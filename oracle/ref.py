@@ -73,6 +73,7 @@ def lib():
             "ref_framesync_get_phase_times": (None, [vp, f64p]),
             "ref_framesync_get_cfo": (None, [vp, f64p]),
             "ref_framesync_skip_to_sync": (C.c_int, [vp, vp, C.c_uint64, C.c_uint64]),
+            "ref_framesync_fast_forward": (C.c_int, [vp, vp, C.c_uint64]),
             "ref_sc_metric_at": (C.c_float, [vp, C.c_uint64, C.c_uint32]),
             "ref_demap_evm": (None, [vp, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32,
                                      u8p, u8p, f64p, f64p, u64p]),
@@ -283,6 +284,17 @@ class FrameSyncRef:
         if lib().ref_framesync_skip_to_sync(self._h, ptrs, int(trigger), int(sync_index)) != 0:
             raise RuntimeError("skip_to_sync needs a fresh framesync")
         return self.execute([r[int(trigger) + 1:] for r in rx])
+
+    def execute_from(self, rx, p0):
+        """Test helper: S&C state advanced over samples [0, p0) without the per-sample dot
+        products (ref_framesync_fast_forward: the metric from p0 on equals the full scan's bit
+        for bit; no plateau run may be open at p0 - 1), then execute(rx[:, p0:])."""
+        rx = [np.ascontiguousarray(r, np.complex64) for r in rx]
+        ptrs = (C.c_void_p * self.N)(*[r.ctypes.data for r in rx])
+        rc = lib().ref_framesync_fast_forward(self._h, ptrs, int(p0))
+        if rc != 0:
+            raise RuntimeError("fast_forward(%d) refused: %d" % (p0, rc))
+        return self.execute([r[int(p0):] for r in rx])
 
     def cfo(self):
         """(eps0, delta) of the last estimate (cfo_mode != 0), subcarrier spacings."""

@@ -392,6 +392,24 @@ MIMO_DEV void dma16(uint32_t voff, __attribute__((address_space(1))) const void 
                "global_load_lds_dwordx4 %1, %2 nt\n\ts_mov_b32 m0, %0"
                : "=&s"(keep) : "v"(voff), "s"(sbase), "s"(lds) : "memory");
 }
+// cache prefetch: one dword per lane by LDS-DMA into a scratch word block nobody reads (no
+// VGPR is written, so nothing waits for it but the issuing wave's own counted vmcnt); each
+// lane touches one 128-byte line, which the L2 then holds for the staging DMA that follows
+MIMO_DEV void pf_line(uint32_t voff, __attribute__((address_space(1))) const void *sbase, uint32_t lds) {
+  uint32_t keep;
+  asm volatile("s_nop 4\n\ts_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t"
+               "global_load_lds_dword %1, %2\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(voff), "s"(sbase), "s"(lds) : "memory");
+}
+// DS_PF (experiment, off by default): 1 = the waves with no staging DMA of their own prefetch
+// the next symbol's rows into L2 at the top of this symbol; 2 = they prefetch the symbol after
+// the next at the staging point
+#ifndef DS_PF
+#define DS_PF 0
+#endif
+#ifndef DS_PROF_TID
+#define DS_PROF_TID 0
+#endif
 
 constexpr size_t kStreamStaticLds = 8192;   // pfx, fbody, fcr, ptab, gidx, cpe_part, cfo_tab (+ slack)
 
@@ -420,8 +438,9 @@ constexpr bool stream_wave_fft() {
 
 // CPE (opt-in CFO path): per-symbol common phase, decision directed and non-recursive. The
 // residual frequency offset left by the CFO estimate turns every symbol by a slowly growing
-// angle. Each symbol measures its own: c = sum over stream 0's outputs y of conj(Q(y)) y
-// (Q the hard decision's constellation point), reduced over the workgroup in a fixed order,
+// angle. Each symbol measures its own: c = sum of conj(Q(y)) y over every stream's outputs y
+// at the subcarriers k with k even and bit 9 of k clear (Q the hard decision's constellation
+// point; oracle cfo_common_phase), reduced over the workgroup in a fixed order,
 // and every output of the symbol is turned by conj(c)/|c| before its decision, EVM and
 // stores. Nothing carries from one symbol to the next, so a symbol's outputs are a function
 // of the frame alone, not of where a workgroup's range starts (oracle/mimo_ref.c restates it,
@@ -606,6 +625,33 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
         const uint32_t t = (uint32_t)tr / (M / 16), q = (uint32_t)tr % (M / 16);
         const auto rb = sgpr_ptr(a.ref_idx + fb.ref + (uint64_t)ss * a.M_occ);
         dma16(t * (uint32_t)(a.max_out * a.M_occ) + 16 * q, rb, dst);
+      }
+    }
+  };
+  // prefetch waves (DS_PF): the first NA waves after the row and reference waves, one row each
+  constexpr int PFW0 = RW0 + (REF == 1 ? NREF / 64 : 0);
+  constexpr bool PF = DS_PF != 0 && !SC16 && DS_ROW_DMA && PFW0 + NA <= T / 64;
+  constexpr int NPFI = (M * SB + 128 + 64 * 128 - 1) / (64 * 128);   // prefetch instructions per row
+  __shared__ uint32_t pf_junk[PF ? 64 : 1];
+  const bool pf_wave = PF && wv >= (uint32_t)PFW0 && wv < (uint32_t)(PFW0 + NA);
+  auto prefetch = [&](const FrameBase &fb, uint32_t ss) {
+    if constexpr (PF) {
+      if (pf_wave) {
+        const int64_t abs0 = fb.body + (int64_t)((uint64_t)ss * a.SL);
+        if (abs0 >= 0 && abs0 + M <= (int64_t)a.frame_len) {
+          const uint32_t g = wv - PFW0;
+          const int64_t byte0 = (fb.row0 + abs0 + (int64_t)g * a.stride) * SB;
+          const int64_t line0 = byte0 & ~(int64_t)127;
+          const uint32_t span = (uint32_t)(byte0 + M * SB - line0);
+          const auto xa = sgpr_ptr(reinterpret_cast<const char *>(a.iq) + line0);
+          const uint32_t lane = (uint32_t)(opq(tid) & 63);
+          const uint32_t dst = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)pf_junk);
+#pragma unroll
+          for (int j = 0; j < NPFI; j++) {
+            const uint32_t o = ((uint32_t)j * 64u + lane) * 128u;
+            if (o < span) pf_line(o, xa, dst);
+          }
+        }
       }
     }
   };
@@ -812,9 +858,22 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
     // this symbol's staging has landed (the previous symbol's stores may still be in flight)
     MARK(";@@A top");
     DSP(const unsigned long long ds_0 = __builtin_amdgcn_s_memtime(); ds_t[4] += ds_0 - ds_c;)
-    asm volatile("s_waitcnt vmcnt(%0)" :: "n"(NSTORE) : "memory");
+    if (DS_PF == 2 && pf_wave) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(NSTORE + NPFI) : "memory");
+    else asm volatile("s_waitcnt vmcnt(%0)" :: "n"(NSTORE) : "memory");
     __syncthreads();
     DSP(const unsigned long long ds_1 = __builtin_amdgcn_s_memtime(); ds_t[1] += ds_1 - ds_0;)
+    if constexpr (PF && DS_PF == 1) {   // the next symbol's rows into L2 now
+      if (i + 1 < i_end) {
+        uint32_t f1 = f, s1 = s + 1;
+        FrameBase fb1 = fbase;
+        if (s1 >= n_out_f) {
+          do { f1++; } while (pfx[f1 + 1] == pfx[f1]);
+          s1 = 0;
+          fb1 = frame_base(__builtin_amdgcn_readfirstlane(f1));
+        }
+        prefetch(fb1, __builtin_amdgcn_readfirstlane(s1));
+      }
+    }
     v2f v[8];
     {
       const int t0 = opq(tid);
@@ -900,6 +959,18 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
       sn = __builtin_amdgcn_readfirstlane(sn);
       n_out_n = __builtin_amdgcn_readfirstlane(n_out_n);
       odd_n = fetch(fbase_n, sn);
+      if constexpr (PF && DS_PF == 2) {   // the symbol after the next one into L2
+        if (i + 2 < i_end) {
+          uint32_t f2 = fn, s2 = sn + 1;
+          FrameBase fb2 = fbase_n;
+          if (s2 >= n_out_n) {
+            do { f2++; } while (pfx[f2 + 1] == pfx[f2]);
+            s2 = 0;
+            fb2 = frame_base(__builtin_amdgcn_readfirstlane(f2));
+          }
+          prefetch(fb2, __builtin_amdgcn_readfirstlane(s2));
+        }
+      }
     }
     // passes 1 .. NP-1 through the LDS images (pass 1 needs no leading barrier: the previous
     // symbol's image readers finished before the barrier at the top), then the exchange that
@@ -1126,7 +1197,7 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
     odd = __builtin_amdgcn_readfirstlane(odd_n);
     fbase = fbase_n;
   }
-  DSP(if (a.prof && threadIdx.x == 0) {
+  DSP(if (a.prof && threadIdx.x == DS_PROF_TID) {
     for (int q = 0; q < 8; q++) atomicAdd(&a.prof[q], ds_t[q]);
   })
 }
@@ -1730,6 +1801,9 @@ __global__ __launch_bounds__(kR8T) void decode_res8_kernel(DecodeArgs a) {
       }
       a.evm_part[(((uint64_t)ff * a.rec_stride + jrec) * (T / 64) + wv) * NA * 3 + lane] = (double)v;
     }
+    // the table spans both images: every wave's reads of it before the next symbol's pass 0
+    // writes an image (the next pair is already in registers, so pass 0 follows at once)
+    __syncthreads();
   };
 
   // the samples of antenna pair j of symbol (ff, ss): x_g[n + 512 r], r < 8 (the row of

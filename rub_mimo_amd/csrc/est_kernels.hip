@@ -702,15 +702,18 @@ void search_ls_wave_kernel(SearchArgs a) {
     if (!valid) return;                               // uniform per wave
     const uint32_t ac = s0 + u - 1, code = ac / a.N, tx = ac % a.N;
     // (code row bases uniform per wave: SGPR pointers, 32-bit lane offsets; X S1 as a product
-    // with the sign: exact for +-1, and a null subcarrier's 0 term is dropped by the combine)
+    // with the sign, exact for +-1; a null subcarrier's term is an exact +0, as the unfused
+    // ls_kernel writes it, whatever X holds)
     const auto sg = sgpr_ptr(a.s1sign + ((size_t)tx * a.nac + code) * M);
     const auto q = sgpr_ptr(reinterpret_cast<v2f *>(a.lsq) +
                             ((((uint64_t)f * a.N + r) * a.N + tx) * a.nac + code) * M);
 #pragma unroll
     for (int e = 0; e < 8; e++) {
       const uint32_t k = (uint32_t)reg_index<LOG2M, 8>((int)lt, e);
-      const float sgn = (float)sg[k];
-      __builtin_nontemporal_store(xw[e] * v2f{sgn, sgn}, &q[k]);   // read once, by the combine
+      const int8_t sv = sg[k];
+      const float sgn = (float)sv;
+      const v2f term = sv ? xw[e] * v2f{sgn, sgn} : v2f{0.0f, 0.0f};
+      __builtin_nontemporal_store(term, &q[k]);   // read once, by the combine
     }
     return;
   } else {

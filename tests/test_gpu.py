@@ -479,7 +479,7 @@ def test_framegen_matches_oracle_tx():
 
 
 def _c_frame_parity(M, cp, N, nac, pid, qam, det, snr, seed, bias=True, max_delta=SYM_TOL,
-                    search_mode=0, path=None, out_idx=False):
+                    search_mode=0, path=None, out_idx=False, ff_margin=None):
     S = Synthesizer(SynthParams(M=M, cp_len=cp, num_streams=N, num_access_codes=nac, pid=pid,
                                 qam_order=qam, seed=seed, snr_db=snr))
     L = S.frame_len(0)
@@ -501,7 +501,16 @@ def _c_frame_parity(M, cp, N, nac, pid, qam, det, snr, seed, bias=True, max_delt
     ci, si = rxo.corr()
     o = ref.FrameSyncRef(M, cp, N, nac, pid_max=pid, detector=det, keep_identity_bias=bias,
                          trace_corr=True, search_mode=search_mode)
-    assert o.execute(rx) == ref.STATE_MIMO
+    if ff_margin is None:
+        assert o.execute(rx) == ref.STATE_MIMO
+    else:
+        # full-size frames: the oracle's S&C histories advanced without the dot products to
+        # ff_margin samples before the earliest plateau the GPU reported (the metric from there
+        # on is the full scan's bit for bit, ref_framesync_fast_forward; the oracle refuses a
+        # start inside a plateau run), then its own plateau rule, search, LS and decode
+        p0 = min(r["plateau_start"][:N]) - ff_margin
+        assert p0 > 0
+        assert o.execute_from(rx, p0) == ref.STATE_MIMO
     assert r["status"] == _lib.FRAME_OK
     assert r["sync_index"] == o.get_sync_index()
     assert r["plateau_start"] == [o.get_plateau_start(s) for s in range(N)]
@@ -849,6 +858,22 @@ def test_c4_full_codes_against_parseval_oracle():
     wherever the peak is unambiguous, symbols within the EVM tolerance."""
     _c_frame_parity(4096, 304, 8, 20, 12, 256, _lib.DET_MMSE, 35.0, seed=43, bias=False,
                     search_mode=1)
+
+
+def test_c4_full_frame_split_decode_against_parseval_oracle():
+    """BASELINE config C4 at full size: 8x8 MMSE, M 4096, 256-QAM, all 20 access codes per
+    stream, PID 1000, through the production split decode (path asserted). The oracle runs the
+    Parseval search variant (search_mode 1, pinned to the brute force by test_oracle) and
+    starts its S&C scan two symbols before the earliest plateau (test_oracle::
+    test_fast_forward_equals_full_run; the full scan of the 700k-sample prefix on 8 antennas
+    is ~75 s of CPU, and test_c4_full_codes_against_parseval_oracle runs it on the same frame
+    layout). Sync, plateau starts and samples processed bit-exact, corr indices exact where
+    the peak is unambiguous, all 1000 symbols within the EVM tolerance, indices and
+    symbol-error counts up to boundary decisions, EVM-dB within 1e-3 dB."""
+    d, e = _c_frame_parity(4096, 304, 8, 20, 1000, 256, _lib.DET_MMSE, 35.0, seed=44, bias=False,
+                           search_mode=1, path=_lib.DECODE_SPLIT, out_idx=True,
+                           ff_margin=2 * (4096 + 304))
+    assert np.median(e) < -20
 
 
 @pytest.mark.parametrize("det", [_lib.DET_ZF, _lib.DET_MMSE])

@@ -188,6 +188,34 @@ def test_execute_from_sync_equals_full_run(path):
     assert np.array_equal(fs.symbols(), full.symbols())
 
 
+@pytest.mark.parametrize("path", GOLDEN, ids=[os.path.basename(p) for p in GOLDEN])
+def test_fast_forward_equals_full_run(path):
+    """Test helper for full-size frames (ref_framesync_fast_forward): the S&C histories
+    advanced without the dot products up to p0, then the full path, gives the full run's
+    plateau starts, sync index, samples processed, corr indices, G and symbols bit for bit;
+    a p0 inside a plateau run is refused."""
+    g = load(path)
+    full = run_oracle(g)
+    N = int(g["N"])
+    kw = dict(pid_max=int(g["pid"]), detector=int(g["detector"]),
+              keep_identity_bias=bool(g["keep_identity_bias"]), p=g["p"],
+              siso_tx=int(g["siso_tx"]), siso_rx=int(g["siso_rx"]))
+    trig = _trigger_of(g)
+    starts = [full.get_plateau_start(s) for s in range(N)]
+    for p0 in (1, min(starts) // 2, min(starts) - 3):
+        fs = ref.FrameSyncRef(int(g["M"]), int(g["cp"]), N, int(g["nac"]), **kw)
+        assert fs.execute_from(g["rx"], p0) == ref.STATE_MIMO
+        assert fs.get_sync_index() == full.get_sync_index()
+        assert [fs.get_plateau_start(s) for s in range(N)] == starts
+        assert fs.get_num_samples_processed() == full.get_num_samples_processed()
+        assert (fs.get_corr()[0] == full.get_corr()[0]).all()
+        assert np.array_equal(fs.get_G(), full.get_G())
+        assert np.array_equal(fs.symbols(), full.symbols())
+    fs = ref.FrameSyncRef(int(g["M"]), int(g["cp"]), N, int(g["nac"]), **kw)
+    with pytest.raises(RuntimeError):
+        fs.execute_from(g["rx"], trig)          # every antenna is in its plateau there
+
+
 def _trigger_of(g):
     """First sample where every antenna's plateau is longer than cp (framing.cc:617-623),
     from the oracle's S&C trace."""
