@@ -443,33 +443,12 @@ MIMO_DEV void dma16(uint32_t voff, __attribute__((address_space(1))) const void 
                "global_load_lds_dwordx4 %1, %2 nt\n\ts_mov_b32 m0, %0"
                : "=&s"(keep) : "v"(voff), "s"(sbase), "s"(lds) : "memory");
 }
-// cache prefetch: one dword per lane by LDS-DMA into a scratch word block nobody reads (no
-// VGPR is written, so nothing waits for it but the issuing wave's own counted vmcnt); each
-// lane touches one 128-byte line, which the L2 then holds for the staging DMA that follows
-MIMO_DEV void pf_line(uint32_t voff, __attribute__((address_space(1))) const void *sbase, uint32_t lds) {
-  uint32_t keep;
-  asm volatile("s_nop 4\n\ts_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t"
-               "global_load_lds_dword %1, %2\n\ts_mov_b32 m0, %0"
-               : "=&s"(keep) : "v"(voff), "s"(sbase), "s"(lds) : "memory");
-}
-// DS_PF (experiment, off by default): 1 = the waves with no staging DMA of their own prefetch
-// the next symbol's rows into L2 at the top of this symbol; 2 = they prefetch the symbol after
-// the next at the staging point
-#ifndef DS_PF
-#define DS_PF 0
-#endif
-// where the next symbol's staging DMA is issued (experiment): 0 after pass 0's barrier, 1 after
-// the issuing wave's sub-transforms, 2 after the barrier that ends them
-#ifndef DS_DMA_AT
-#define DS_DMA_AT 0
-#endif
 #ifndef DS_PROF_TID
 #define DS_PROF_TID 0
 #endif
-// output stores non-temporal from this transform size up (the outputs are written once and
-// read by the caller; below it plain stores)
-#ifndef DS_NTST_MIN_LOG2M
-#define DS_NTST_MIN_LOG2M 10
+// index stores non-temporal from this transform size up (see NTI)
+#ifndef DS_NTI_MIN_LOG2M
+#define DS_NTI_MIN_LOG2M 11
 #endif
 template <bool NT, typename V, typename P>
 MIMO_DEV void out_store(V v, P p) {
@@ -481,12 +460,9 @@ constexpr size_t kStreamStaticLds = 8192;   // pfx, fbody, fcr, ptab, gidx, cpe_
 
 // dynamic LDS of the kernel: FFT images, staging, reference staging, twiddle table
 template <int LOG2M, int NA>
-constexpr size_t stream_dyn_lds(bool wave_fft, int ref_mode, bool sc16, bool db = false) {
+constexpr size_t stream_dyn_lds(bool wave_fft, int ref_mode, bool sc16) {
   using PL = StreamPlan<LOG2M, NA>;
   using WP = WavePlan<LOG2M, NA>;
-  if (db)   // two region images, the staging inside them (stream_db)
-    return sizeof(float2) * (2 * (size_t)NA * WP::GS + WP::TW0 + WP::TWS) +
-           (ref_mode == 1 ? (size_t)NA * PL::M : 0);
   size_t tw = 0;
   if (wave_fft) {
     tw = (size_t)WP::TW0 + WP::TWS;
@@ -503,25 +479,6 @@ constexpr size_t stream_dyn_lds(bool wave_fft, int ref_mode, bool sc16, bool db 
 template <int LOG2M, int NA, int REF, bool SC16>
 constexpr bool stream_wave_fft() {
   return LOG2M >= 11 && stream_dyn_lds<LOG2M, NA>(true, REF, SC16) + kStreamStaticLds <= 163840;
-}
-
-// Double-buffered in-place staging (DS_DB, the 4 x 2048 geometry of C3): two region images,
-// symbol s staged straight into the region layout of one while s - 1 is transformed in the
-// other, so the next symbol's staging DMA can be issued at the top of a symbol instead of
-// after pass 0 has read the one staging area. Row g's staged position P (body sample P - odd)
-// sits in region min(P / 256, 7) at slot P - 256 region (positions 2048, 2049: slots 256, 257
-// of region 7); pass 0 of thread (g, n) reads positions n + odd + 256 r and writes c_q[n] at
-// slot n + odd of region q -- the slots it read, except that thread 255 with odd = 1 reads
-// slot 0 of regions 1..7 (which no thread writes) and writes slot 256 (which only it reads):
-// no thread writes a slot another thread reads, so pass 0 needs no barrier between its reads
-// and its writes. The sub-transforms and the apply address every region from slot odd.
-#ifndef DS_DB
-#define DS_DB 0
-#endif
-template <int LOG2M, int NA, int REF, bool SC16, bool CPE>
-constexpr bool stream_db() {
-  return DS_DB && LOG2M == 11 && NA == 4 && !SC16 && !CPE &&
-         stream_dyn_lds<LOG2M, NA>(true, REF, false, true) + 6400 <= 163840;
 }
 
 // CPE (opt-in CFO path): per-symbol common phase, decision directed and non-recursive. The
@@ -567,17 +524,24 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
   // one S-byte index store per stream) on the wave-FFT layout, else k = tid + q T
   constexpr bool KADJ = WF && S == 2;
   constexpr int SPS = KADJ ? NA : NA * S;          // store instructions per output kind
-  constexpr int NSTORE = ((OUTS & 1) ? SPS : 0) + ((OUTS & 2) ? SPS : 0);
-  constexpr bool NTST = LOG2M >= DS_NTST_MIN_LOG2M;
-  constexpr bool DB = stream_db<LOG2M, NA, REF, SC16, CPE>() && KADJ;
-  static_assert(!DB || (WP::X256 && MS == 256 && RS == M + 2 && DS_ROW_DMA), "in-place staging: 256-point regions");
+#ifdef DS_ABL_NOIDX   // timing ablation: no index stores
+  constexpr int OUTX = OUTS & 1;
+#elif defined(DS_ABL_NOSYM)   // timing ablation: no symbol stores
+  constexpr int OUTX = OUTS & 2;
+#else
+  constexpr int OUTX = OUTS;
+#endif
+  constexpr int NSTORE = ((OUTX & 1) ? SPS : 0) + ((OUTX & 2) ? SPS : 0);
+  // output store policies (measured): symbols non-temporal everywhere (the
+  // captures of the next batch stay cached for its S&C); the uint8 indices non-temporal from
+  // M = 2048 up, plain below (C2: decode -6%, the next S&C unchanged; at C3 plain index stores
+  // cost the next S&C 15%)
+  constexpr bool NTS = true, NTI = LOG2M >= DS_NTI_MIN_LOG2M;
   extern __shared__ __attribute__((aligned(16))) float2 lds_raw[];
   v2f *img = reinterpret_cast<v2f *>(lds_raw);    // [NA][PB] FFT exchange ([NA][8][QS] if WF)
-  v2f *const img0 = img, *const img1 = img + (DB ? NA * GS : 0);   // (DB: the two images)
-  v2f *stg = DB ? img0 : img + NA * (WF ? GS : PB);                // [NA][RS] next symbol
+  v2f *stg = img + NA * (WF ? GS : PB);                            // [NA][RS] next symbol
   short2 *stg16 = reinterpret_cast<short2 *>(stg);                 // (sc16 staging)
-  uint8_t *rstg = DB ? reinterpret_cast<uint8_t *>(img1 + NA * GS)
-                     : reinterpret_cast<uint8_t *>(stg) + (size_t)NA * RS * SB;   // [NA][M] next references
+  uint8_t *rstg = reinterpret_cast<uint8_t *>(stg) + (size_t)NA * RS * SB;   // [NA][M] next references
   v2f *twl = reinterpret_cast<v2f *>(rstg + ((REF == 1) ? NA * M : 0));   // twiddle table
   __shared__ uint32_t pfx[kStreamMaxFrames + 1];
   __shared__ int64_t fbody[kStreamMaxFrames];
@@ -672,7 +636,7 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
   const v2f inv_sc = v2f{a.qam.inv_scale, a.qam.inv_scale};
   const v2f Lf = v2f{(float)a.qam.L, (float)a.qam.L};
   const uint32_t Lm1 = a.qam.L - 1;
-  [[maybe_unused]] const uint32_t stg_base = (uint32_t)(uintptr_t)stg;
+  const uint32_t stg_base = (uint32_t)(uintptr_t)stg;
   const uint32_t rstg_base = (uint32_t)(uintptr_t)rstg;
 
   // staging of symbol (ff, ss): antenna row g is staged as M + SPC samples from the SPC-aligned
@@ -721,33 +685,6 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
       }
     }
   };
-  // prefetch waves (DS_PF): the first NA waves after the row and reference waves, one row each
-  constexpr int PFW0 = RW0 + (REF == 1 ? NREF / 64 : 0);
-  constexpr bool PF = DS_PF != 0 && !SC16 && DS_ROW_DMA && PFW0 + NA <= T / 64;
-  constexpr int NPFI = (M * SB + 128 + 64 * 128 - 1) / (64 * 128);   // prefetch instructions per row
-  __shared__ uint32_t pf_junk[PF ? 64 : 1];
-  const bool pf_wave = PF && wv >= (uint32_t)PFW0 && wv < (uint32_t)(PFW0 + NA);
-  auto prefetch = [&](const FrameBase &fb, uint32_t ss) {
-    if constexpr (PF) {
-      if (pf_wave) {
-        const int64_t abs0 = fb.body + (int64_t)((uint64_t)ss * a.SL);
-        if (abs0 >= 0 && abs0 + M <= (int64_t)a.frame_len) {
-          const uint32_t g = wv - PFW0;
-          const int64_t byte0 = (fb.row0 + abs0 + (int64_t)g * a.stride) * SB;
-          const int64_t line0 = byte0 & ~(int64_t)127;
-          const uint32_t span = (uint32_t)(byte0 + M * SB - line0);
-          const auto xa = sgpr_ptr(reinterpret_cast<const char *>(a.iq) + line0);
-          const uint32_t lane = (uint32_t)(opq(tid) & 63);
-          const uint32_t dst = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)pf_junk);
-#pragma unroll
-          for (int j = 0; j < NPFI; j++) {
-            const uint32_t o = ((uint32_t)j * 64u + lane) * 128u;
-            if (o < span) pf_line(o, xa, dst);
-          }
-        }
-      }
-    }
-  };
   // ... and the wait (the reference waves' only loads in flight: with RW0 = 0 they also stage
   // samples, whose DMA this waits for as well)
   auto wait_ref = [&]() {
@@ -755,14 +692,7 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
       if (ref_wave) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   };
 
-  // DB: byte offset of row DMA block b (positions 128 b ..) in its row's regions
-  auto db_off = [](int b) -> uint32_t {
-    const int p0 = 128 * b, reg = p0 / 256 < 7 ? p0 / 256 : 7;
-    return (uint32_t)((reg * QS + p0 - 256 * reg) * (int)sizeof(v2f));
-  };
-  auto fetch = [&](const FrameBase &fb, uint32_t ss, v2f *dstp = nullptr, bool with_ref = true) -> uint32_t {
-    if (!DB) dstp = stg;
-    const uint32_t dstb = (uint32_t)(uintptr_t)dstp;
+  auto fetch = [&](const FrameBase &fb, uint32_t ss) -> uint32_t {
     const int64_t abs0 = fb.body + (int64_t)((uint64_t)ss * a.SL);
     const int64_t row0 = fb.row0;
     const int64_t e0 = row0 + abs0;                   // batch sample index of row 0's first
@@ -784,12 +714,12 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
         const int64_t ag = (e0 + (int64_t)g * a.stride) & ~(int64_t)(SPC - 1);
         const auto xa = sgpr_ptr(reinterpret_cast<const char *>(a.iq) + ag * SB);
         const uint32_t lane = (uint32_t)(opq(tid) & 63);
-        const uint32_t dst0 = __builtin_amdgcn_readfirstlane(dstb + g * (uint32_t)(DB ? GS * sizeof(v2f) : RS * SB));
+        const uint32_t dst0 = __builtin_amdgcn_readfirstlane(stg_base + g * RS * (uint32_t)SB);
 #pragma unroll
         for (int j = 0; j < (NBLK + WPR - 1) / WPR; j++) {
           const uint32_t b = sub + (uint32_t)j * WPR;             // uniform
           if (b < (uint32_t)NBLK && (b + 1 < (uint32_t)NBLK || lane < (uint32_t)LASTC))
-            dma16(b * 1024u + lane * 16u, xa, dst0 + (DB ? db_off((int)b) : b * 1024u));
+            dma16(b * 1024u + lane * 16u, xa, dst0 + b * 1024u);
         }
       }
 #else
@@ -823,19 +753,12 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
           stg16[c] = in ? reinterpret_cast<const short2 *>(xf)[(uint64_t)g * a.stride + n]
                         : make_short2(0, 0);
         } else {
-          const v2f val = in ? reinterpret_cast<const v2f *>(xf)[(uint64_t)g * a.stride + n]
-                             : v2f{0.0f, 0.0f};
-          if constexpr (DB) {
-            const int reg = q / 256 < 7 ? q / 256 : 7;
-            dstp[g * GS + reg * QS + q - 256 * reg] = val;
-          } else {
-            stg[c] = val;
-          }
+          stg[c] = in ? reinterpret_cast<const v2f *>(xf)[(uint64_t)g * a.stride + n]
+                      : v2f{0.0f, 0.0f};
         }
       }
     }
-    if constexpr (REF == 1 && !CPE)
-      if (with_ref) fetch_ref(fb, ss);   // the next symbol's, with its samples
+    if constexpr (REF == 1 && !CPE) fetch_ref(fb, ss);   // the next symbol's, with its samples
     return odds;
   };
   // this frame's weights * gain * dn for the thread's subcarriers k = tid + q T
@@ -965,49 +888,9 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
     // this symbol's staging has landed (the previous symbol's stores may still be in flight)
     MARK(";@@A top");
     DSP(const unsigned long long ds_0 = __builtin_amdgcn_s_memtime(); ds_t[4] += ds_0 - ds_c;)
-    if (DS_PF == 2 && pf_wave) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(NSTORE + NPFI) : "memory");
-    else asm volatile("s_waitcnt vmcnt(%0)" :: "n"(NSTORE) : "memory");
+    asm volatile("s_waitcnt vmcnt(%0)" :: "n"(NSTORE) : "memory");
     __syncthreads();
     DSP(const unsigned long long ds_1 = __builtin_amdgcn_s_memtime(); ds_t[1] += ds_1 - ds_0;)
-    // the item after this one (uniform) and its staging, in flight during this symbol
-    uint32_t fn = f, sn = s + 1, n_out_n = n_out_f;
-    uint32_t odd_n = 0;
-    FrameBase fbase_n = fbase;
-    auto next_item = [&]() {
-      if (sn >= n_out_f) {
-        do { fn++; } while (pfx[fn + 1] == pfx[fn]);
-        sn = 0;
-        n_out_n = pfx[fn + 1] - pfx[fn];
-        fn = __builtin_amdgcn_readfirstlane(fn);
-        fbase_n = frame_base(fn);
-      }
-      fn = __builtin_amdgcn_readfirstlane(fn);
-      sn = __builtin_amdgcn_readfirstlane(sn);
-      n_out_n = __builtin_amdgcn_readfirstlane(n_out_n);
-    };
-    if constexpr (DB) {
-      // this symbol's image; the next symbol's rows into the other one, whose readers (the
-      // previous symbol's apply) passed the barrier above. Its reference indices follow
-      // after pass 0's barrier (one reference buffer: this symbol's are read below)
-      const bool odd_i = ((i - i_begin) & 1u) != 0;
-      img = odd_i ? img1 : img0;
-      if (i + 1 < i_end) {
-        next_item();
-        odd_n = fetch(fbase_n, sn, odd_i ? img0 : img1, false);
-      }
-    }
-    if constexpr (PF && DS_PF == 1) {   // the next symbol's rows into L2 now
-      if (i + 1 < i_end) {
-        uint32_t f1 = f, s1 = s + 1;
-        FrameBase fb1 = fbase;
-        if (s1 >= n_out_f) {
-          do { f1++; } while (pfx[f1 + 1] == pfx[f1]);
-          s1 = 0;
-          fb1 = frame_base(__builtin_amdgcn_readfirstlane(f1));
-        }
-        prefetch(fb1, __builtin_amdgcn_readfirstlane(s1));
-      }
-    }
     v2f v[8];
     {
       const int t0 = opq(tid);
@@ -1019,15 +902,6 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
           const float2 w = cv.cvt(x[r * W8]);
           v[r] = v2f{w.x, w.y};
         }
-      } else if constexpr (DB) {
-        // staged position P = n + odd + 256 r: region r (r + 1 where n + odd = 256), slot
-        // (n + odd) mod 256; for r = 7 region 7, slot n + odd (up to 256)
-        const uint32_t g = (uint32_t)t0 / W8, u = (uint32_t)t0 % W8 + ((odd >> (4 * g)) & 15u);
-        const v2f *bg = img + g * GS;
-        const v2f *x = bg + (u >= (uint32_t)W8 ? QS : 0) + (u & (W8 - 1));
-#pragma unroll
-        for (int r = 0; r < 7; r++) v[r] = x[r * QS];
-        v[7] = bg[7 * QS + u];
       } else {
         const v2f *x = stg + (t0 / W8) * RS + ((odd >> (4 * (t0 / W8))) & 15u) + (t0 % W8);
 #pragma unroll
@@ -1079,30 +953,29 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
       twiddle_powers<8>(w, twl[n]);
 #pragma unroll
       for (int q = 1; q < 8; q++) v[q] = cmul_pk(v[q], w[q]);
-      v2f *e = img + g * GS + (WP::X256 ? (int)n : padk<WP::PADK>((int)n)) +
-               (DB ? (int)((odd >> (4 * g)) & 15u) : 0);
+      v2f *e = img + g * GS + (WP::X256 ? (int)n : padk<WP::PADK>((int)n));
 #pragma unroll
       for (int q = 0; q < 8; q++) e[q * QS] = v[q];
     }
     __syncthreads();                                  // staging consumed by every wave
     DSP(const unsigned long long ds_2 = __builtin_amdgcn_s_memtime(); ds_t[5] += ds_2 - ds_1;)
     MARK(";@@C fetch");
-    if (DB && i + 1 < i_end) fetch_ref(fbase_n, sn);   // (every wave read this symbol's)
-    if (!DB && i + 1 < i_end) {
-      next_item();
-      if (DS_DMA_AT == 0 || !WF) odd_n = fetch(fbase_n, sn);
-      if constexpr (PF && DS_PF == 2) {   // the symbol after the next one into L2
-        if (i + 2 < i_end) {
-          uint32_t f2 = fn, s2 = sn + 1;
-          FrameBase fb2 = fbase_n;
-          if (s2 >= n_out_n) {
-            do { f2++; } while (pfx[f2 + 1] == pfx[f2]);
-            s2 = 0;
-            fb2 = frame_base(__builtin_amdgcn_readfirstlane(f2));
-          }
-          prefetch(fb2, __builtin_amdgcn_readfirstlane(s2));
-        }
+    // the item after this one (uniform) and its staging, in flight during this symbol
+    uint32_t fn = f, sn = s + 1, n_out_n = n_out_f;
+    uint32_t odd_n = 0;
+    FrameBase fbase_n = fbase;
+    if (i + 1 < i_end) {
+      if (sn >= n_out_f) {
+        do { fn++; } while (pfx[fn + 1] == pfx[fn]);
+        sn = 0;
+        n_out_n = pfx[fn + 1] - pfx[fn];
+        fn = __builtin_amdgcn_readfirstlane(fn);
+        fbase_n = frame_base(fn);
       }
+      fn = __builtin_amdgcn_readfirstlane(fn);
+      sn = __builtin_amdgcn_readfirstlane(sn);
+      n_out_n = __builtin_amdgcn_readfirstlane(n_out_n);
+      odd_n = fetch(fbase_n, sn);
     }
     // passes 1 .. NP-1 through the LDS images (pass 1 needs no leading barrier: the previous
     // symbol's image readers finished before the barrier at the top), then the exchange that
@@ -1115,7 +988,7 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
       static_assert(!WP::PADK || LG == 32, "pad2(s + 32 r) = pad2(s) + pad2(32 r) for s < 32");
       const uint32_t t0 = (uint32_t)opq(tid);
       const uint32_t s = t0 & (LG - 1), sg = t0 / LG;
-      v2f *rg = img + (sg >> 3) * GS + (sg & 7) * QS + (DB ? (int)((odd >> (4 * (sg >> 3))) & 15u) : 0);
+      v2f *rg = img + (sg >> 3) * GS + (sg & 7) * QS;
       if constexpr (WP::X256) {
         sub256_fwd(rg, v, twl + WP::TW0, s);
       } else {
@@ -1125,10 +998,9 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
         dft_fwd_pk<8>(v);
         wave_passes<LOG2M - 3, 1, WP::PADK>(rg, v, twl + WP::TW0, s);
       }
-      if (DS_DMA_AT == 1 && i + 1 < i_end) odd_n = fetch(fbase_n, sn);
       wait_ref();
       __syncthreads();                                // every spectrum in its region
-      if (DS_DMA_AT == 2 && i + 1 < i_end) odd_n = fetch(fbase_n, sn);
+
     } else {
       st_store<LOG2M, NA, 0, 0, ex_layout<PL::NP>(0)>(img, v, (uint32_t)opq(tid));
 #ifndef DS_ABL_NOFFT   // timing ablation: no passes 1.. and no final exchange
@@ -1249,7 +1121,7 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
         const uint32_t kk = (uint32_t)opq(tid) * S + q;
         const v2f *xp = img + (kk & 7u) * QS + (WP::X256 ? (int)(kk >> 3) : padk<WP::PADK>((int)(kk >> 3)));
 #pragma unroll
-        for (int r = 0; r < NA; r++) X[q][r] = xp[r * GS + (DB ? (int)((odd >> (4 * r)) & 15u) : 0)];
+        for (int r = 0; r < NA; r++) X[q][r] = xp[r * GS];
         if constexpr (CPE) {
           if (q == 0) {
 #pragma unroll
@@ -1271,11 +1143,11 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
         const uint32_t d1 = finish(t, 1, kb + 1, y1);
 #ifndef DS_ABL_NOSTORE   // timing ablation: no symbol / index stores
         // (outputs are written once and not read back here: non-temporal stores)
-        if constexpr (OUTS & 1)
-          out_store<NTST>(v4f{y0.x, y0.y, y1.x, y1.y},
+        if constexpr (OUTX & 1)
+          out_store<NTS>(v4f{y0.x, y0.y, y1.x, y1.y},
                                       (gptr<v4f>)((gptr<char>)osym + kb * (uint32_t)sizeof(v2f)));
-        if constexpr (OUTS & 2)
-          out_store<NTST>((uint16_t)(d0 | (d1 << 8)), (gptr<uint16_t>)((gptr<char>)oidx + kb));
+        if constexpr (OUTX & 2)
+          out_store<NTI>((uint16_t)(d0 | (d1 << 8)), (gptr<uint16_t>)((gptr<char>)oidx + kb));
 #endif
       }
     } else {
@@ -1306,8 +1178,8 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
           const uint32_t d = finish(t, q, k, acc);
 #ifndef DS_ABL_NOSTORE   // timing ablation: no symbol / index stores
           if constexpr (OUTS & 1)
-            out_store<NTST>(acc, (gptr<v2f>)((gptr<char>)osym + k * (uint32_t)sizeof(v2f)));
-          if constexpr (OUTS & 2) out_store<NTST>((uint8_t)d, &oidx[k]);
+            out_store<NTS>(acc, (gptr<v2f>)((gptr<char>)osym + k * (uint32_t)sizeof(v2f)));
+          if constexpr (OUTS & 2) out_store<NTI>((uint8_t)d, &oidx[k]);
 #endif
         }
       }
@@ -2200,9 +2072,7 @@ uint32_t launch_decode_split(const DecodeArgs &a, int log2M, uint32_t n_frames, 
 // returns the EVM partial sets per record (waves per workgroup), 0 when the configuration is
 // not handled here (the caller then uses the per-symbol kernels)
 template <int LOG2M, int NA>
-static size_t stream_lds_bytes(int ref_mode, bool sc16, bool cpe = false) {
-  if (!cpe && (ref_mode == 1 ? stream_db<LOG2M, NA, 1, false, false>() : stream_db<LOG2M, NA, 0, false, false>()) && !sc16)
-    return stream_dyn_lds<LOG2M, NA>(true, ref_mode, false, true);
+static size_t stream_lds_bytes(int ref_mode, bool sc16) {
   const bool wf = ref_mode == 1 ? (sc16 ? stream_wave_fft<LOG2M, NA, 1, true>()
                                         : stream_wave_fft<LOG2M, NA, 1, false>())
                                 : (sc16 ? stream_wave_fft<LOG2M, NA, 0, true>()
@@ -2218,7 +2088,7 @@ bool decode_stream_cpe(const DecodeArgs &a) {
 template <int LOG2M, int NA>
 static uint32_t stream_launch(const DecodeArgs &a, hipStream_t s) {
   using PL = StreamPlan<LOG2M, NA>;
-  const size_t shm = stream_lds_bytes<LOG2M, NA>(a.ref_mode, a.sc16 != 0, decode_stream_cpe(a));
+  const size_t shm = stream_lds_bytes<LOG2M, NA>(a.ref_mode, a.sc16 != 0);
   auto pick_out = [&](auto ref) -> void (*)(DecodeArgs) {
     constexpr int R = decltype(ref)::value;
     const int outs = (a.out_sym ? 1 : 0) | (a.out_idx ? 2 : 0);

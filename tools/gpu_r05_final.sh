@@ -3,7 +3,7 @@
 # CPU baseline, C2/C4/C5), PMC FETCH/WRITE passes over the decode stage and kernel-trace stats.
 set -o pipefail
 R=$(cd "$(dirname "$0")/.." && pwd)
-tag=${1:-r04}
+tag=${1:-r05}
 part=${2:-all}          # all | bench (tests + bench lines) | prof (PMC, stats, CFO)
 O=$R/gpurun_out/$tag
 mkdir -p $O
@@ -15,7 +15,7 @@ timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke(); print('smok
 tail -1 $O/smoke.log
 timeout -k 10 300 python bench.py > $O/bench_c3.json 2> $O/bench_c3.err || { echo "bench c3 failed"; tail -20 $O/bench_c3.err; exit 1; }
 for w in c2 c4 c5; do
-  timeout -k 10 200 python bench.py --workload $w --cpu-baseline 0 > $O/bench_$w.json 2> $O/bench_$w.err || { echo "bench $w failed"; tail -20 $O/bench_$w.err; exit 1; }
+  timeout -k 10 400 python bench.py --workload $w --cpu-baseline 1 > $O/bench_$w.json 2> $O/bench_$w.err || { echo "bench $w failed"; tail -20 $O/bench_$w.err; exit 1; }
 done
 fi
 [ $part = bench ] && exit 0

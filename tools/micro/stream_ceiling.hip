@@ -23,14 +23,26 @@ constexpr int NBLK = 17, LASTC = RS / 2 - 16 * 64;   // 1 KB DMA blocks per row,
 constexpr int NSTORE = 8;
 typedef float v4f __attribute__((ext_vector_type(4)));
 
+template <bool NT = true>
 __device__ inline void dma16(uint32_t voff, const void *sbase, uint32_t lds) {
   uint32_t keep;
-  asm volatile("s_nop 4\n\ts_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t"
-               "global_load_lds_dwordx4 %1, %2 nt\n\ts_mov_b32 m0, %0"
-               : "=&s"(keep) : "v"(voff), "s"(sbase), "s"(lds) : "memory");
+  if constexpr (NT)
+    asm volatile("s_nop 4\n\ts_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t"
+                 "global_load_lds_dwordx4 %1, %2 nt\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(voff), "s"(sbase), "s"(lds) : "memory");
+  else
+    asm volatile("s_nop 4\n\ts_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t"
+                 "global_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(voff), "s"(sbase), "s"(lds) : "memory");
+}
+// OPT bits: 1 plain (not nt) stores, 2 plain DMA loads, 4 no index stores
+template <bool NT, typename V, typename P>
+__device__ inline void st(V v, P p) {
+  if constexpr (NT) __builtin_nontemporal_store(v, p);
+  else *p = v;
 }
 
-template <int MODE, int FILL, int LDSX>
+template <int MODE, int FILL, int LDSX, int OPT = 0>
 __global__ __launch_bounds__(T) void kern(const float2 *iq, uint64_t L, const uint8_t *ref, float2 *osym,
                                           uint8_t *oidx, uint32_t nsym, uint32_t spf, float *sink) {
   extern __shared__ __attribute__((aligned(16))) float2 lds[];
@@ -53,22 +65,23 @@ __global__ __launch_bounds__(T) void kern(const float2 *iq, uint64_t L, const ui
       const char *xa = reinterpret_cast<const char *>(iq + e);
       const uint32_t dst = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(stg + g * RS));
       for (int b = 0; b < NBLK; b++)
-        if (b + 1 < NBLK || lane < LASTC) dma16(b * 1024u + lane * 16u, xa, dst + b * 1024u);
+        if (b + 1 < NBLK || lane < LASTC) dma16<!(OPT & 2)>(b * 1024u + lane * 16u, xa, dst + b * 1024u);
     }
     if (MODE != 3 && MODE != 4 && wv >= 4 && wv < 12) {             // reference indices: 8 x 1 KB
       const uint32_t w = wv - 4, t = w / 2, h = w % 2;
       const uint8_t *rb = ref + ((uint64_t)(f * NA + t) * spf + s) * M + h * 1024;
-      dma16(lane * 16u, rb, __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(rstg + t * M + h * 1024)));
+      dma16<!(OPT & 2)>(lane * 16u, rb, __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(rstg + t * M + h * 1024)));
     }
   };
   fetch(i0, stg0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   float acc = 0.0f;
+  const unsigned long long c0 = __builtin_amdgcn_s_memtime();
   for (uint32_t i = i0; i < i1; i++) {
     float2 *cur = (DB && (i - i0) % 2) ? stg1 : stg0;
     float2 *nxt = (DB && (i - i0) % 2) ? stg0 : stg1;
-    asm volatile("s_waitcnt vmcnt(%0)" :: "n"(MODE == 2 || MODE == 4 ? 0 : NSTORE) : "memory");
+    asm volatile("s_waitcnt vmcnt(%0)" :: "n"(MODE == 2 || MODE == 4 ? 0 : ((OPT & 4) ? NSTORE / 2 : NSTORE)) : "memory");
     __syncthreads();
     if (DB && i + 1 < i1) fetch(i + 1, nxt);
     const uint32_t f = i / spf, s = i % spf;
@@ -93,24 +106,30 @@ __global__ __launch_bounds__(T) void kern(const float2 *iq, uint64_t L, const ui
       const uint32_t kb = 2 * (uint32_t)tid;
       for (int t = 0; t < NA; t++) {
         const uint64_t ob = ((uint64_t)(f * NA + t) * spf + s) * M;
-        __builtin_nontemporal_store(v4f{v[2 * t].x, v[2 * t].y, v[2 * t + 1].x, v[2 * t + 1].y},
-                                    reinterpret_cast<v4f *>(osym + ob + kb));
-        __builtin_nontemporal_store((uint16_t)(refw + t), reinterpret_cast<uint16_t *>(oidx + ob + kb));
+        st<!(OPT & 1)>(v4f{v[2 * t].x, v[2 * t].y, v[2 * t + 1].x, v[2 * t + 1].y},
+                       reinterpret_cast<v4f *>(osym + ob + kb));
+        if constexpr (!(OPT & 4))
+          st<!(OPT & 1)>((uint16_t)(refw + t), reinterpret_cast<uint16_t *>(oidx + ob + kb));
       }
     }
   }
   if (acc == 12345.0f) sink[0] = acc;
+  if (tid == 0) {   // shader cycles per symbol of this workgroup, summed over the grid
+    const unsigned long long c1 = __builtin_amdgcn_s_memtime();
+    atomicAdd(reinterpret_cast<unsigned long long *>(sink) + 1, (c1 - c0) / (i1 - i0));
+  }
 }
 
-template <int MODE, int FILL, int LDSX>
+template <int MODE, int FILL, int LDSX, int OPT = 0>
 float run(const float2 *iq, uint64_t L, const uint8_t *ref, float2 *osym, uint8_t *oidx, uint32_t nsym,
           uint32_t spf, float *sink, int ncu) {
   const size_t lds = sizeof(float2) * NA * RS * (MODE == 1 ? 2 : 1) + NA * M + sizeof(float2) * 64 * 9;
-  auto k = kern<MODE, FILL, LDSX>;
+  auto k = kern<MODE, FILL, LDSX, OPT>;
   CHK(hipFuncSetAttribute((const void *)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   hipEvent_t a, b;
   CHK(hipEventCreate(&a)); CHK(hipEventCreate(&b));
   for (int w = 0; w < 3; w++) k<<<ncu, T, lds>>>(iq, L, ref, osym, oidx, nsym, spf, sink);
+  CHK(hipMemset(sink, 0, 64));
   CHK(hipEventRecord(a));
   const int reps = 10;
   for (int w = 0; w < reps; w++) k<<<ncu, T, lds>>>(iq, L, ref, osym, oidx, nsym, spf, sink);
@@ -118,6 +137,10 @@ float run(const float2 *iq, uint64_t L, const uint8_t *ref, float2 *osym, uint8_
   CHK(hipEventSynchronize(b));
   float ms;
   CHK(hipEventElapsedTime(&ms, a, b));
+  unsigned long long cyc[2];
+  CHK(hipMemcpy(cyc, sink, 16, hipMemcpyDeviceToHost));
+  printf("  [%llu cycles/symbol, %.2f GHz]", cyc[1] / (reps * (unsigned long long)ncu),
+         (double)(cyc[1] / (reps * (unsigned long long)ncu)) * (nsym / (double)ncu) / (ms / reps * 1e6));
   return ms / reps;
 }
 
@@ -138,17 +161,17 @@ int main() {
   auto rep = [&](const char *name, float ms, double b) {
     printf("%-34s %.4f ms  %.2f TB/s\n", name, ms, b / ms * 1e-9);
   };
-  rep("mode0 (kernel schedule, no filler)", run<0, 0, 0>(iq, L, ref, osym, oidx, nsym, spf, sink, ncu), bytes);
-  rep("mode1 (double-buffered staging)", run<1, 0, 0>(iq, L, ref, osym, oidx, nsym, spf, sink, ncu), bytes);
-#define GRID(F, X) \
-  rep("mode4 fill " #F " ldsx " #X " (filler alone)", run<4, F, X>(iq, L, ref, osym, oidx, nsym, spf, sink, ncu), bytes); \
-  rep("mode0 fill " #F " ldsx " #X, run<0, F, X>(iq, L, ref, osym, oidx, nsym, spf, sink, ncu), bytes); \
-  rep("mode1 fill " #F " ldsx " #X, run<1, F, X>(iq, L, ref, osym, oidx, nsym, spf, sink, ncu), bytes);
-  GRID(8, 0)
-  GRID(16, 0)
-  GRID(0, 2)
-  GRID(0, 4)
-  GRID(8, 2)
-  GRID(12, 3)
+  const double bytes_ld = (double)nsym * NA * M * 9, bytes_noidx = (double)nsym * NA * M * 17;
+  rep("mode0 (kernel schedule)", run<0, 0, 0>(iq, L, ref, osym, oidx, nsym, spf, sink, ncu), bytes);
+  rep("mode0 plain stores", run<0, 0, 0, 1>(iq, L, ref, osym, oidx, nsym, spf, sink, ncu), bytes);
+  rep("mode0 plain DMA", run<0, 0, 0, 2>(iq, L, ref, osym, oidx, nsym, spf, sink, ncu), bytes);
+  rep("mode0 plain stores + DMA", run<0, 0, 0, 3>(iq, L, ref, osym, oidx, nsym, spf, sink, ncu), bytes);
+  rep("mode0 no index stores", run<0, 0, 0, 4>(iq, L, ref, osym, oidx, nsym, spf, sink, ncu), bytes_noidx);
+  rep("mode1 (double-buffered)", run<1, 0, 0>(iq, L, ref, osym, oidx, nsym, spf, sink, ncu), bytes);
+  rep("mode2 (loads only)", run<2, 0, 0>(iq, L, ref, osym, oidx, nsym, spf, sink, ncu), bytes_ld);
+  rep("mode2 (loads only, plain)", run<2, 0, 0, 2>(iq, L, ref, osym, oidx, nsym, spf, sink, ncu), bytes_ld);
+  rep("mode3 (stores only)", run<3, 0, 0>(iq, L, ref, osym, oidx, nsym, spf, sink, ncu), bytes_ld);
+  rep("mode3 (stores only, plain)", run<3, 0, 0, 1>(iq, L, ref, osym, oidx, nsym, spf, sink, ncu), bytes_ld);
+  rep("mode0 fill 12 ldsx 3", run<0, 12, 3>(iq, L, ref, osym, oidx, nsym, spf, sink, ncu), bytes);
   return 0;
 }
