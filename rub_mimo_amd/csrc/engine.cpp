@@ -232,6 +232,8 @@ struct mimo_rx {
   DevBuf<float> gain;
   DevBuf<double> nvp, evm_part, evm_out, lspart, evm_chunk;
   DevBuf<float2> lsq;                   // fused search + LS: X/S1 per access code
+  DevBuf<uint32_t> ls_arrive;           // fused LS combine: [F][N][N] counters (self-resetting)
+  size_t cap_ls_arrive = 0;
   DevBuf<uint32_t> evm_cnt;             // per-frame chunk counters of evm_kernel (self-resetting)
   DevBuf<uint32_t> nrec;                // per-frame EVM records of the streaming decode
   size_t cap_lspart = 0;
@@ -577,9 +579,28 @@ int run_estimate(mimo_rx *h, const float2 *iq, uint64_t stride, uint32_t F, uint
     HIPCHK(h->lsq.ensure((size_t)F * h->N * h->N * h->nac * h->M));
     sa.s1sign = h->s1sign.p; sa.lsq = h->lsq.p; sa.nac = h->nac;
     sa.cfo_part = (cfo && cfo->fold) ? cfo->part : nullptr;   // folded CFO: derotating loads
-    static const bool xcd = [] { const char *e = getenv("RMIMO_SEARCH_XCD"); return !(e && e[0] == '0'); }();
-    sa.xcd_order = xcd ? 1u : 0u;
+    static const int xcd = [] { const char *e = getenv("RMIMO_SEARCH_XCD"); return e ? atoi(e) : 1; }();
+    sa.xcd_order = (uint32_t)xcd;
+    static const int fr_chunk = [] { const char *e = getenv("RMIMO_LS_CHUNK"); return e ? atoi(e) : 32; }();
+    sa.fr_chunk = (uint32_t)std::max(fr_chunk, 1);
     la.lsq = h->lsq.p;
+    // opt-in (RMIMO_LS_FUSE=1, not with CFO, whose stage 2 rotates the terms in between): the
+    // LS combine fused into the search's last workgroup per (frame, rx, tx). Measured slower
+    // than the separate ls_combine_q_kernel (C3 search + LS 0.555 vs 0.521 ms, C4 0.673 vs
+    // 0.586; DESIGN "LS combine fused into the search")
+    static const bool ls_fuse = [] { const char *e = getenv("RMIMO_LS_FUSE"); return e && e[0] == '1'; }();
+    const bool fuse = ls_fuse && !cfo && search_ls_wave_enabled() && h->codes.codespec_w.p;
+    if (fuse) {
+      const size_t need = (size_t)F * h->N * h->N;
+      if (need > h->cap_ls_arrive) {
+        HIPCHK(h->ls_arrive.ensure(need));
+        HIPCHK(hipMemsetAsync(h->ls_arrive.p, 0, sizeof(uint32_t) * need, s));
+        h->cap_ls_arrive = need;
+      }
+      sa.ls_arrive = h->ls_arrive.p;
+      sa.G = h->G.p; sa.nv_part = h->nvp.p; sa.n_nvp = la.n_nvp;
+      sa.occ_index = h->occ.p; sa.keep_bias = h->keep_bias; sa.ls_scale = h->ls_scale;
+    }
     hipEvent_t e = h->timer.begin(s);
     launch_search_ls(sa, h->log2F, h->log2M, F, s);
     h->timer.end(2, e, s);
@@ -588,8 +609,8 @@ int run_estimate(mimo_rx *h, const float2 *iq, uint64_t stride, uint32_t F, uint
       launch_cfo_batch(*cfo, F, 2, s);
       la.cfo_part = cfo->part;
     }
-    e = h->timer.begin(s);
-    launch_ls_combine_q(la, F, s);
+    e = h->timer.begin(s);   // (fused: the LS stage's clock stays, empty)
+    if (!fuse) launch_ls_combine_q(la, F, s);
     h->timer.end(3, e, s);
   } else {
     hipEvent_t e = h->timer.begin(s);

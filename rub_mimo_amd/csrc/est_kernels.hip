@@ -463,6 +463,122 @@ void search_ls_kernel(SearchArgs a) {
   }
 }
 
+// LS term stores and the fused combine's loads. Fused, they are agent-coherent (relaxed
+// agent-scope atomics: sc1, written through / read past the XCD's L2), so the arrival needs no
+// L2 write-back or invalidate (an agent-scope fence per workgroup costs ~6x the search); else
+// non-temporal, read once by ls_combine_q_kernel.
+template <typename PT>   // v2f * or gptr<v2f>
+__device__ __forceinline__ void ls_term_store(PT p, v2f t, bool coherent) {
+  if (coherent) {
+    unsigned long long b;
+    __builtin_memcpy(&b, &t, sizeof(b));
+    __hip_atomic_store((gptr<unsigned long long>)p, b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  } else {
+    __builtin_nontemporal_store(t, p);
+  }
+}
+__device__ __forceinline__ v2f ls_term_load(const v2f *p) {
+  const unsigned long long b = __hip_atomic_load(reinterpret_cast<const unsigned long long *>(p),
+                                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  v2f t;
+  __builtin_memcpy(&t, &b, sizeof(t));
+  return t;
+}
+
+// The LS combine of one (frame, rx, tx), run by the search workgroup that stored its last
+// access code's terms (framing.cc:801-824): ls_combine_q_kernel's arithmetic and order -- per
+// subcarrier the codes' X/S1 summed in code order in fp64, G = (bias + sum) * scale, and the
+// training residual's variance -- with its reduction tree: a 64-lane xor butterfly per 64
+// subcarriers, then the four of each 256 summed left to right into the same nv_part entry.
+// G and nv_part are therefore bitwise those of the separate kernel.
+template <int T>
+__device__ __forceinline__ void ls_combine_fused(const SearchArgs &a, uint32_t f, uint32_t r,
+                                                 uint32_t t, double *red) {
+  const uint32_t M = a.M, N = a.N, nac = a.nac;
+  const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
+  const uint32_t rt = r * N + t, nitems = (M + 63) / 64;
+  const v2f *q0 = reinterpret_cast<const v2f *>(a.lsq) + (((uint64_t)f * N + r) * N + t) * nac * M;
+  const double bias = (a.keep_bias && r == t) ? 1.0 : 0.0;
+  // (every code's term of the lane's subcarrier loaded before any is summed: one memory
+  // latency per subcarrier instead of one per batch; codes beyond CMAX in further rounds)
+  constexpr uint32_t CMAX = 24;
+  for (uint32_t it = wv; it < nitems; it += T / 64) {   // uniform per wave
+    const uint32_t k = it * 64 + lane;
+    double nv = 0.0;
+    if (k < M) {
+      const bool occ = a.occ_index[k] >= 0;
+      const v2f *q = q0 + k;
+      double sr = 0.0, si = 0.0, s2 = 0.0;
+      for (uint32_t c0 = 0; c0 < nac; c0 += CMAX) {
+        v2f vb[CMAX];
+#pragma unroll
+        for (uint32_t j = 0; j < CMAX; j++)
+          if (c0 + j < nac) vb[j] = ls_term_load(q + (uint64_t)(c0 + j) * M);
+#pragma unroll
+        for (uint32_t j = 0; j < CMAX; j++) {
+          if (c0 + j < nac) {
+            sr += (double)vb[j].x;
+            si += (double)vb[j].y;
+            s2 += (double)vb[j].x * vb[j].x + (double)vb[j].y * vb[j].y;
+          }
+        }
+      }
+      a.G[(((uint64_t)f * M + k) * N + r) * N + t] =
+          occ ? make_float2((float)((bias + sr) * a.ls_scale), (float)(si * a.ls_scale))
+              : make_float2(0.0f, 0.0f);
+      if (occ) nv = s2 - (sr * sr + si * si) / (double)nac;
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) nv += __shfl_xor(nv, off);
+    if (lane == 0) red[it] = nv;
+  }
+  __syncthreads();
+  const uint32_t nb = (M + 255) / 256;
+  for (uint32_t b = tid; b < nb; b += T) {
+    double v = red[4 * b];
+#pragma unroll
+    for (uint32_t j = 1; j < 4; j++) v += 4 * b + j < nitems ? red[4 * b + j] : 0.0;
+    a.nv_part[(uint64_t)f * a.n_nvp + (uint64_t)rt * nb + b] = v;
+  }
+  __syncthreads();                                     // red free for the next combine
+}
+
+// Arrival of a slot-pair workgroup whose LS terms are stored: one count per valid slot on its
+// (frame, rx, tx) counter, issued after every wave's coherent term stores have completed (the
+// release without an L2 write-back); the workgroup that brings a counter to nac runs that
+// (frame, rx, tx)'s combine, its coherent loads issued after the count returned, and re-arms the
+// counter for the next launch.
+template <int T>
+__device__ __forceinline__ void ls_arrive(const SearchArgs &a, uint32_t f, uint32_t r,
+                                          uint32_t s0, bool valid0, bool valid1, double *red,
+                                          uint32_t *s_last) {
+  const uint32_t N = a.N;
+  const uint32_t tx0 = valid0 ? (s0 - 1) % N : 0u, tx1 = s0 % N;   // slots s0, s0 + 1
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's coherent term stores done
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t *ctr = a.ls_arrive + ((uint64_t)f * N + r) * N;
+    s_last[0] = s_last[1] = 0u;
+    if (valid0 && valid1 && tx0 == tx1) {              // (N = 1: both slots one tx)
+      const uint32_t old = __hip_atomic_fetch_add(&ctr[tx0], 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      s_last[0] = old + 2u == a.nac;
+    } else {
+      if (valid0)
+        s_last[0] = __hip_atomic_fetch_add(&ctr[tx0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u == a.nac;
+      if (valid1)
+        s_last[1] = __hip_atomic_fetch_add(&ctr[tx1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u == a.nac;
+    }
+    if (s_last[0]) __hip_atomic_store(&ctr[tx0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (s_last[1]) __hip_atomic_store(&ctr[tx1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  const uint32_t l0 = s_last[0], l1 = s_last[1];
+  if (l0 | l1) {   // (the terms are read with coherent loads issued after the counts)
+    if (l0) ls_combine_fused<T>(a, f, r, tx0, red);
+    if (l1) ls_combine_fused<T>(a, f, r, tx1, red);
+  }
+}
+
 // The same search + LS with the FFT_F split into one workgroup-wide radix-B pass and B
 // wave-local 1024-point transforms (F = 1024 B, one wave per sub-transform, T = 64 B):
 //   forward  X[B k + q] = DFT_1024( c_q )[k],   c_q[n] = W_F^{nq} sum_r x[n + 1024 r] W_B^{rq}
@@ -496,8 +612,26 @@ void search_ls_wave_kernel(SearchArgs a) {
     const uint32_t x = b % 8, q = G / 8, rem = G % 8;
     const uint32_t lid = x * q + min(x, rem) + b / 8;
     const uint32_t nf = gridDim.y, nrx = a.N;
-    bx = (lid / (nrx * nf)) * nrx + lid % nrx;
-    f = (lid / nrx) % nf;
+    if (a.xcd_order == 2) {   // slot pair fastest: a (frame, rx)'s pairs together on one XCD
+      const uint32_t np = gridDim.x / nrx, fr = lid / np;
+      bx = (lid % np) * nrx + fr % nrx;
+      f = fr / nrx;
+    } else if (a.xcd_order == 3) {
+      // chunks of fr_chunk (frame, rx)s in dispatch order, each walked as order 1 (every XCD a
+      // contiguous range of slot pairs): a chunk's (frame, rx)s complete while the next chunk
+      // searches, so the fused LS combines of all but the last chunk overlap the search
+      const uint32_t np = gridDim.x / nrx, nfr = nf * nrx, K = a.fr_chunk;
+      const uint32_t c = b / (np * K), fr0 = c * K, Kc = min(K, nfr - fr0);
+      const uint32_t bl = b - c * np * K, Gc = np * Kc;
+      const uint32_t xl = bl % 8, ql = Gc / 8, rl = Gc % 8;
+      const uint32_t l = xl * ql + min(xl, rl) + bl / 8;
+      const uint32_t fr = fr0 + l % Kc;
+      bx = (l / Kc) * nrx + fr % nrx;
+      f = fr / nrx;
+    } else {
+      bx = (lid / (nrx * nf)) * nrx + lid % nrx;
+      f = (lid / nrx) % nf;
+    }
   }
   const FrameInfo &I = a.info[f];
   if (I.status != 0) return;
@@ -699,23 +833,23 @@ void search_ls_wave_kernel(SearchArgs a) {
     reg_twiddles<LOG2M, 8>(wm, a.tw, (int)lt);
     reg_compute<LOG2M, 8, 0, false>(xw, wm);
     reg_rest_lay<LOG2M, 8, 1, false>(buf + u * PBX, xw, wm, (int)lt);
-    if (!valid) return;                               // uniform per wave
-    const uint32_t ac = s0 + u - 1, code = ac / a.N, tx = ac % a.N;
-    // (code row bases uniform per wave: SGPR pointers, 32-bit lane offsets; X S1 as a product
-    // with the sign, exact for +-1; a null subcarrier's term is an exact +0, as the unfused
-    // ls_kernel writes it, whatever X holds)
-    const auto sg = sgpr_ptr(a.s1sign + ((size_t)tx * a.nac + code) * M);
-    const auto q = sgpr_ptr(reinterpret_cast<v2f *>(a.lsq) +
-                            ((((uint64_t)f * a.N + r) * a.N + tx) * a.nac + code) * M);
+    if (valid) {                                      // uniform per wave
+      const uint32_t ac = s0 + u - 1, code = ac / a.N, tx = ac % a.N;
+      // (code row bases uniform per wave: SGPR pointers, 32-bit lane offsets; X S1 as a product
+      // with the sign, exact for +-1; a null subcarrier's term is an exact +0, as the unfused
+      // ls_kernel writes it, whatever X holds)
+      const auto sg = sgpr_ptr(a.s1sign + ((size_t)tx * a.nac + code) * M);
+      const auto q = sgpr_ptr(reinterpret_cast<v2f *>(a.lsq) +
+                              ((((uint64_t)f * a.N + r) * a.N + tx) * a.nac + code) * M);
 #pragma unroll
-    for (int e = 0; e < 8; e++) {
-      const uint32_t k = (uint32_t)reg_index<LOG2M, 8>((int)lt, e);
-      const int8_t sv = sg[k];
-      const float sgn = (float)sv;
-      const v2f term = sv ? xw[e] * v2f{sgn, sgn} : v2f{0.0f, 0.0f};
-      __builtin_nontemporal_store(term, &q[k]);   // read once, by the combine
+      for (int e = 0; e < 8; e++) {
+        const uint32_t k = (uint32_t)reg_index<LOG2M, 8>((int)lt, e);
+        const int8_t sv = sg[k];
+        const float sgn = (float)sv;
+        const v2f term = sv ? xw[e] * v2f{sgn, sgn} : v2f{0.0f, 0.0f};
+        ls_term_store(&q[k], term, a.ls_arrive != nullptr);   // read once, by the combine
+      }
     }
-    return;
   } else {
     float2 *twm = reinterpret_cast<float2 *>(lds_raw) + lds_padded_len(F);
     fill_twiddles_lds<LOG2M, T>(twm, a.tw);
@@ -749,7 +883,15 @@ void search_ls_wave_kernel(SearchArgs a) {
       float2 *q = a.lsq + ((((uint64_t)f * a.N + r) * a.N + tx) * a.nac + code) * M;
       const float2 Xk = lb[uu * PBM + lds_pad(k)];
       const int sgn = sg[k];
-      q[k] = sgn > 0 ? Xk : (sgn < 0 ? cneg(Xk) : make_float2(0.0f, 0.0f));
+      const float2 t = sgn > 0 ? Xk : (sgn < 0 ? cneg(Xk) : make_float2(0.0f, 0.0f));
+      if (a.ls_arrive) ls_term_store(reinterpret_cast<v2f *>(q) + k, v2f{t.x, t.y}, true);
+      else q[k] = t;
+    }
+  }
+  if constexpr (!CFO) {   // fused LS combine (the CFO path rotates the terms first: separate)
+    if (a.ls_arrive) {    // uniform
+      __shared__ uint32_t s_last[2];
+      ls_arrive<T>(a, f, r, s0, valid0, valid1, reinterpret_cast<double *>(lds_raw), s_last);
     }
   }
 }

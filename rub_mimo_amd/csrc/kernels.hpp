@@ -168,8 +168,18 @@ struct SearchArgs {
   float2 *lsq;                     // [F][N][N][nac][M] X/S1 per access code
   uint32_t nac;
   uint32_t xcd_order;              // search_ls_kernel: slot pair slowest within each XCD
+  uint32_t fr_chunk;               // xcd_order 3: (frame, rx)s per chunk
   const double *cfo_part;          // opt-in CFO, folded: derotate the loads by stage 1 (or null)
   float *corr_trace;               // DEBUG_LOG: [F][N][n_slots][SL] every lag's metric (or null)
+  // LS combine fused into the search (search_ls_wave_kernel, no CFO): the last workgroup to
+  // store a (frame, rx, tx)'s terms sums them as ls_combine_q_kernel does (or null: off)
+  uint32_t *ls_arrive;             // [F][N][N] arrival counters, zero between launches
+  float2 *G;                       // [F][M][N][N]
+  double *nv_part;                 // [F][n_nvp] residual-variance partials, ls_combine_q's layout
+  uint32_t n_nvp;
+  const int32_t *occ_index;        // [M] -> j or -1
+  int keep_bias;
+  float ls_scale;                  // dft_normalizer / float(nac)
 };
 void launch_search(const SearchArgs &a, int log2F, uint32_t n_frames, hipStream_t s);
 // true when (log2F, log2M) has a search_ls_kernel instance (it then ran)

@@ -579,6 +579,60 @@ def test_block_search_form_matches_oracle():
     assert "block-search parity ok" in out.stdout
 
 
+def _ls_batch_outputs(M, cp, N, nac, pid, qam, det, seed, n_frames):
+    """One batch of n_frames synthetic frames through the default receive path: G, W, the
+    frames' result records and the decoded symbols (raw bytes for bitwise comparisons)."""
+    S = Synthesizer(SynthParams(M=M, cp_len=cp, num_streams=N, num_access_codes=nac, pid=pid,
+                                qam_order=qam, seed=seed, snr_db=30.0))
+    L = max(S.frame_len(i) for i in range(n_frames))
+    out = _lib.DeviceBuffer(n_frames * N * L * 8)
+    S.generate(out, L, L, n_frames)
+    P = RxParams(M=M, cp_len=cp, num_streams=N, num_access_codes=nac, pid_max=pid,
+                 detector=det, keep_identity_bias=True, qam_order=qam)
+    rxo = Receiver(P)
+    osym = _lib.DeviceBuffer(n_frames * N * pid * M * 8)
+    rxo.process(out, L, L, n_frames, max_out=pid, out_sym=osym, ref_mode=2, ref_seed=seed)
+    res = rxo.results()
+    nv = np.array([r["noise_var"] for r in res], np.float64)
+    ev = np.array([[r["evm_num"], r["evm_den"]] for r in res], np.float64)
+    return (rxo.G(), rxo.W(), nv, ev,
+            osym.download(np.complex64, n_frames * N * pid * M))
+
+
+def test_ls_combine_fused_equals_separate_kernel():
+    """The LS combine fused into the search (opt-in RMIMO_LS_FUSE=1, read once per process: a
+    child interpreter; the last slot-pair workgroup of each (frame, rx, tx) sums its codes'
+    terms in ls_combine_q_kernel's order and reduction tree) against the default separate
+    kernel: G, W, the noise variances, EVM sums and symbols of C2- and C3-geometry batches are
+    bitwise equal."""
+    import subprocess
+    import sys
+    import tempfile
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cases = [(1024, 76, 2, 20, 24, 16, _lib.DET_ZF2, 51, 5),
+             (2048, 152, 4, 20, 12, 64, _lib.DET_MMSE, 52, 6)]
+    with tempfile.TemporaryDirectory() as td:
+        code = ("import sys; sys.path.insert(0, %r); sys.path.insert(0, %r)\n"
+                "import numpy as np, test_gpu as t\n"
+                "for i, c in enumerate(%r):\n"
+                "    G, W, nv, ev, y = t._ls_batch_outputs(*c)\n"
+                "    np.savez(%r + '/c%%d.npz' %% i, G=G, W=W, nv=nv, ev=ev, y=y)\n"
+                "print('fused ok')\n" % (root, os.path.join(root, "tests"), cases, td))
+        env = dict(os.environ, RMIMO_LS_FUSE="1")
+        out = subprocess.run([sys.executable, "-c", code], env=env, cwd=root, timeout=150,
+                             capture_output=True, text=True)
+        assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-4000:]
+        for i, c in enumerate(cases):
+            G, W, nv, ev, y = _ls_batch_outputs(*c)
+            o = np.load(os.path.join(td, "c%d.npz" % i))
+            assert np.abs(G).max() > 0
+            assert G.tobytes() == o["G"].tobytes(), c
+            assert W.tobytes() == o["W"].tobytes(), c
+            assert nv.tobytes() == o["nv"].tobytes(), c
+            assert ev.tobytes() == o["ev"].tobytes(), c
+            assert y.tobytes() == o["y"].tobytes(), c
+
+
 def test_c3_4x4_mmse_2048_64qam_full_frame():
     """BASELINE config C3 at full size (PID 1000): the oracle needs ~20 s of CPU."""
     d, e = _c_frame_parity(2048, 152, 4, 20, 1000, 64, _lib.DET_MMSE, 30.0, seed=31,
