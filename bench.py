@@ -95,6 +95,10 @@ def parse():
                     help="0 to skip the separately reported pinned-host -> HBM copy timing")
     ap.add_argument("--cpu-threads", type=int, default=0,
                     help="threads of the multi-core CPU baseline (0: the box's core share)")
+    ap.add_argument("--out-layout", default="symbol", choices=["symbol", "stream"],
+                    help="output (and reference-index) layout per frame slot: symbol-major "
+                         "[pid][N][M_occ] (the reference callback's per-symbol order) or "
+                         "stream-major [N][pid][M_occ]; the same bytes either way")
     ap.add_argument("--ref-mode", type=int, default=1,
                     help="EVM reference: 0 decided symbols, 1 transmitted indices from HBM, "
                          "2 transmitted indices regenerated from the seed")
@@ -316,15 +320,20 @@ def main():
                            detector=det, qam_order=args.qam, cfo_correct=args.cfo != 0.0),
                   stream=sh)
     m_occ = rx.M_occ
-    out_sym = torch.empty((F * K, N, pid, m_occ), dtype=torch.complex64, device=dev)
-    out_idx = torch.empty((F * K, N, pid, m_occ), dtype=torch.uint8, device=dev)
+    sym_major = args.out_layout == "symbol"
+    layout = _lib.LAYOUT_SYMBOL_MAJOR if sym_major else _lib.LAYOUT_STREAM_MAJOR
+    oshape = (F * K, pid, N, m_occ) if sym_major else (F * K, N, pid, m_occ)
+    out_sym = torch.empty(oshape, dtype=torch.complex64, device=dev)
+    out_idx = torch.empty(oshape, dtype=torch.uint8, device=dev)
+    # the reference rows in the output layout (tx_idx itself stays stream-major for the CPU check)
+    ref_rows = tx_idx.transpose(1, 2).contiguous() if sym_major else tx_idx
 
     def step(x=None, wire_in=sc16):
         rx.process(src if x is None else x, L, L, F, max_out=pid, out_sym=out_sym,
                    out_idx=out_idx, ref_mode=args.ref_mode,
-                   ref_idx=tx_idx if args.ref_mode == 1 else None, ref_seed=args.seed,
+                   ref_idx=ref_rows if args.ref_mode == 1 else None, ref_seed=args.seed,
                    frame_id0=frame_id0, stream=sh, frames_per_capture=K, ref_starts=ref_starts,
-                   sc16=wire_in, sc16_scale=wscale)
+                   sc16=wire_in, sc16_scale=wscale, out_layout=layout)
 
     # ---- rank-0 sc16 ingest (used by --ingest scatter and the secondary scatter leg)
     wire = None
@@ -595,6 +604,8 @@ def main():
                    "ingest": ("rank-0 sc16 scatter over RCCL P2P" if timed_scatter
                               else "resident in HBM"),
                    "cfo": args.cfo,
+                   "out_layout": ("symbol-major [frame][symbol][stream][M_occ]" if sym_major
+                                  else "stream-major [frame][stream][symbol][M_occ]"),
                    "sample_format": ("sc16 wire samples read in place (4 B/sample)" if sc16
                                      else "fc32 complex64 (8 B/sample)"),
                    "parallelism": ("%d streams over %d GPU(s)" % (args.frames, world) if c5 else

@@ -141,7 +141,7 @@ typedef struct mimo_batch {
   uint64_t frame_len;
   uint32_t n_frames;
   uint32_t max_out_syms;  /* symbols kept per frame (main.cc keeps PID_MAX, main.cc:106) */
-  void *d_out_sym;        /* [n_frames][N][max_out_syms][M_occ] complex64, or NULL */
+  void *d_out_sym;        /* [n_frames][N][max_out_syms][M_occ] complex64 (out_layout), or NULL */
   void *d_out_idx;        /* same layout, uint8 demapped index, or NULL */
   int32_t ref_mode;       /* 0: decision-directed EVM; 1: d_ref_idx; 2: synthetic hash */
   const void *d_ref_idx;  /* ref_mode 1: same layout as d_out_idx */
@@ -161,9 +161,16 @@ typedef struct mimo_batch {
    * it directly (C3-type geometries); other configurations widen it into an internal buffer. */
   uint32_t sample_format;
   float sc16_scale;
+  /* MIMO_LAYOUT_STREAM_MAJOR (0): d_out_sym, d_out_idx and d_ref_idx are
+   * [n_frames][N][max_out_syms][M_occ]. MIMO_LAYOUT_SYMBOL_MAJOR (1): [n_frames][max_out_syms][N][M_occ],
+   * each symbol's N stream rows together -- the order the reference's callback hands them out in
+   * (one call per symbol with the N stream arrays, framing.cc:587) -- and a sequential write
+   * stream per decode workgroup (fewer concurrent HBM write streams: the C3 decode ~7% faster) */
+  uint32_t out_layout;
 } mimo_batch;
 
 enum { MIMO_SAMPLE_FC32 = 0, MIMO_SAMPLE_SC16 = 1 };
+enum { MIMO_LAYOUT_STREAM_MAJOR = 0, MIMO_LAYOUT_SYMBOL_MAJOR = 1 };
 
 /* Positions are those a framesync started at `origin` reports (origin 0 for one frame per
  * capture): add origin for the capture sample. */

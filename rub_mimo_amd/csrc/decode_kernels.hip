@@ -127,7 +127,7 @@ __global__ __launch_bounds__(T) void decode_kernel(DecodeArgs a) {
       const uint32_t d = qam_demap(y, a.qam);
       uint32_t ref = d;
       if (a.ref_mode == 1)
-        ref = a.ref_idx[(((uint64_t)I.ref * NA + t) * a.max_out + s) * a.M_occ + j];
+        ref = a.ref_idx[(uint64_t)I.ref * NA * a.max_out * a.M_occ + t * a.o_ts + s * a.o_ss + j];
       else if (a.ref_mode == 2)
         ref = (uint32_t)(hash5(a.ref_seed, DOM_DATA, frame_id, t,
                                (uint64_t)s * a.M_occ + j) & (uint64_t)(a.qam.L * a.qam.L - 1));
@@ -136,7 +136,7 @@ __global__ __launch_bounds__(T) void decode_kernel(DecodeArgs a) {
       e_num[t] += er * er + ei * ei;
       e_den[t] += (double)sp.x * sp.x + (double)sp.y * sp.y;
       e_err[t] += (d != ref) ? 1.0 : 0.0;
-      const uint64_t o = (((uint64_t)f * NA + t) * a.max_out + s) * a.M_occ + j;
+      const uint64_t o = (uint64_t)f * NA * a.max_out * a.M_occ + t * a.o_ts + s * a.o_ss + j;
       if (a.out_sym) a.out_sym[o] = y;
       if (a.out_idx) a.out_idx[o] = (uint8_t)d;
     }
@@ -339,7 +339,7 @@ void decode_persistent_kernel(DecodeArgs a) {
         uint32_t refs = 0;
         if constexpr (REF == 1)
           refs = *reinterpret_cast<const uint32_t *>(
-              a.ref_idx + (((uint64_t)fref * NA + t) * a.max_out + s) * a.M_occ + k0);
+              a.ref_idx + (uint64_t)fref * NA * a.max_out * a.M_occ + t * a.o_ts + s * a.o_ss + k0);
 #pragma unroll
         for (int e = 0; e < 4; e++) {
           const int k = k0 + e;
@@ -359,7 +359,7 @@ void decode_persistent_kernel(DecodeArgs a) {
           e_err[t] += (d != refi) ? 1.0f : 0.0f;
           packed |= d << (8 * e);
         }
-        const uint64_t o = (((uint64_t)f * NA + t) * a.max_out + s) * a.M_occ + k0;
+        const uint64_t o = (uint64_t)f * NA * a.max_out * a.M_occ + t * a.o_ts + s * a.o_ss + k0;
         if (a.out_sym) {
           float4 *op = reinterpret_cast<float4 *>(a.out_sym + o);
           op[0] = make_float4(y[0].x, y[0].y, y[1].x, y[1].y);
@@ -597,7 +597,7 @@ void decode_reg_kernel(DecodeArgs a) {
     uint32_t refq[NA];
 #pragma unroll
     for (int t = 0; t < NA; t++) {
-      const uint64_t ob = (((uint64_t)I.ref * NA + t) * a.max_out + s) * a.M_occ;
+      const uint64_t ob = (uint64_t)I.ref * NA * a.max_out * a.M_occ + t * a.o_ts + s * a.o_ss;
       refq[t] = 0xFFFFFFFFu;
       if (a.ref_mode == 1 && jq[q] >= 0) refq[t] = a.ref_idx[ob + jq[q]];
     }
@@ -662,7 +662,7 @@ void decode_reg_kernel(DecodeArgs a) {
   // ---- phase B: stores (equalised symbols, indices, per-wave EVM partials)
 #pragma unroll
   for (int t = 0; t < NA; t++) {
-    const uint64_t ob = (((uint64_t)f * NA + t) * a.max_out + s) * a.M_occ;
+    const uint64_t ob = (uint64_t)f * NA * a.max_out * a.M_occ + t * a.o_ts + s * a.o_ss;
 #pragma unroll
     for (int q = 0; q < 4; q++) {
       if (jq[q] < 0) continue;

@@ -633,7 +633,7 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
   uint32_t s = __builtin_amdgcn_readfirstlane(i_begin - pfx[f]);
   uint32_t n_out_f = __builtin_amdgcn_readfirstlane(pfx[f + 1] - pfx[f]);
 
-  const uint64_t rowstep = rfl64((uint64_t)a.max_out * a.M_occ);   // samples between streams
+  const uint64_t rowstep = rfl64(a.o_ts);             // output elements between streams
   const v2f inv_sc = v2f{a.qam.inv_scale, a.qam.inv_scale};
   const v2f Lf = v2f{(float)a.qam.L, (float)a.qam.L};
   const uint32_t Lm1 = a.qam.L - 1;
@@ -681,8 +681,8 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
         const int tr = opq(tid) - RW0 * 64;
         const uint32_t dst = __builtin_amdgcn_readfirstlane(rstg_base + (uint32_t)((wv - RW0) * 64) * 16u);
         const uint32_t t = (uint32_t)tr / (M / 16), q = (uint32_t)tr % (M / 16);
-        const auto rb = sgpr_ptr(a.ref_idx + fb.ref + (uint64_t)ss * a.M_occ);
-        dma16(t * (uint32_t)(a.max_out * a.M_occ) + 16 * q, rb, dst);
+        const auto rb = sgpr_ptr(a.ref_idx + fb.ref + (uint64_t)ss * a.o_ss);
+        dma16(t * (uint32_t)a.o_ts + 16 * q, rb, dst);
       }
     }
   };
@@ -1023,8 +1023,8 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
     DSP(const unsigned long long ds_3 = __builtin_amdgcn_s_memtime(); ds_t[2] += ds_3 - ds_1; ds_t[7] += ds_3 - ds_2b;)
     // apply, demap, EVM, stores: subcarriers k = tid + q T (KADJ: S tid + q) of every stream
     const uint64_t frame_id = a.frame_id0 + (fcr[f] >> 16);
-    // output row (f, t, s) = ob0 + t * max_out * M_occ: uniform, one 64-bit product per symbol
-    const uint64_t ob0 = rfl64((((uint64_t)f * NA) * a.max_out + s) * a.M_occ);
+    // output row (f, t, s) = ob0 + t o_ts: uniform, one 64-bit product per symbol
+    const uint64_t ob0 = rfl64(((uint64_t)f * NA) * a.max_out * a.M_occ + (uint64_t)s * a.o_ss);
     // one output's apply (stream t, slot q): y = sum_r W[t][r][q] gain dn X_r
     auto apply1 = [&](int t, int q, const v2f *X) -> v2f {
       v2f acc = v2f{0.0f, 0.0f};
@@ -1386,11 +1386,11 @@ __global__ __launch_bounds__(32 * NA) void apply_split_kernel(DecodeArgs a) {
   const uint32_t Lm1 = a.qam.L - 1;
   const uint64_t frame_id = a.frame_id0 + I.ref;
   // symbol s of this chunk: 4 KB at spec4 + (s - sym0) * 256 (16 B per thread), reference
-  // indices of stream t at ref + (t * max_out + s) * M_occ (16 B per thread for tid < 32)
+  // indices of stream t at ref + t o_ts + s o_ss (16 B per thread for tid < 32)
   const float4 *spec4 = reinterpret_cast<const float4 *>(a.spec) +
                         ((uint64_t)f * NCH + c) * a.sym_cap * (NA * 64 / 2) + tid;
-  const uint8_t *refb = (REF == 1) ? a.ref_idx + ((uint64_t)I.ref * NA + (tid >> 2)) * a.max_out * a.M_occ +
-                                         c * 64 + (tid & 3) * 16
+  const uint8_t *refb = (REF == 1) ? a.ref_idx + (uint64_t)I.ref * NA * a.max_out * a.M_occ +
+                                         (uint64_t)(tid >> 2) * a.o_ts + c * 64 + (tid & 3) * 16
                                    : nullptr;
   // symbols in flight: slot u holds symbol sb + u; loads are unconditional (past the range
   // they re-read the last symbol) so the slots stay in registers with counted waits
@@ -1401,7 +1401,7 @@ __global__ __launch_bounds__(32 * NA) void apply_split_kernel(DecodeArgs a) {
     const uint32_t sc = min(s, slast);
     x = spec4[(uint64_t)(sc - a.sym0) * (NA * 64 / 2)];
     if constexpr (REF == 1)
-      if (tid < 32) r = *reinterpret_cast<const uint4 *>(refb + (uint64_t)sc * a.M_occ);
+      if (tid < 32) r = *reinterpret_cast<const uint4 *>(refb + (uint64_t)sc * a.o_ss);
   };
   if (s0 < s1) {
     load_sym(pf0, pr0, s0);
@@ -1429,7 +1429,7 @@ __global__ __launch_bounds__(32 * NA) void apply_split_kernel(DecodeArgs a) {
 #pragma unroll
       for (int q = 0; q < NA; q++) acc = cmac_pk(acc, Wr[tt][q], X[q]);
       const uint32_t d = qam_slice_pk(acc, inv_sc, Lf, Lm1, a.qam.b);
-      const uint64_t o = (((uint64_t)f * NA + t) * a.max_out + s) * a.M_occ + k;
+      const uint64_t o = (uint64_t)f * NA * a.max_out * a.M_occ + t * a.o_ts + s * a.o_ss + k;
       uint32_t refi;
       if constexpr (REF == 1) refi = rs[b][t * 64 + lane];
       else if constexpr (REF == 2)
@@ -1532,8 +1532,8 @@ __global__ __launch_bounds__(64 * NA) void apply_split2_kernel(DecodeArgs a) {
                         ((uint64_t)f * NCH + 2 * c2 + half) * a.sym_cap * (NA * 64 / 2) + u;
   v4f *xdst0 = reinterpret_cast<v4f *>(&xs[0][(u >> 5) * CW + half * 64 + 2 * (u & 31)]);
   v4f *xdst1 = reinterpret_cast<v4f *>(&xs[1][(u >> 5) * CW + half * 64 + 2 * (u & 31)]);
-  const uint8_t *refb = (REF == 1) ? a.ref_idx + ((uint64_t)I.ref * NA + (tid >> 3)) * a.max_out * a.M_occ +
-                                         c2 * CW + (tid & 7) * 16
+  const uint8_t *refb = (REF == 1) ? a.ref_idx + (uint64_t)I.ref * NA * a.max_out * a.M_occ +
+                                         (uint64_t)(tid >> 3) * a.o_ts + c2 * CW + (tid & 7) * 16
                                    : nullptr;
   const uint32_t slast = s1 > s0 ? s1 - 1 : s0;
   float4 pf0, pf1, pf2, pf3;                          // symbol slots (named: no scratch)
@@ -1542,7 +1542,7 @@ __global__ __launch_bounds__(64 * NA) void apply_split2_kernel(DecodeArgs a) {
     const uint32_t sc = min(s, slast);
     x = spec4[(uint64_t)(sc - a.sym0) * (NA * 64 / 2)];
     if constexpr (REF == 1)
-      if (tid < 64) r = *reinterpret_cast<const uint4 *>(refb + (uint64_t)sc * a.M_occ);
+      if (tid < 64) r = *reinterpret_cast<const uint4 *>(refb + (uint64_t)sc * a.o_ss);
   };
   if (s0 < s1) {
     load_sym(pf0, pr0, s0);
@@ -1582,7 +1582,7 @@ __global__ __launch_bounds__(64 * NA) void apply_split2_kernel(DecodeArgs a) {
       e_num = __builtin_fmaf(er.x, er.x, __builtin_fmaf(er.y, er.y, e_num));
       e_den = __builtin_fmaf(pt.x, pt.x, __builtin_fmaf(pt.y, pt.y, e_den));
     }
-    const uint64_t o = (((uint64_t)f * NA + w) * a.max_out + s) * a.M_occ + kb;
+    const uint64_t o = (uint64_t)f * NA * a.max_out * a.M_occ + w * a.o_ts + s * a.o_ss + kb;
     // (plain stores: non-temporal ones measured +3.7% on this kernel at C4)
     if (a.out_sym)
       *reinterpret_cast<v4f *>(reinterpret_cast<v2f *>(a.out_sym) + o) =
@@ -2014,8 +2014,8 @@ __global__ __launch_bounds__(kR8T) void decode_res8_kernel(DecodeArgs a) {
       else if (more) issue_row(ynext, g + 2 - NA, (krow + g + 2) % 3u);
       if constexpr (g == 0 && REF == 1) {   // this symbol's reference indices: the dword holding byte k
         const uint32_t tt = tid_now(), h = tt & 1u, k = 8 * (tt >> 1) + q;
-        const uint64_t rowstep = (uint64_t)a.max_out * a.M_occ;
-        const auto rref = sgpr_ptr(a.ref_idx + rfl64((uint64_t)(fcr[f] >> 16) * NA * rowstep + (uint64_t)s * a.M_occ));
+        const uint64_t rowstep = a.o_ts;
+        const auto rref = sgpr_ptr(a.ref_idx + rfl64((uint64_t)(fcr[f] >> 16) * NA * a.max_out * a.M_occ + (uint64_t)s * a.o_ss));
         const uint32_t rb = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)rl + wv * 1024u);
 #pragma unroll
         for (int j = 0; j < 4; j++)
@@ -2081,8 +2081,8 @@ __global__ __launch_bounds__(kR8T) void decode_res8_kernel(DecodeArgs a) {
     }
     const uint32_t cr = fcr[f];
     const uint64_t frame_id = a.frame_id0 + (cr >> 16);
-    const uint64_t rowstep = (uint64_t)a.max_out * a.M_occ;
-    const uint64_t ob0 = rfl64((((uint64_t)f * NA) * a.max_out + s) * a.M_occ);
+    const uint64_t rowstep = a.o_ts;
+    const uint64_t ob0 = rfl64(((uint64_t)f * NA) * a.max_out * a.M_occ + (uint64_t)s * a.o_ss);
     const auto osym = sgpr_ptr(reinterpret_cast<v2f *>(a.out_sym) + ob0);
     const auto oidx = sgpr_ptr(a.out_idx + ob0);
 #pragma unroll

@@ -197,6 +197,7 @@ struct mimo_rx {
   bool cfo = false;                     // opt-in CFO estimate + derotation (batched path)
   int cur_sc16 = 0;                     // the batch being launched reads sc16 wire samples
   float cur_scale = 1.0f;
+  uint32_t cur_layout = 0;              // its output layout (MIMO_LAYOUT_*)
   DevBuf<float2> spec;                  // 8x8 split decode: spectra scratch
   DevBuf<float2> wide;                  // sc16 batches the fused kernels do not take: widened
   DevBuf<float2> cfo_iq;                // derotated scratch capture
@@ -672,6 +673,13 @@ int run_decode(mimo_rx *h, const float2 *iq, uint64_t stride, uint32_t F, uint64
   d.detector = h->det; d.siso_tx = h->siso_tx; d.siso_rx = h->siso_rx; d.dn = h->dn;
   d.occ_index = h->occ.p; d.W = h->W.p; d.gain = h->gain.p; d.G = h->G.p; d.info = h->info.p;
   d.max_out = max_out; d.out_sym = out_sym; d.out_idx = out_idx;
+  if (h->cur_layout == MIMO_LAYOUT_SYMBOL_MAJOR) {   // [F][max_out][N][M_occ]
+    d.o_ts = h->M_occ;
+    d.o_ss = (uint64_t)h->N * h->M_occ;
+  } else {                                         // [F][N][max_out][M_occ]
+    d.o_ts = (uint64_t)max_out * h->M_occ;
+    d.o_ss = h->M_occ;
+  }
   d.ref_mode = ref_mode; d.ref_idx = ref_idx; d.ref_seed = ref_seed; d.frame_id0 = frame_id0;
   d.qam = h->qam; d.evm_part = h->evm_part.p; d.tw = h->tw;
   d.n_frames = F; d.n_cu = h->n_cu;
@@ -991,6 +999,7 @@ static int finish_estimate(mimo_rx *h) {
   const size_t per = (size_t)h->N * h->M_occ;
   if (n_sym) {
     HIPCHK(h->symbuf.ensure(per * n_sym));
+    h->cur_layout = MIMO_LAYOUT_STREAM_MAJOR;        // symbuf is [N][n_sym][M_occ]
     rc = run_decode(h, iq, h->cap_len, 1, h->total, n_sym, h->symbuf.p, nullptr, 0, nullptr, 0,
                     0, h->stream);
     if (rc) return rc;
@@ -1378,6 +1387,7 @@ static int run_batch(mimo_rx *h, const mimo_batch *b, hipStream_t s) {
   const uint32_t fpc = batch_fpc(b), slots = b->n_frames * fpc;
   h->cur_sc16 = 0;
   h->cur_scale = 1.0f;
+  h->cur_layout = b->out_layout;
   if (b->sample_format == MIMO_SAMPLE_SC16) {
     // sc16 wire input: read in place by S&C, the fused search + LS and the streaming decode
     // where the configuration takes them; otherwise widened once into an internal fc32 batch
@@ -1453,6 +1463,7 @@ static int run_batch(mimo_rx *h, const mimo_batch *b, hipStream_t s) {
                     s, b->n_frames, fold ? ca.part : nullptr);
   h->cur_sc16 = 0;
   h->cur_scale = 1.0f;
+  h->cur_layout = 0;
   return rc;
 }
 
@@ -1476,7 +1487,7 @@ static bool same_batch(const mimo_batch &x, const mimo_batch &y) {
          x.d_ref_idx == y.d_ref_idx && x.ref_seed == y.ref_seed && x.frame_id0 == y.frame_id0 &&
          batch_fpc(&x) == batch_fpc(&y) && x.d_ref_starts == y.d_ref_starts &&
          x.ref_stride == y.ref_stride && x.sample_format == y.sample_format &&
-         x.sc16_scale == y.sc16_scale;
+         x.sc16_scale == y.sc16_scale && x.out_layout == y.out_layout;
 }
 
 int mimo_rx_process_batch(mimo_rx *h, const mimo_batch *b, void *hip_stream) {
@@ -1484,6 +1495,8 @@ int mimo_rx_process_batch(mimo_rx *h, const mimo_batch *b, void *hip_stream) {
   if (b->n_frames == 0) return MIMO_OK;
   if (b->stride < b->frame_len) return fail(MIMO_ERR_ARG, "stride < frame_len");
   if (b->ref_mode == 1 && !b->d_ref_idx) return fail(MIMO_ERR_ARG, "ref_mode 1 needs d_ref_idx");
+  if (b->out_layout != MIMO_LAYOUT_STREAM_MAJOR && b->out_layout != MIMO_LAYOUT_SYMBOL_MAJOR)
+    return fail(MIMO_ERR_ARG, "mimo_batch.out_layout must be MIMO_LAYOUT_STREAM_MAJOR or _SYMBOL_MAJOR");
   if (batch_fpc(b) > 64)
     return fail(MIMO_ERR_ARG, "frames_per_capture must be at most 64");
   // the unfolded CFO stages derotate each frame's window into one scratch capture per

@@ -269,8 +269,12 @@ struct DecodeArgs {
   const float2 *G;
   const FrameInfo *info;
   uint32_t max_out;
-  float2 *out_sym;                 // [F][N][max_out][M_occ] or null
+  float2 *out_sym;                 // frame slot f at f N max_out M_occ, or null
   uint8_t *out_idx;                // same layout or null
+  // element strides inside a frame slot (out_sym, out_idx, ref_idx): between streams and
+  // between symbols. MIMO_LAYOUT_STREAM_MAJOR [F][N][max_out][M_occ]: (max_out M_occ, M_occ);
+  // MIMO_LAYOUT_SYMBOL_MAJOR [F][max_out][N][M_occ]: (M_occ, N M_occ)
+  uint64_t o_ts, o_ss;
   int ref_mode;
   const uint8_t *ref_idx;
   uint64_t ref_seed, frame_id0;

@@ -123,23 +123,25 @@ class Receiver:
     def process(self, iq, stride, frame_len, n_frames, max_out=None, out_sym=None, out_idx=None,
                 ref_mode=0, ref_idx=None, ref_seed=0, frame_id0=0, stream=None,
                 frames_per_capture=1, ref_starts=None, ref_stride=0, sc16=False,
-                sc16_scale=None):
+                sc16_scale=None, out_layout=0):
         """One batch (mimo_rx_process_batch). frames_per_capture > 1: every capture is a
         stream of back-to-back frames, received as fresh framesyncs re-armed after each frame
         (frame slots [capture][frames_per_capture]; see include/mimo_rx.h). sc16: iq holds
-        the UHD sc16 wire format (interleaved int16 I/Q), read as float(i16) * sc16_scale."""
+        the UHD sc16 wire format (interleaved int16 I/Q), read as float(i16) * sc16_scale.
+        out_layout: _lib.LAYOUT_STREAM_MAJOR (out_sym, out_idx and ref_idx frame slots are
+        [N][max_out][M_occ]) or _lib.LAYOUT_SYMBOL_MAJOR ([max_out][N][M_occ])."""
         P = self.params
         b = _lib.Batch(_ptr(iq), stride, frame_len, n_frames,
                        P.pid_max if max_out is None else max_out, _ptr(out_sym), _ptr(out_idx),
                        ref_mode, _ptr(ref_idx), ref_seed, frame_id0, frames_per_capture,
                        ref_stride, _ptr(ref_starts), 1 if sc16 else 0,
-                       SC16_SCALE if sc16_scale is None else sc16_scale)
+                       SC16_SCALE if sc16_scale is None else sc16_scale, out_layout)
         check(lib().mimo_rx_process_batch(self._h, C.byref(b), stream), "process_batch")
         self._last = n_frames * max(1, frames_per_capture)
 
     def receive_streams(self, iq, stride, frame_len, n_caps, frames_per_capture, max_out=None,
                         out_sym=None, out_idx=None, ref_mode=0, ref_idx=None, ref_seed=0,
-                        frame_id0=0, ref_starts=None, stream=None):
+                        frame_id0=0, ref_starts=None, stream=None, out_layout=0):
         """Back-to-back frames in n_caps captures (process with frames_per_capture), then
         every capture whose chain stopped at a MIMO_FRAME_RESCAN frame is resumed at that
         frame's origin as a fresh capture, into the same frame slots, until none is left.
@@ -157,7 +159,8 @@ class Receiver:
             dev_rs = torch.from_numpy(rs_host.view(np.int64).copy()).cuda()
         self.process(iq, stride, frame_len, n_caps, max_out=mo, out_sym=out_sym, out_idx=out_idx,
                      ref_mode=ref_mode, ref_idx=ref_idx, ref_seed=ref_seed, frame_id0=frame_id0,
-                     stream=stream, frames_per_capture=K, ref_starts=dev_rs)
+                     stream=stream, frames_per_capture=K, ref_starts=dev_rs,
+                     out_layout=out_layout)
         res = self.results(n_caps * K)
         base = _ptr(iq)
         slot_sym = N * mo * mocc * 8
@@ -203,7 +206,7 @@ class Receiver:
                              max_out=mo, out_sym=dsym, out_idx=didx, ref_mode=ref_mode,
                              ref_idx=refp, ref_seed=ref_seed, frame_id0=fid0, stream=stream,
                              frames_per_capture=max(rem, 2), ref_starts=rs,
-                             ref_stride=K if rs is not None else 0)
+                             ref_stride=K if rs is not None else 0, out_layout=out_layout)
                 if ref2 is not None and scratch is None:
                     # ref2 is read by the asynchronous decode on `stream`: keep it alive until
                     # that work has finished, not just until it is rebound

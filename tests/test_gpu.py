@@ -591,12 +591,19 @@ def _ls_batch_outputs(M, cp, N, nac, pid, qam, det, seed, n_frames):
                  detector=det, keep_identity_bias=True, qam_order=qam)
     rxo = Receiver(P)
     osym = _lib.DeviceBuffer(n_frames * N * pid * M * 8)
+    osym.zero()                          # (frames that do not sync write no symbols)
     rxo.process(out, L, L, n_frames, max_out=pid, out_sym=osym, ref_mode=2, ref_seed=seed)
     res = rxo.results()
+    # frames that did not sync leave G, W and their symbols unwritten: compared as zeros
+    ok = np.array([r["status"] == _lib.FRAME_OK for r in res])
     nv = np.array([r["noise_var"] for r in res], np.float64)
     ev = np.array([[r["evm_num"], r["evm_den"]] for r in res], np.float64)
-    return (rxo.G(), rxo.W(), nv, ev,
-            osym.download(np.complex64, n_frames * N * pid * M))
+    G, W = rxo.G(), rxo.W()
+    G[~ok] = 0
+    W[~ok] = 0
+    y = osym.download(np.complex64, n_frames * N * pid * M).reshape(n_frames, -1)
+    y[~ok] = 0
+    return G, W, nv, ev, y
 
 
 def test_ls_combine_fused_equals_separate_kernel():
@@ -631,6 +638,66 @@ def test_ls_combine_fused_equals_separate_kernel():
             assert nv.tobytes() == o["nv"].tobytes(), c
             assert ev.tobytes() == o["ev"].tobytes(), c
             assert y.tobytes() == o["y"].tobytes(), c
+
+
+def _layout_batch(M, cp, N, nac, pid, qam, det, seed, n_frames, layout, path):
+    """n_frames synthetic frames decoded with out_layout = layout and reference indices
+    (ref_mode 1) in that layout; returns the outputs as stream-major host arrays and the
+    frames' result records."""
+    S = Synthesizer(SynthParams(M=M, cp_len=cp, num_streams=N, num_access_codes=nac, pid=pid,
+                                qam_order=qam, seed=seed, snr_db=30.0))
+    L = max(S.frame_len(i) for i in range(n_frames))
+    rx = Receiver(RxParams(M=M, cp_len=cp, num_streams=N, num_access_codes=nac, pid_max=pid,
+                           detector=det, keep_identity_bias=True, qam_order=qam))
+    mocc = rx.M_occ
+    out = _lib.DeviceBuffer(n_frames * N * L * 8)
+    tx = _lib.DeviceBuffer(n_frames * N * pid * mocc)
+    S.generate(out, L, L, n_frames, tx_idx=tx)
+    txi = tx.download(np.uint8, n_frames * N * pid * mocc).reshape(n_frames, N, pid, mocc)
+    ref = _lib.DeviceBuffer(txi.nbytes)
+    sym_major = layout == _lib.LAYOUT_SYMBOL_MAJOR
+    ref.upload(np.ascontiguousarray(txi.transpose(0, 2, 1, 3) if sym_major else txi))
+    osym = _lib.DeviceBuffer(n_frames * N * pid * mocc * 8)
+    oidx = _lib.DeviceBuffer(n_frames * N * pid * mocc)
+    rx.process(out, L, L, n_frames, max_out=pid, out_sym=osym, out_idx=oidx, ref_mode=1,
+               ref_idx=ref, out_layout=layout)
+    res = rx.results()                   # (synchronises the receiver's stream)
+    assert rx.decode_path() == path, (rx.decode_path(), path)
+    shape = (n_frames, pid, N, mocc) if sym_major else (n_frames, N, pid, mocc)
+    y = osym.download(np.complex64, n_frames * N * pid * mocc).reshape(shape)
+    d = oidx.download(np.uint8, n_frames * N * pid * mocc).reshape(shape)
+    if sym_major:
+        y, d = y.transpose(0, 2, 1, 3), d.transpose(0, 2, 1, 3)
+    return np.ascontiguousarray(y), np.ascontiguousarray(d), res
+
+
+@pytest.mark.parametrize("case", [
+    (1024, 76, 2, 20, 24, 16, _lib.DET_ZF2, 61, 3, _lib.DECODE_STREAM),
+    (2048, 152, 4, 20, 12, 64, _lib.DET_MMSE, 62, 3, _lib.DECODE_STREAM),
+    (4096, 304, 8, 2, 66, 256, _lib.DET_MMSE, 63, 2, _lib.DECODE_SPLIT),
+    (4096, 304, 8, 2, 12, 256, _lib.DET_MMSE, 64, 2, _lib.DECODE_SYMBOL),
+    (64, 16, 2, 4, 10, 4, _lib.DET_ZF2, 65, 3, _lib.DECODE_SYMBOL),
+], ids=["c2_stream", "c3_stream", "c4_split", "c4_symbol", "m64_guard_symbol"])
+def test_symbol_major_layout_equals_stream_major(case):
+    """mimo_batch.out_layout = SYMBOL_MAJOR ([F][max_out][N][M_occ], reference rows likewise)
+    writes exactly the stream-major outputs, transposed, on every decode path (streaming,
+    8x8 split, per-symbol incl. a guard-band geometry); results (EVM sums, symbol errors) are
+    bitwise the same."""
+    *geo, path = case
+    pid = geo[4]
+    y0, d0, r0 = _layout_batch(*geo, _lib.LAYOUT_STREAM_MAJOR, path)
+    y1, d1, r1 = _layout_batch(*geo, _lib.LAYOUT_SYMBOL_MAJOR, path)
+    assert any(r["status"] == _lib.FRAME_OK for r in r0)
+    for f, (a, b) in enumerate(zip(r0, r1)):
+        assert a["status"] == b["status"]
+        if a["status"] != _lib.FRAME_OK:
+            continue                      # (a frame without sync writes no outputs)
+        n = min(a["n_sym"], pid)
+        assert np.array_equal(y0[f, :, :n].view(np.uint32), y1[f, :, :n].view(np.uint32)), f
+        assert np.array_equal(d0[f, :, :n], d1[f, :, :n]), f
+        assert a["evm_num"].tobytes() == b["evm_num"].tobytes()
+        assert a["evm_den"].tobytes() == b["evm_den"].tobytes()
+        assert np.array_equal(a["errors"], b["errors"])
 
 
 def test_c3_4x4_mmse_2048_64qam_full_frame():

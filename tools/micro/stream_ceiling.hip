@@ -35,7 +35,8 @@ __device__ inline void dma16(uint32_t voff, const void *sbase, uint32_t lds) {
                  "global_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
                  : "=&s"(keep) : "v"(voff), "s"(sbase), "s"(lds) : "memory");
 }
-// OPT bits: 1 plain (not nt) stores, 2 plain DMA loads, 4 no index stores
+// OPT bits: 1 plain (not nt) stores, 2 plain DMA loads, 4 no index stores, 8 symbol-major
+// outputs ([frame][symbol][stream][M]: a symbol's streams contiguous, instead of [frame][stream][symbol][M])
 template <bool NT, typename V, typename P>
 __device__ inline void st(V v, P p) {
   if constexpr (NT) __builtin_nontemporal_store(v, p);
@@ -105,7 +106,8 @@ __global__ __launch_bounds__(T) void kern(const float2 *iq, uint64_t L, const ui
     if (MODE != 2 && MODE != 4) {
       const uint32_t kb = 2 * (uint32_t)tid;
       for (int t = 0; t < NA; t++) {
-        const uint64_t ob = ((uint64_t)(f * NA + t) * spf + s) * M;
+        const uint64_t ob = (OPT & 8) ? ((uint64_t)(f * spf + s) * NA + t) * M
+                                      : ((uint64_t)(f * NA + t) * spf + s) * M;
         st<!(OPT & 1)>(v4f{v[2 * t].x, v[2 * t].y, v[2 * t + 1].x, v[2 * t + 1].y},
                        reinterpret_cast<v4f *>(osym + ob + kb));
         if constexpr (!(OPT & 4))
@@ -173,5 +175,11 @@ int main() {
   rep("mode3 (stores only)", run<3, 0, 0>(iq, L, ref, osym, oidx, nsym, spf, sink, ncu), bytes_ld);
   rep("mode3 (stores only, plain)", run<3, 0, 0, 1>(iq, L, ref, osym, oidx, nsym, spf, sink, ncu), bytes_ld);
   rep("mode0 fill 12 ldsx 3", run<0, 12, 3>(iq, L, ref, osym, oidx, nsym, spf, sink, ncu), bytes);
+  rep("mode0 symbol-major", run<0, 0, 0, 8>(iq, L, ref, osym, oidx, nsym, spf, sink, ncu), bytes);
+  rep("mode0 symbol-major plain stores", run<0, 0, 0, 9>(iq, L, ref, osym, oidx, nsym, spf, sink, ncu), bytes);
+  rep("mode3 symbol-major", run<3, 0, 0, 8>(iq, L, ref, osym, oidx, nsym, spf, sink, ncu), bytes_ld);
+  rep("mode3 symbol-major plain", run<3, 0, 0, 9>(iq, L, ref, osym, oidx, nsym, spf, sink, ncu), bytes_ld);
+  rep("mode0 (kernel schedule) again", run<0, 0, 0>(iq, L, ref, osym, oidx, nsym, spf, sink, ncu), bytes);
+  rep("mode3 (stores only) again", run<3, 0, 0>(iq, L, ref, osym, oidx, nsym, spf, sink, ncu), bytes_ld);
   return 0;
 }
