@@ -1225,10 +1225,22 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
 // (RMIMO_SPLIT_GROUP, off by default: see split_group_symbols). EVM records: symbol group x
 // chunk x range per frame (nrec), NA/2 per record.
 constexpr uint32_t kSplitSets = 16;   // EVM partial sets per record (<= kMaxEvmParts)
+// the split decode's spectra scratch: [F][M / CH][sym_cap][N][CH] complex64, CH subcarriers of
+// one (symbol, antenna) contiguous
+#ifndef SPEC_CH
+#define SPEC_CH 512   // (64 / 128 / 256 / 512 measured at C4: 512 is 1.2% faster than 64, profiles/r05/ab/r05_specch.txt)
+#endif
+constexpr uint32_t kSpecCH = SPEC_CH;
+static_assert(kSpecCH >= 64 && (kSpecCH & (kSpecCH - 1)) == 0, "power-of-two chunks of >= 64");
+// float2 offset of (chunk-relative) subcarrier k of antenna r, scratch slot sl, frame f
+MIMO_DEV uint64_t spec_off(const DecodeArgs &a, uint32_t f, uint32_t sl, uint32_t r, uint32_t k) {
+  const uint32_t nch = a.M / kSpecCH;
+  return ((((uint64_t)f * nch + k / kSpecCH) * a.sym_cap + sl) * a.N + r) * kSpecCH + k % kSpecCH;
+}
 
 template <int LOG2M, int T, bool SC16>
 __global__ __launch_bounds__(T) void spectra_kernel(DecodeArgs a) {
-  constexpr int M = 1 << LOG2M, NCH = M / 64;
+  constexpr int M = 1 << LOG2M;
   extern __shared__ __attribute__((aligned(16))) float2 lds_sp[];
   const uint32_t f = blockIdx.y, sl = blockIdx.x, r = blockIdx.z;
   const uint32_t s = a.sym0 + sl;                     // symbol; sl its scratch slot
@@ -1254,10 +1266,10 @@ __global__ __launch_bounds__(T) void spectra_kernel(DecodeArgs a) {
   }
   __syncthreads();
   fft_lds<LOG2M, T, 1, false>(lds_sp, a.tw);
-  float2 *o = a.spec + (((uint64_t)f * NCH * a.sym_cap + sl) * a.N + r) * 64;
-  const uint64_t cstep = (uint64_t)a.sym_cap * a.N * 64;
+  float2 *o = a.spec + spec_off(a, f, sl, r, 0);
+  const uint64_t cstep = (uint64_t)a.sym_cap * a.N * kSpecCH;
 #pragma unroll
-  for (int k = tid; k < M; k += T) o[(uint64_t)(k >> 6) * cstep + (k & 63)] = lds_sp[lds_pad(k)];
+  for (int k = tid; k < M; k += T) o[(uint64_t)(k / kSpecCH) * cstep + (k % kSpecCH)] = lds_sp[lds_pad(k)];
 }
 
 // Persistent form of spectra_kernel for M = 2^LOG2M >= 2048 (C4: M = 4096): each workgroup
@@ -1270,7 +1282,7 @@ __global__ __launch_bounds__(T) void spectra_kernel(DecodeArgs a) {
 template <int LOG2M, bool SC16>
 __global__ __launch_bounds__((1 << LOG2M) / 16) void spectra_persist_kernel(DecodeArgs a) {
   using PL = RegPlan<LOG2M, 16>;
-  constexpr int M = 1 << LOG2M, T = PL::T, NCH = M / 64;
+  constexpr int M = 1 << LOG2M, T = PL::T;
   static_assert(T % 64 == 0, "whole waves");
   extern __shared__ __attribute__((aligned(16))) float2 lds_sp[];
   v2f *buf = reinterpret_cast<v2f *>(lds_sp);
@@ -1329,12 +1341,12 @@ __global__ __launch_bounds__((1 << LOG2M) / 16) void spectra_persist_kernel(Deco
     reg_compute<LOG2M, 16, 0, false>(v, w1);
     reg_rest<LOG2M, 16, 1, false>(buf, v, w1, tid);
     // X[k], k = tid + T e, into [frame][chunk][slot][antenna][64]
-    float2 *o = a.spec + (((uint64_t)f * NCH * a.sym_cap + sl) * a.N + r) * 64;
-    const uint64_t cstep = (uint64_t)a.sym_cap * a.N * 64;
+    float2 *o = a.spec + spec_off(a, f, sl, r, 0);
+    const uint64_t cstep = (uint64_t)a.sym_cap * a.N * kSpecCH;
 #pragma unroll
     for (int e = 0; e < 16; e++) {
       const uint32_t k = (uint32_t)reg_index<LOG2M, 16>(tid, e);
-      o[(uint64_t)(k >> 6) * cstep + (k & 63)] = make_float2(v[e].x, v[e].y);
+      o[(uint64_t)(k / kSpecCH) * cstep + (k % kSpecCH)] = make_float2(v[e].x, v[e].y);
     }
     if (nit >= total) break;                          // uniform
     it = nit; f = nf; sl = nsl; r = nr;
@@ -1387,8 +1399,9 @@ __global__ __launch_bounds__(32 * NA) void apply_split_kernel(DecodeArgs a) {
   const uint64_t frame_id = a.frame_id0 + I.ref;
   // symbol s of this chunk: 4 KB at spec4 + (s - sym0) * 256 (16 B per thread), reference
   // indices of stream t at ref + t o_ts + s o_ss (16 B per thread for tid < 32)
-  const float4 *spec4 = reinterpret_cast<const float4 *>(a.spec) +
-                        ((uint64_t)f * NCH + c) * a.sym_cap * (NA * 64 / 2) + tid;
+  // (thread tid: antenna tid / 32, subcarriers c 64 + 2 (tid % 32) + 0, 1; symbols N CH apart)
+  const float4 *spec4 = reinterpret_cast<const float4 *>(
+      a.spec + spec_off(a, f, 0, (uint32_t)tid >> 5, c * 64 + 2 * ((uint32_t)tid & 31u)));
   const uint8_t *refb = (REF == 1) ? a.ref_idx + (uint64_t)I.ref * NA * a.max_out * a.M_occ +
                                          (uint64_t)(tid >> 2) * a.o_ts + c * 64 + (tid & 3) * 16
                                    : nullptr;
@@ -1399,7 +1412,7 @@ __global__ __launch_bounds__(32 * NA) void apply_split_kernel(DecodeArgs a) {
   uint4 pr0, pr1, pr2, pr3;
   auto load_sym = [&](float4 &x, uint4 &r, uint32_t s) {
     const uint32_t sc = min(s, slast);
-    x = spec4[(uint64_t)(sc - a.sym0) * (NA * 64 / 2)];
+    x = spec4[(uint64_t)(sc - a.sym0) * (NA * kSpecCH / 2)];
     if constexpr (REF == 1)
       if (tid < 32) r = *reinterpret_cast<const uint4 *>(refb + (uint64_t)sc * a.o_ss);
   };
@@ -1490,7 +1503,7 @@ __global__ __launch_bounds__(64 * NA) void apply_split2_kernel(DecodeArgs a) {
   constexpr int CW = 128;                             // subcarriers per chunk
   static_assert(NA == 8, "one 16-byte load per thread covers a symbol's 8 x 128 spectra");
   const uint32_t c2 = blockIdx.x, f = blockIdx.y, part = blockIdx.z;
-  const uint32_t NCH2 = gridDim.x, P = gridDim.z, NCH = 2 * NCH2;   // NCH: scratch chunks of 64
+  const uint32_t NCH2 = gridDim.x, P = gridDim.z;
   const int tid = threadIdx.x, lane = tid & 63;
   const uint32_t w = __builtin_amdgcn_readfirstlane((uint32_t)tid >> 6);
   __shared__ v2f ptab[kStreamMaxQam];
@@ -1524,14 +1537,13 @@ __global__ __launch_bounds__(64 * NA) void apply_split2_kernel(DecodeArgs a) {
   const v2f Lf = v2f{(float)a.qam.L, (float)a.qam.L};
   const uint32_t Lm1 = a.qam.L - 1;
   const uint64_t frame_id = a.frame_id0 + I.ref;
-  // thread t loads float4 u = t % 256 of the symbol's 4 KB block of 64-chunk 2 c2 + t / 256
-  // (antenna u / 32, subcarriers 2 (u % 32) + 0, 1); threads < 64 load 16 bytes of reference
-  // indices (stream t / 8, bytes 16 (t % 8) ..)
-  const uint32_t half = (uint32_t)tid >> 8, u = (uint32_t)tid & 255u;
-  const float4 *spec4 = reinterpret_cast<const float4 *>(a.spec) +
-                        ((uint64_t)f * NCH + 2 * c2 + half) * a.sym_cap * (NA * 64 / 2) + u;
-  v4f *xdst0 = reinterpret_cast<v4f *>(&xs[0][(u >> 5) * CW + half * 64 + 2 * (u & 31)]);
-  v4f *xdst1 = reinterpret_cast<v4f *>(&xs[1][(u >> 5) * CW + half * 64 + 2 * (u & 31)]);
+  // thread t loads the float4 of antenna t / 64, subcarriers c2 CW + 2 (t % 64) + 0, 1 (symbols
+  // N CH apart in the scratch); threads < 64 load 16 bytes of reference indices (stream t / 8,
+  // bytes 16 (t % 8) ..)
+  const uint32_t ant = (uint32_t)tid >> 6, pr = (uint32_t)tid & 63u;
+  const float4 *spec4 = reinterpret_cast<const float4 *>(a.spec + spec_off(a, f, 0, ant, c2 * CW + 2 * pr));
+  v4f *xdst0 = reinterpret_cast<v4f *>(&xs[0][ant * CW + 2 * pr]);
+  v4f *xdst1 = reinterpret_cast<v4f *>(&xs[1][ant * CW + 2 * pr]);
   const uint8_t *refb = (REF == 1) ? a.ref_idx + (uint64_t)I.ref * NA * a.max_out * a.M_occ +
                                          (uint64_t)(tid >> 3) * a.o_ts + c2 * CW + (tid & 7) * 16
                                    : nullptr;
@@ -1540,7 +1552,7 @@ __global__ __launch_bounds__(64 * NA) void apply_split2_kernel(DecodeArgs a) {
   uint4 pr0, pr1, pr2, pr3;
   auto load_sym = [&](float4 &x, uint4 &r, uint32_t s) {
     const uint32_t sc = min(s, slast);
-    x = spec4[(uint64_t)(sc - a.sym0) * (NA * 64 / 2)];
+    x = spec4[(uint64_t)(sc - a.sym0) * (NA * kSpecCH / 2)];
     if constexpr (REF == 1)
       if (tid < 64) r = *reinterpret_cast<const uint4 *>(refb + (uint64_t)sc * a.o_ss);
   };
