@@ -122,6 +122,35 @@ __global__ __launch_bounds__(T) void kern(const float2 *iq, uint64_t L, const ui
   }
 }
 
+// pure write rate: n16 16-byte non-temporal stores (ILV 0: a contiguous chunk per workgroup,
+// 1: grid-stride, every workgroup's wave stores adjacent)
+template <int ILV>
+__global__ __launch_bounds__(T) void wkern(v4f *out, uint64_t n16) {
+  const uint64_t G = (uint64_t)gridDim.x * T;
+  if (ILV) {
+    for (uint64_t i = (uint64_t)blockIdx.x * T + threadIdx.x; i < n16; i += G)
+      __builtin_nontemporal_store(v4f{1.0f, 2.0f, 3.0f, (float)i}, out + i);
+  } else {
+    const uint64_t per = (n16 + gridDim.x - 1) / gridDim.x, b = blockIdx.x * per;
+    const uint64_t e = b + per < n16 ? b + per : n16;
+    for (uint64_t i = b + threadIdx.x; i < e; i += T)
+      __builtin_nontemporal_store(v4f{1.0f, 2.0f, 3.0f, (float)i}, out + i);
+  }
+}
+template <int ILV>
+float wrun(v4f *out, uint64_t n16, int ncu) {
+  hipEvent_t a, b;
+  CHK(hipEventCreate(&a)); CHK(hipEventCreate(&b));
+  for (int w = 0; w < 3; w++) wkern<ILV><<<ncu, T>>>(out, n16);
+  CHK(hipEventRecord(a));
+  for (int w = 0; w < 10; w++) wkern<ILV><<<ncu, T>>>(out, n16);
+  CHK(hipEventRecord(b));
+  CHK(hipEventSynchronize(b));
+  float ms;
+  CHK(hipEventElapsedTime(&ms, a, b));
+  return ms / 10;
+}
+
 template <int MODE, int FILL, int LDSX, int OPT = 0>
 float run(const float2 *iq, uint64_t L, const uint8_t *ref, float2 *osym, uint8_t *oidx, uint32_t nsym,
           uint32_t spf, float *sink, int ncu) {
@@ -175,6 +204,15 @@ int main() {
   rep("mode3 (stores only)", run<3, 0, 0>(iq, L, ref, osym, oidx, nsym, spf, sink, ncu), bytes_ld);
   rep("mode3 (stores only, plain)", run<3, 0, 0, 1>(iq, L, ref, osym, oidx, nsym, spf, sink, ncu), bytes_ld);
   rep("mode0 fill 12 ldsx 3", run<0, 12, 3>(iq, L, ref, osym, oidx, nsym, spf, sink, ncu), bytes);
+  {
+    // the symbol buffer's bytes exactly (osym holds nsym NA M complex64)
+    const size_t osym_bytes = sizeof(float2) * (size_t)nf * NA * spf * M;
+    const uint64_t n16 = osym_bytes / 16;
+    if (n16 * 16 > osym_bytes) { printf("bad size\n"); return 1; }
+    rep("pure 16 B nt stores, chunk per WG", wrun<0>(reinterpret_cast<v4f *>(osym), n16, ncu), (double)osym_bytes);
+    rep("pure 16 B nt stores, grid-stride", wrun<1>(reinterpret_cast<v4f *>(osym), n16, ncu), (double)osym_bytes);
+  }
+  rep("mode3 symbol-major, no index stores", run<3, 0, 0, 12>(iq, L, ref, osym, oidx, nsym, spf, sink, ncu), (double)nsym * NA * M * 8);
   rep("mode0 symbol-major", run<0, 0, 0, 8>(iq, L, ref, osym, oidx, nsym, spf, sink, ncu), bytes);
   rep("mode0 symbol-major plain stores", run<0, 0, 0, 9>(iq, L, ref, osym, oidx, nsym, spf, sink, ncu), bytes);
   rep("mode3 symbol-major", run<3, 0, 0, 8>(iq, L, ref, osym, oidx, nsym, spf, sink, ncu), bytes_ld);
