@@ -1225,17 +1225,13 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
 // (RMIMO_SPLIT_GROUP, off by default: see split_group_symbols). EVM records: symbol group x
 // chunk x range per frame (nrec), NA/2 per record.
 constexpr uint32_t kSplitSets = 16;   // EVM partial sets per record (<= kMaxEvmParts)
-// the split decode's spectra scratch: [F][M / CH][sym_cap][N][CH] complex64, CH subcarriers of
-// one (symbol, antenna) contiguous
-#ifndef SPEC_CH
-#define SPEC_CH 512   // (64 / 128 / 256 / 512 measured at C4: 512 is 1.2% faster than 64, profiles/r05/ab/r05_specch.txt)
-#endif
-constexpr uint32_t kSpecCH = SPEC_CH;
-static_assert(kSpecCH >= 64 && (kSpecCH & (kSpecCH - 1)) == 0, "power-of-two chunks of >= 64");
-// float2 offset of (chunk-relative) subcarrier k of antenna r, scratch slot sl, frame f
+// the split decode's spectra scratch: [F][sym_cap][N][M] complex64, each (symbol, antenna)
+// spectrum one contiguous row: the spectra pass writes one sequential 8 M-byte run per item
+// (chunked forms [F][M / CH][sym_cap][N][CH] measured slower the smaller CH: C4 decode 1.335 /
+// 1.317 / 1.290 / 1.254 ms at CH = 64 / 512 / 1024 / M, profiles/r05/ab/r05_specch.txt)
+// float2 offset of subcarrier k of antenna r, scratch slot sl, frame f
 MIMO_DEV uint64_t spec_off(const DecodeArgs &a, uint32_t f, uint32_t sl, uint32_t r, uint32_t k) {
-  const uint32_t nch = a.M / kSpecCH;
-  return ((((uint64_t)f * nch + k / kSpecCH) * a.sym_cap + sl) * a.N + r) * kSpecCH + k % kSpecCH;
+  return (((uint64_t)f * a.sym_cap + sl) * a.N + r) * a.M + k;
 }
 
 template <int LOG2M, int T, bool SC16>
@@ -1267,9 +1263,8 @@ __global__ __launch_bounds__(T) void spectra_kernel(DecodeArgs a) {
   __syncthreads();
   fft_lds<LOG2M, T, 1, false>(lds_sp, a.tw);
   float2 *o = a.spec + spec_off(a, f, sl, r, 0);
-  const uint64_t cstep = (uint64_t)a.sym_cap * a.N * kSpecCH;
 #pragma unroll
-  for (int k = tid; k < M; k += T) o[(uint64_t)(k / kSpecCH) * cstep + (k % kSpecCH)] = lds_sp[lds_pad(k)];
+  for (int k = tid; k < M; k += T) o[k] = lds_sp[lds_pad(k)];
 }
 
 // Persistent form of spectra_kernel for M = 2^LOG2M >= 2048 (C4: M = 4096): each workgroup
@@ -1342,11 +1337,10 @@ __global__ __launch_bounds__((1 << LOG2M) / 16) void spectra_persist_kernel(Deco
     reg_rest<LOG2M, 16, 1, false>(buf, v, w1, tid);
     // X[k], k = tid + T e, into [frame][chunk][slot][antenna][64]
     float2 *o = a.spec + spec_off(a, f, sl, r, 0);
-    const uint64_t cstep = (uint64_t)a.sym_cap * a.N * kSpecCH;
 #pragma unroll
     for (int e = 0; e < 16; e++) {
       const uint32_t k = (uint32_t)reg_index<LOG2M, 16>(tid, e);
-      o[(uint64_t)(k / kSpecCH) * cstep + (k % kSpecCH)] = make_float2(v[e].x, v[e].y);
+      o[k] = make_float2(v[e].x, v[e].y);
     }
     if (nit >= total) break;                          // uniform
     it = nit; f = nf; sl = nsl; r = nr;
@@ -1399,7 +1393,7 @@ __global__ __launch_bounds__(32 * NA) void apply_split_kernel(DecodeArgs a) {
   const uint64_t frame_id = a.frame_id0 + I.ref;
   // symbol s of this chunk: 4 KB at spec4 + (s - sym0) * 256 (16 B per thread), reference
   // indices of stream t at ref + t o_ts + s o_ss (16 B per thread for tid < 32)
-  // (thread tid: antenna tid / 32, subcarriers c 64 + 2 (tid % 32) + 0, 1; symbols N CH apart)
+  // (thread tid: antenna tid / 32, subcarriers c 64 + 2 (tid % 32) + 0, 1; symbols N M apart)
   const float4 *spec4 = reinterpret_cast<const float4 *>(
       a.spec + spec_off(a, f, 0, (uint32_t)tid >> 5, c * 64 + 2 * ((uint32_t)tid & 31u)));
   const uint8_t *refb = (REF == 1) ? a.ref_idx + (uint64_t)I.ref * NA * a.max_out * a.M_occ +
@@ -1412,7 +1406,7 @@ __global__ __launch_bounds__(32 * NA) void apply_split_kernel(DecodeArgs a) {
   uint4 pr0, pr1, pr2, pr3;
   auto load_sym = [&](float4 &x, uint4 &r, uint32_t s) {
     const uint32_t sc = min(s, slast);
-    x = spec4[(uint64_t)(sc - a.sym0) * (NA * kSpecCH / 2)];
+    x = spec4[(uint64_t)(sc - a.sym0) * (NA * a.M / 2)];
     if constexpr (REF == 1)
       if (tid < 32) r = *reinterpret_cast<const uint4 *>(refb + (uint64_t)sc * a.o_ss);
   };
@@ -1538,7 +1532,7 @@ __global__ __launch_bounds__(64 * NA) void apply_split2_kernel(DecodeArgs a) {
   const uint32_t Lm1 = a.qam.L - 1;
   const uint64_t frame_id = a.frame_id0 + I.ref;
   // thread t loads the float4 of antenna t / 64, subcarriers c2 CW + 2 (t % 64) + 0, 1 (symbols
-  // N CH apart in the scratch); threads < 64 load 16 bytes of reference indices (stream t / 8,
+  // N M apart in the scratch); threads < 64 load 16 bytes of reference indices (stream t / 8,
   // bytes 16 (t % 8) ..)
   const uint32_t ant = (uint32_t)tid >> 6, pr = (uint32_t)tid & 63u;
   const float4 *spec4 = reinterpret_cast<const float4 *>(a.spec + spec_off(a, f, 0, ant, c2 * CW + 2 * pr));
@@ -1552,7 +1546,7 @@ __global__ __launch_bounds__(64 * NA) void apply_split2_kernel(DecodeArgs a) {
   uint4 pr0, pr1, pr2, pr3;
   auto load_sym = [&](float4 &x, uint4 &r, uint32_t s) {
     const uint32_t sc = min(s, slast);
-    x = spec4[(uint64_t)(sc - a.sym0) * (NA * kSpecCH / 2)];
+    x = spec4[(uint64_t)(sc - a.sym0) * (NA * a.M / 2)];
     if constexpr (REF == 1)
       if (tid < 64) r = *reinterpret_cast<const uint4 *>(refb + (uint64_t)sc * a.o_ss);
   };

@@ -703,7 +703,7 @@ int run_decode(mimo_rx *h, const float2 *iq, uint64_t stride, uint32_t F, uint64
   if (d.expt == 0 && decode_res8_accepts(d, h->log2M, F))   // residue-class records per frame
     d.rec_stride = std::max(d.rec_stride, res8_records(h->n_cu));
   if (!no_split && d.expt == 0 && decode_split_accepts(d, h->log2M)) {
-    // [F][M/64][group][N][64] complex64 spectra of the 8x8 split decode (one symbol group)
+    // [F][group][N][M] complex64 spectra of the 8x8 split decode (one symbol group)
     if (h->spec.ensure((size_t)F * split_group_symbols(max_out) * h->N * h->M) != hipSuccess)
       return fail(MIMO_ERR_NOMEM, "split decode scratch");
     d.spec = h->spec.p;

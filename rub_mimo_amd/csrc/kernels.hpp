@@ -287,7 +287,7 @@ struct DecodeArgs {
   uint32_t n_cu;                   // compute units (persistent grid size)
   unsigned long long *prof;        // diagnostics: [items, load, fft, apply, reduce] cycles
   uint32_t *nrec;                  // [F] EVM records per frame (decode_stream_kernel) or null
-  float2 *spec;                    // split decode (8x8) spectra scratch [F][M/64][sym_cap][N][64]
+  float2 *spec;                    // split decode (8x8) spectra scratch [F][sym_cap][N][M]
   uint32_t sym0, sym_cap, sym_groups;   // split decode: this launch's symbol group (set inside)
   uint32_t rec_stride;             // EVM records per frame in evm_part (max_out, or the split's)
   int cpe;                         // opt-in CFO: decision-directed common-phase tracking; 2 =
