@@ -213,3 +213,44 @@ def test_c5_streams_8x3_c3_frames_match_oracle(tmp_path):
             assert np.abs(e_gpu - e_ref).max() <= EVM_DB_TOL, (s, k, e_gpu, e_ref)
             n_frames += 1
     assert n_frames >= S * J // 2, n_frames
+
+
+def test_streams_symbol_major_layout_equals_stream_major():
+    """Back-to-back streams (frames_per_capture > 1, the C5 path) with mimo_batch.out_layout =
+    SYMBOL_MAJOR: every frame slot's outputs are the stream-major ones transposed, bit for bit,
+    and the per-slot results (origins, EVM sums, errors against the transposed reference rows)
+    are identical. Also an out-of-range layout is refused."""
+    import torch
+    S, J, K, pid = 3, 2, 3, 40
+    iq, L, tx, starts = synth_streams(S, J, K, seed=907, pid=pid)
+    M, N = 2048, 4
+    outs = []
+    for layout in (_lib.LAYOUT_STREAM_MAJOR, _lib.LAYOUT_SYMBOL_MAJOR):
+        rxo = Receiver(RxParams(M=M, cp_len=152, num_streams=N, num_access_codes=20,
+                                pid_max=pid, detector=_lib.DET_MMSE, qam_order=64))
+        sm = layout == _lib.LAYOUT_SYMBOL_MAJOR
+        shape = (S * K, pid, N, M) if sm else (S * K, N, pid, M)
+        sym = torch.zeros(shape, dtype=torch.complex64, device="cuda")
+        idx = torch.zeros(shape, dtype=torch.uint8, device="cuda")
+        refr = (tx.transpose(1, 2) if sm else tx).contiguous()
+        res = rxo.receive_streams(iq, L, L, S, K, max_out=pid, out_sym=sym, out_idx=idx,
+                                  ref_mode=1, ref_idx=refr, ref_starts=starts, out_layout=layout)
+        torch.cuda.synchronize()
+        if sm:
+            sym, idx = sym.transpose(1, 2), idx.transpose(1, 2)
+        outs.append((res, sym.contiguous().cpu().numpy(), idx.contiguous().cpu().numpy()))
+    (r0, y0, d0), (r1, y1, d1) = outs
+    assert sum(r["status"] == _lib.FRAME_OK for r in r0) >= S
+    for q, (a, b) in enumerate(zip(r0, r1)):
+        assert (a["status"], a["origin"], a["sync_index"]) == (b["status"], b["origin"], b["sync_index"])
+        if a["status"] != _lib.FRAME_OK:
+            continue
+        n = min(a["n_sym"], pid)
+        assert np.array_equal(y0[q, :, :n].view(np.uint32), y1[q, :, :n].view(np.uint32)), q
+        assert np.array_equal(d0[q, :, :n], d1[q, :, :n]), q
+        assert a["evm_num"].tobytes() == b["evm_num"].tobytes()
+        assert np.array_equal(a["errors"], b["errors"])
+    rxo = Receiver(RxParams(M=M, cp_len=152, num_streams=N, num_access_codes=20, pid_max=pid,
+                            detector=_lib.DET_MMSE, qam_order=64))
+    with pytest.raises(_lib.MimoError):
+        rxo.process(iq, L, L, 1, max_out=pid, out_layout=2)
