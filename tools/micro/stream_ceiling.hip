@@ -55,7 +55,12 @@ __global__ __launch_bounds__(T) void kern(const float2 *iq, uint64_t L, const ui
   const int tid = threadIdx.x, lane = tid & 63;
   const uint32_t wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const uint32_t chunk = (nsym + gridDim.x - 1) / gridDim.x;
-  const uint32_t i0 = blockIdx.x * chunk, i1 = min(i0 + chunk, nsym);
+  // OPT 16: symbols interleaved over the grid (workgroup b takes b, b + G, ..: every
+  // workgroup's writes adjacent to the others'), else a contiguous chunk per workgroup
+  constexpr bool ILV = (OPT & 16) != 0;
+  const uint32_t i0 = ILV ? blockIdx.x : blockIdx.x * chunk;
+  const uint32_t i1 = ILV ? nsym : min(i0 + chunk, nsym);
+  const uint32_t ST = ILV ? gridDim.x : 1u;
   if (i0 >= i1) return;
   const uint32_t rowwave0 = 0;
   auto fetch = [&](uint32_t i, float2 *stg) {
@@ -79,19 +84,21 @@ __global__ __launch_bounds__(T) void kern(const float2 *iq, uint64_t L, const ui
   __syncthreads();
   float acc = 0.0f;
   const unsigned long long c0 = __builtin_amdgcn_s_memtime();
-  for (uint32_t i = i0; i < i1; i++) {
-    float2 *cur = (DB && (i - i0) % 2) ? stg1 : stg0;
-    float2 *nxt = (DB && (i - i0) % 2) ? stg0 : stg1;
+  uint32_t nsym_wg = 0;
+  for (uint32_t i = i0; i < i1; i += ST) {
+    nsym_wg++;
+    float2 *cur = (DB && ((i - i0) / ST) % 2) ? stg1 : stg0;
+    float2 *nxt = (DB && ((i - i0) / ST) % 2) ? stg0 : stg1;
     asm volatile("s_waitcnt vmcnt(%0)" :: "n"(MODE == 2 || MODE == 4 ? 0 : ((OPT & 4) ? NSTORE / 2 : NSTORE)) : "memory");
     __syncthreads();
-    if (DB && i + 1 < i1) fetch(i + 1, nxt);
+    if (DB && i + ST < i1) fetch(i + ST, nxt);
     const uint32_t f = i / spf, s = i % spf;
     float2 v[8];
     const int g = tid / 256, n = tid % 256;
     for (int r = 0; r < 8; r++) v[r] = cur[g * RS + n + 256 * r];
     const uint32_t refw = *reinterpret_cast<const uint16_t *>(rstg + (tid & 3) * M + 2 * (tid >> 2));
     __syncthreads();
-    if (!DB && i + 1 < i1) fetch(i + 1, stg0);
+    if (!DB && i + ST < i1) fetch(i + ST, stg0);
     // filler: VALU and LDS exchanges (the transform's work stands in here)
     for (int k = 0; k < FILL; k++)
       for (int r = 0; r < 8; r++) v[r] = make_float2(v[r].x * 0.999f + v[(r + 1) & 7].y, v[r].y * 1.001f - v[r].x);
@@ -118,7 +125,7 @@ __global__ __launch_bounds__(T) void kern(const float2 *iq, uint64_t L, const ui
   if (acc == 12345.0f) sink[0] = acc;
   if (tid == 0) {   // shader cycles per symbol of this workgroup, summed over the grid
     const unsigned long long c1 = __builtin_amdgcn_s_memtime();
-    atomicAdd(reinterpret_cast<unsigned long long *>(sink) + 1, (c1 - c0) / (i1 - i0));
+    atomicAdd(reinterpret_cast<unsigned long long *>(sink) + 1, (c1 - c0) / (nsym_wg ? nsym_wg : 1));
   }
 }
 
@@ -194,30 +201,19 @@ int main() {
   };
   const double bytes_ld = (double)nsym * NA * M * 9, bytes_noidx = (double)nsym * NA * M * 17;
   rep("mode0 (kernel schedule)", run<0, 0, 0>(iq, L, ref, osym, oidx, nsym, spf, sink, ncu), bytes);
-  rep("mode0 plain stores", run<0, 0, 0, 1>(iq, L, ref, osym, oidx, nsym, spf, sink, ncu), bytes);
-  rep("mode0 plain DMA", run<0, 0, 0, 2>(iq, L, ref, osym, oidx, nsym, spf, sink, ncu), bytes);
-  rep("mode0 plain stores + DMA", run<0, 0, 0, 3>(iq, L, ref, osym, oidx, nsym, spf, sink, ncu), bytes);
-  rep("mode0 no index stores", run<0, 0, 0, 4>(iq, L, ref, osym, oidx, nsym, spf, sink, ncu), bytes_noidx);
-  rep("mode1 (double-buffered)", run<1, 0, 0>(iq, L, ref, osym, oidx, nsym, spf, sink, ncu), bytes);
+  rep("mode0 symbol-major", run<0, 0, 0, 8>(iq, L, ref, osym, oidx, nsym, spf, sink, ncu), bytes);
+  rep("mode0 symbol-major interleaved", run<0, 0, 0, 24>(iq, L, ref, osym, oidx, nsym, spf, sink, ncu), bytes);
+  rep("mode3 symbol-major", run<3, 0, 0, 8>(iq, L, ref, osym, oidx, nsym, spf, sink, ncu), bytes_ld);
+  rep("mode3 symbol-major interleaved", run<3, 0, 0, 24>(iq, L, ref, osym, oidx, nsym, spf, sink, ncu), bytes_ld);
   rep("mode2 (loads only)", run<2, 0, 0>(iq, L, ref, osym, oidx, nsym, spf, sink, ncu), bytes_ld);
-  rep("mode2 (loads only, plain)", run<2, 0, 0, 2>(iq, L, ref, osym, oidx, nsym, spf, sink, ncu), bytes_ld);
-  rep("mode3 (stores only)", run<3, 0, 0>(iq, L, ref, osym, oidx, nsym, spf, sink, ncu), bytes_ld);
-  rep("mode3 (stores only, plain)", run<3, 0, 0, 1>(iq, L, ref, osym, oidx, nsym, spf, sink, ncu), bytes_ld);
-  rep("mode0 fill 12 ldsx 3", run<0, 12, 3>(iq, L, ref, osym, oidx, nsym, spf, sink, ncu), bytes);
+  rep("mode2 (loads only) interleaved", run<2, 0, 0, 16>(iq, L, ref, osym, oidx, nsym, spf, sink, ncu), bytes_ld);
   {
     // the symbol buffer's bytes exactly (osym holds nsym NA M complex64)
     const size_t osym_bytes = sizeof(float2) * (size_t)nf * NA * spf * M;
     const uint64_t n16 = osym_bytes / 16;
-    if (n16 * 16 > osym_bytes) { printf("bad size\n"); return 1; }
     rep("pure 16 B nt stores, chunk per WG", wrun<0>(reinterpret_cast<v4f *>(osym), n16, ncu), (double)osym_bytes);
     rep("pure 16 B nt stores, grid-stride", wrun<1>(reinterpret_cast<v4f *>(osym), n16, ncu), (double)osym_bytes);
   }
-  rep("mode3 symbol-major, no index stores", run<3, 0, 0, 12>(iq, L, ref, osym, oidx, nsym, spf, sink, ncu), (double)nsym * NA * M * 8);
-  rep("mode0 symbol-major", run<0, 0, 0, 8>(iq, L, ref, osym, oidx, nsym, spf, sink, ncu), bytes);
-  rep("mode0 symbol-major plain stores", run<0, 0, 0, 9>(iq, L, ref, osym, oidx, nsym, spf, sink, ncu), bytes);
-  rep("mode3 symbol-major", run<3, 0, 0, 8>(iq, L, ref, osym, oidx, nsym, spf, sink, ncu), bytes_ld);
-  rep("mode3 symbol-major plain", run<3, 0, 0, 9>(iq, L, ref, osym, oidx, nsym, spf, sink, ncu), bytes_ld);
-  rep("mode0 (kernel schedule) again", run<0, 0, 0>(iq, L, ref, osym, oidx, nsym, spf, sink, ncu), bytes);
-  rep("mode3 (stores only) again", run<3, 0, 0>(iq, L, ref, osym, oidx, nsym, spf, sink, ncu), bytes_ld);
+  rep("mode0 symbol-major again", run<0, 0, 0, 8>(iq, L, ref, osym, oidx, nsym, spf, sink, ncu), bytes);
   return 0;
 }
