@@ -388,8 +388,14 @@ int run_sync(mimo_rx *h, const float2 *iq, uint64_t stride, uint32_t F, uint64_t
     a.band = band_env >= 0.0 ? band_env : sc_band(h->M);
     static const int diag_env = [] { const char *e = getenv("RMIMO_SC_DIAG"); return e ? atoi(e) : 0; }();
     a.diag = (uint32_t)diag_env;
-    static const bool split_env = [] { const char *e = getenv("RMIMO_SC_SPLIT"); return e && e[0] == '1'; }();
-    a.split_iters = split_env ? 1u : 0u;
+    // workgroups per (item, antenna) of the exact pass, each a contiguous share of the item's
+    // iterations: 1 (default), 2 or 4 (RMIMO_SC_SPLIT; 1 there selects 4, as before)
+    static const uint32_t split_env = [] {
+      const char *e = getenv("RMIMO_SC_SPLIT");
+      const int v = e ? atoi(e) : 0;
+      return v == 1 ? (uint32_t)(kScSpan / kScIterLen) : (v == 2 || v == 4) ? (uint32_t)v : 1u;
+    }();
+    a.split_iters = split_env;
     a.chunk_len = K; a.chunk_lo = chunk_lo; a.chunk_hi = nchunks;
     a.trig = h->trig.p; a.rec = h->rec.p; a.rec_stride = h->cap_chunks;
     a.cand = stream ? h->cand.p : nullptr;

@@ -68,7 +68,7 @@ struct ScArgs {
   unsigned long long *cand;
   int no_skip;
   uint32_t diag;            // diagnostics (RMIMO_SC_DIAG bits 8/16: skip in-place resolve/finalize)
-  uint32_t split_iters;     // sc_exact_kernel: one workgroup per (antenna, iteration) (else per antenna)
+  uint32_t split_iters;     // sc_exact_kernel: workgroups per (item, antenna), 1, 2 or 4 (0 = 1)
   uint32_t *snap;           // sc_exact_kernel: copy of *hot_count (the items of this phase), or null
 };
 

@@ -1623,9 +1623,12 @@ void sc_exact_kernel(ScArgs a) {
   // window sums (history of M samples), so an item's iterations run side by side instead of
   // one after the other: the item's critical path is one iteration, not four.
   // (a.split_iters = 0: one workgroup per antenna walks the item's iterations in turn)
-  const uint32_t IT = a.split_iters ? kScIters : 1u;
+  // (a.split_iters = IT > 1: IT workgroups per antenna, workgroup itw the kScIters / IT
+  // iterations from itw kScIters / IT)
+  const uint32_t IT = a.split_iters > 1 ? a.split_iters : 1u;
   const uint32_t s = blockIdx.x / IT;
   const int itw = (int)(blockIdx.x % IT);
+  const int KI = kScIters / (int)IT;
   // the first slot's record is read before the count is known (it is inside the allocation
   // whatever the count, and used only if the slot is live): in phase 1 (item0 = 0) its loads
   // go out with the count's instead of one memory latency after it
@@ -1654,10 +1657,13 @@ void sc_exact_kernel(ScArgs a) {
   const bool vec = x.pair_ok();
   if (tid == 0 && itw == 0) hp->lo[s] = w0 + (int64_t)it_lo * kScIt;   // first evaluated position
   bool active = true;
-  if (a.split_iters) {
-    active = itw >= it_lo && itw <= it_hi;            // uniform
-    if (!active) hp->wbits[((int)s * kScIters + itw) * kScT + tid] = 0;
-    it_lo = it_hi = itw;                              // this workgroup's iteration
+  if (IT > 1) {
+    const int k0 = itw * KI, k1 = k0 + KI - 1;        // this workgroup's iterations
+    for (int it = k0; it <= k1; it++)
+      if (it < it_lo || it > it_hi) hp->wbits[((int)s * kScIters + it) * kScT + tid] = 0;
+    it_lo = it_lo > k0 ? it_lo : k0;
+    it_hi = it_hi < k1 ? it_hi : k1;
+    active = it_lo <= it_hi;                          // uniform
   } else {
     for (int it = 0; it < kScIters; it++)
       if (it < it_lo || it > it_hi) hp->wbits[((int)s * kScIters + it) * kScT + tid] = 0;
@@ -2112,7 +2118,7 @@ void launch_sc_exact(const ScArgs &a, hipStream_t s) {
                               (int)shm);
     set_shm[v] = shm;
   }
-  hipLaunchKernelGGL(kern, dim3(a.N * (a.split_iters ? kScIters : 1),
+  hipLaunchKernelGGL(kern, dim3(a.N * (a.split_iters > 1 ? a.split_iters : 1),
                                  std::min<uint32_t>(a.hot_cap, 256)), dim3(kScT), shm, s, a);
 }
 
