@@ -728,8 +728,8 @@ def test_c4_residue_decode_in_child():
     read once per process; eight workgroups per symbol, each the 512-point transforms of one
     subcarrier residue class of all eight antennas and the 8x8 apply of those subcarriers): a
     child interpreter runs the oracle parity cases (PID 66 with indices: 22 groups of 3
-    symbols, EVM records of every class; PID 12: fewer symbols than its 32 groups) and the
-    batch = single-frame equality on it."""
+    symbols, EVM records of every class; PID 12: fewer symbols than its 32 groups), the
+    batch = single-frame equality and the symbol-major output layout on it."""
     import subprocess
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -740,6 +740,8 @@ def test_c4_residue_decode_in_child():
             "t._c_frame_parity(4096, 304, 8, 2, 12, 256, _lib.DET_MMSE, 35.0, seed=41,"
             " bias=False, path=_lib.DECODE_RESIDUE)\n"
             "t._c4_batch_equals_single_frames(_lib.DECODE_RESIDUE)\n"
+            "t.test_symbol_major_layout_equals_stream_major("
+            "(4096, 304, 8, 2, 66, 256, _lib.DET_MMSE, 63, 2, _lib.DECODE_RESIDUE))\n"
             "print('residue parity ok')\n"
             % (root, os.path.join(root, "tests")))
     env = dict(os.environ, RMIMO_DECODE_RES="1")
