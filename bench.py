@@ -27,6 +27,7 @@ Prints one JSON line (rank 0) with the roofline of the dominant kernel (decode) 
 oracle baseline measured on this host (1 core and the box's core share).
 """
 import argparse
+import ctypes
 import json
 import os
 import socket
@@ -142,21 +143,17 @@ def decode_kernel_name(M, N, args, path=None):
     lg = M.bit_length() - 1
     if path == 1:
         return "decode_stream_kernel<%d,%d>" % (lg, N)
-    if path == 4:   # one pass, 8x8 at M = 4096 by subcarrier residue class
-        return "decode_res8_kernel"
     if path == 2:   # (the persistent spectra form for M >= 2048 and the 128-subcarrier apply)
         return ("spectra_persist_kernel<%d>|apply_split2_kernel<8>" % lg if lg >= 11 else
                 "spectra_kernel<%d>|apply_split2_kernel<8>" % lg)
-    stream_ok = (os.environ.get("RMIMO_DECODE_STREAM", "1") != "0" and args.detector != "siso"
-                 and args.qam <= 256 and (N, lg) in ((4, 11), (4, 10), (2, 12), (2, 11), (2, 10)))
+    stream_ok = (args.detector != "siso" and args.qam <= 256 and (N, lg) in ((4, 11), (4, 10), (2, 12), (2, 11), (2, 10)))
     if stream_ok:
         return "decode_stream_kernel<%d,%d>" % (lg, N)
     if 512 <= M <= 4096 and N in (2, 4):
         return "decode_reg_kernel<%d,%d>" % (lg, N)
     if M < 512 and N in (2, 4):
         return "decode_persistent_kernel"
-    if (N == 8 and 512 <= M <= 4096 and args.detector != "siso" and args.pid >= M // 64
-            and os.environ.get("RMIMO_DECODE_SPLIT", "1") != "0"):
+    if N == 8 and 512 <= M <= 4096 and args.detector != "siso" and args.pid >= M // 64:
         return "spectra_kernel<%d>|apply_split_kernel<8>" % lg
     return "decode_kernel<%d,%d>" % (lg, N)
 
@@ -511,10 +508,32 @@ def main():
     # transmitted index read when the EVM reference comes from HBM)
     kname = decode_kernel_name(M, N, args, rx.decode_path())
     # (sc16 is read in place by the streaming decode; other decode kernels read the widened copy)
-    dec_in = in_bytes if kname.startswith(("decode_stream", "decode_res8")) else 8
+    dec_in = in_bytes if kname.startswith("decode_stream") else 8
     per_sym = N * M * dec_in + N * m_occ * 9 + (N * m_occ if args.ref_mode == 1 else 0)
     dec_bytes = n_dec * per_sym
     achieved = dec_bytes / dec_avg_s / 1e9 if dec_avg_s > 0 else 0.0
+    # ---- the decode's memory pattern alone, on this box, in this process (after the timed
+    # region): mimo_probe_decode_pattern stages and stores exactly the decode's bytes on its
+    # grid with no arithmetic, over the same buffers -- the rate this box's HBM gives that
+    # pattern, against which the decode's own time is stated
+    pattern = None
+    if (kname.startswith("decode_stream") and not c5 and not sc16 and not args.cfo
+            and args.ref_mode == 1 and sym_major and m_occ == M and ok > 0
+            and (N, M) in ((4, 2048), (4, 1024), (2, 4096), (2, 2048), (2, 1024))):
+        pms = ctypes.c_float(0.0)
+        prc = _lib.lib().mimo_probe_decode_pattern(
+            iq.data_ptr(), L, F, N, M, cp, ok, pid, ref_rows.data_ptr(), out_sym.data_ptr(),
+            out_idx.data_ptr(), 5, sh, ctypes.byref(pms))
+        torch.cuda.synchronize(dev)
+        if prc == 0 and pms.value > 0:
+            p_s = pms.value / 1e3
+            p_bytes = ok * pid * (N * (M + 2) * 8 + N * M * 9 + N * M)
+            pattern = {"ms": pms.value, "bytes": p_bytes, "gbs": p_bytes / p_s / 1e9,
+                       "decode_ms": dec_avg_s * 1e3,
+                       "decode_vs_pattern": (dec_avg_s / p_s) if p_s > 0 else None,
+                       "note": "mimo_probe_decode_pattern: the decode's staging DMA and output "
+                               "stores (the same grid, bytes and buffers), no transform, apply "
+                               "or demap; mean of 5 launches after the timed region"}
     traffic = None
     if os.path.exists(args.pmc_json):
         try:
@@ -615,6 +634,9 @@ def main():
                      "kernel": kname, "bytes_per_launch": dec_bytes,
                      "symbols_per_launch": n_dec, "bytes_per_symbol": per_sym,
                      "avg_launch_ms": dec_avg_s * 1e3},
+        "decode_pattern_ms": pattern["ms"] if pattern else None,
+        "decode_vs_pattern": pattern["decode_vs_pattern"] if pattern else None,
+        "decode_pattern": pattern,
         "cpu_baseline": cpu,
         "evm_db_delta_vs_cpu": evm_delta,
         "scan_rate_all_captures": scanned_total / elapsed,

@@ -212,13 +212,23 @@ int mimo_rx_get_stage_times(mimo_rx *h, double *ms, uint32_t *launches);
  * oracle's exact fp32 order, since the last call (diagnostic; synchronises) */
 int mimo_rx_get_sc_exact_count(mimo_rx *h, uint64_t *out);
 /* the replay-decode kernel family the last batch or execute launched (diagnostic, no sync):
- * STREAM = decode_stream_kernel (persistent, 2x2/4x4), RESIDUE = decode_res8_kernel (one pass,
- * 8x8 at M = 4096, eight workgroups per symbol by subcarrier residue class), SPLIT =
- * spectra_kernel + apply_split_kernel (8x8 at M >= 512 otherwise), SYMBOL = the per-symbol
- * kernels, NONE = no decode yet */
+ * STREAM = decode_stream_kernel (persistent, 2x2/4x4), SPLIT = spectra_kernel +
+ * apply_split_kernel (8x8 at M >= 512), SYMBOL = the per-symbol kernels, NONE = no decode yet */
 enum { MIMO_DECODE_NONE = 0, MIMO_DECODE_STREAM = 1, MIMO_DECODE_SPLIT = 2,
-       MIMO_DECODE_SYMBOL = 3, MIMO_DECODE_RESIDUE = 4 };
+       MIMO_DECODE_SYMBOL = 3 };
 int mimo_rx_get_decode_path(const mimo_rx *h, int32_t *path);
+/* roofline probe (diagnostic, no reference counterpart): the streaming decode's memory pattern
+ * without its arithmetic -- per symbol N rows of M + 2 complex64 samples staged by LDS-DMA and
+ * N x M uint8 reference indices, N x M complex64 + N x M uint8 written symbol-major, on the
+ * decode's persistent grid -- over n_frames x spf symbols of the caller's captures ([n_caps][N]
+ * [stride] complex64), reference rows and output buffers ([n_frames][spf][N][M]); reps timed
+ * launches after one warm-up, the mean in *ms_per_launch. N x M in {4 x 2048, 4 x 1024,
+ * 2 x 4096, 2 x 2048, 2 x 1024} (the streaming decode's geometries, every subcarrier occupied).
+ * Returns 0, or 1 (arguments), 2 (HIP), 3 (geometry). */
+int mimo_probe_decode_pattern(const void *d_iq, uint64_t stride, uint32_t n_caps, uint32_t N,
+                              uint32_t M, uint32_t cp, uint32_t n_frames, uint32_t spf,
+                              const void *d_ref, void *d_out_sym, void *d_out_idx, int reps,
+                              void *hip_stream, float *ms_per_launch);
 /* the CFO stages the last batch ran (diagnostic, no sync): 0 off, 1 estimate and derotation,
  * 2 the same plus the per-symbol common phase (the streaming decode's CPE variant) -- the
  * oracle's cfo_mode for the same batch */

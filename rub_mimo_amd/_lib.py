@@ -21,7 +21,7 @@ STAGE_NAMES = ("sc", "plateau", "search", "ls", "weights", "decode", "evm")
 STATE_SEEK_PLATEAU, STATE_SAVE_ACCESS_CODES, STATE_WAIT, STATE_MIMO = 0, 1, 2, 3
 DET_ZF2, DET_ZF, DET_MMSE, DET_SISO = 0, 1, 2, 3
 FRAME_OK, FRAME_NO_SYNC, FRAME_INCOMPLETE, FRAME_RESCAN, FRAME_NONE = 0, 1, 2, 3, 4
-DECODE_NONE, DECODE_STREAM, DECODE_SPLIT, DECODE_SYMBOL, DECODE_RESIDUE = 0, 1, 2, 3, 4
+DECODE_NONE, DECODE_STREAM, DECODE_SPLIT, DECODE_SYMBOL = 0, 1, 2, 3
 # mimo_batch.out_layout: [F][N][max_out][M_occ] or [F][max_out][N][M_occ]
 LAYOUT_STREAM_MAJOR, LAYOUT_SYMBOL_MAJOR = 0, 1
 
@@ -95,6 +95,8 @@ SIGNATURES = {
     "mimo_rx_get_stage_times": (C.c_int, [_vp, _P(C.c_double), _P(_u32)]),
     "mimo_rx_get_sc_exact_count": (C.c_int, [_vp, _P(_u64)]),
     "mimo_rx_get_decode_path": (C.c_int, [_vp, _P(_i32)]),
+    "mimo_probe_decode_pattern": (C.c_int, [_vp, _u64, _u32, _u32, _u32, _u32, _u32, _u32, _vp,
+                                            _vp, _vp, C.c_int, _vp, _P(C.c_float)]),
     "mimo_rx_get_cfo_mode": (C.c_int, [_vp, _P(_i32)]),
     "mimo_rx_get_stream_capacity": (C.c_int, [_vp, _P(_u64), _P(_u64)]),
     "mimo_rx_set_debug_log": (C.c_int, [_vp, C.c_char_p]),

@@ -779,25 +779,6 @@ static uint32_t decode_launch_na(const DecodeArgs &a, uint32_t nf, hipStream_t s
     const size_t shm = sizeof(float2) * lds_padded_len(M) * 2;
     auto kern = (a.detector == 3) ? decode_reg_kernel<LOG2M, NA, true>
                                   : decode_reg_kernel<LOG2M, NA, false>;
-    if constexpr (LOG2M == 11 && NA == 4) {   // diagnostics: RMIMO_DEC_EXPT variants
-      switch (a.expt) {
-        case 1: kern = decode_reg_kernel<LOG2M, NA, false, 1>; break;
-        case 2: kern = decode_reg_kernel<LOG2M, NA, false, 2>; break;
-        case 3: kern = decode_reg_kernel<LOG2M, NA, false, 3>; break;
-        case 4: kern = decode_reg_kernel<LOG2M, NA, false, 4>; break;
-        case 7: kern = decode_reg_kernel<LOG2M, NA, false, 7>; break;
-        case 8: kern = decode_reg_kernel<LOG2M, NA, false, 8>; break;
-        case 16: kern = decode_reg_kernel<LOG2M, NA, false, 16>; break;
-        case 32: kern = decode_reg_kernel<LOG2M, NA, false, 32>; break;
-        case 11: kern = decode_reg_kernel<LOG2M, NA, false, 11>; break;
-        case 27: kern = decode_reg_kernel<LOG2M, NA, false, 27>; break;
-        case 64: kern = decode_reg_kernel<LOG2M, NA, false, 64>; break;
-        case 67: kern = decode_reg_kernel<LOG2M, NA, false, 67>; break;
-        case 115: kern = decode_reg_kernel<LOG2M, NA, false, 115>; break;
-        case 59: kern = decode_reg_kernel<LOG2M, NA, false, 59>; break;
-        default: break;
-      }
-    }
     (void)hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)shm);
     hipLaunchKernelGGL(kern, dim3(a.max_out, nf), dim3(M / 4), shm, s, a);
@@ -856,13 +837,12 @@ uint32_t launch_decode(const DecodeArgs &a, int log2M, uint32_t n_frames, hipStr
                        bool *per_frame_records, int *path) {
   *per_frame_records = false;
   *path = 0;
-  if (a.expt == 0) {
+  {
     uint32_t parts = launch_decode_stream(a, log2M, n_frames, s);
     if (parts) *path = 1;
     // the folded CFO (cpe == 2: no derotated scratch capture) is applied by the streaming
     // decode only; any other kernel would decode the raw samples
     if (!parts && a.cpe == 2) return 0;
-    if (!parts && (parts = launch_decode_res8(a, log2M, n_frames, s))) *path = 4;
     if (!parts && (parts = launch_decode_split(a, log2M, n_frames, s))) *path = 2;
     if (parts) {
       *per_frame_records = true;

@@ -1178,9 +1178,10 @@ __global__ __launch_bounds__(NA * (1 << LOG2M) / 8) void decode_stream_kernel(De
           const v2f acc = out1(t, q, X);
           const uint32_t d = finish(t, q, k, acc);
 #ifndef DS_ABL_NOSTORE   // timing ablation: no symbol / index stores
-          if constexpr (OUTS & 1)
+          // (OUTX: the stores the DS_ABL_NOIDX / NOSYM ablations keep, as NSTORE counts them)
+          if constexpr (OUTX & 1)
             out_store<NTS>(acc, (gptr<v2f>)((gptr<char>)osym + k * (uint32_t)sizeof(v2f)));
-          if constexpr (OUTS & 2) out_store<NTI>((uint8_t)d, &oidx[k]);
+          if constexpr (OUTX & 2) out_store<NTI>((uint8_t)d, &oidx[k]);
 #endif
         }
       }
@@ -1335,7 +1336,7 @@ __global__ __launch_bounds__((1 << LOG2M) / 16) void spectra_persist_kernel(Deco
     if (nit < total) load(nx, ncap, nr, nabs0);
     reg_compute<LOG2M, 16, 0, false>(v, w1);
     reg_rest<LOG2M, 16, 1, false>(buf, v, w1, tid);
-    // X[k], k = tid + T e, into [frame][chunk][slot][antenna][64]
+    // X[k], k = tid + T e, into the whole row [F][sym_cap][N][M] (spec_off)
     float2 *o = a.spec + spec_off(a, f, sl, r, 0);
 #pragma unroll
     for (int e = 0; e < 16; e++) {
@@ -1616,558 +1617,6 @@ __global__ __launch_bounds__(64 * NA) void apply_split2_kernel(DecodeArgs a) {
   }
 }
 
-// ------------------------------------------------------------------------------------
-// One-pass 8x8 decode at M = 4096 by residue class (C4; replaces the split decode's spectra
-// round trip through HBM). With the radix-8 decimation in frequency over stride 512,
-//   X_g[8 k + q] = DFT_512( c_q )[k],   c_q[n] = W_4096^{n q} sum_{r<8} x_g[n + 512 r] W_8^{r q},
-// the subcarriers k = q (mod 8) of a symbol need only the 512-point transforms of c_q. So eight
-// workgroups share a symbol, workgroup q computing residue class q for all eight antennas
-// (the one-output DFT over r by Horner's rule, then eight wave-local 512-point transforms) and
-// applying the weights of its 512 subcarriers, which it keeps in registers for all symbols of a
-// frame (64 VGPRs: 512 x 8 x 8 complex = 256 KB per class, one 1024-thread workgroup). Every
-// workgroup reads the whole symbol (256 KB), from L2: the eight of a symbol are blocks
-// b, b + 8, ..., b + 56, dealt to one XCD by the round-robin placement (speed only), so HBM
-// reads each symbol once; their outputs (every eighth subcarrier) merge in that XCD's L2 into
-// whole lines. No scratch, no hand-over between workgroups, no atomics.
-// Per symbol (stage A): the eight antenna rows stream through a three-slot LDS ring by LDS-DMA
-// (every wave issues two or three 1 KB pieces of a row; two rows in flight behind the one being
-// summed, the next symbol's first two rows during stages B and C, counted vmcnt waits: no
-// register holds a sample in flight, and the compiler's own waits never see the DMA); each
-// row's c_q[n] is summed by lane pairs (r < 4 and r >= 4, combined by a DPP swap) into the
-// image. Stage B: waves 0-7 transform antennas 0-7 in their own regions (exchanges in
-// conflict-free layouts, as the streaming decode). Stage C: all 16 waves apply W (thread: one
-// subcarrier, four of the eight output streams; the four streams' W in registers, 64 VGPRs),
-// demap, EVM and store; the transmitted indices arrive by LDS-DMA of one byte per lane at the
-// top of the symbol. The eight workgroups of a symbol read it from L2 at ~100 GB/s per CU
-// (tools/micro/l2dma: 25 TB/s chip-wide, one HBM read per symbol).
-constexpr int kR8T = 1024;
-constexpr int kR8MS = 512;                    // points of a residue transform
-constexpr int kR8RS = 576;                    // region stride (entries): the x2 layout's 570
-constexpr int kR8Groups = 8;                  // residue classes = workgroups per symbol
-
-// LDS staging of one antenna row of an 8 x 4096 symbol (fc32: 8 B per sample; sc16 on the wire:
-// 4 B): SPAN samples from the 16-byte-aligned sample at or before the body start, in 1 KB DMA
-// pieces; pieces of the row's upper half sit SHIFT samples (128 B, 32 banks) further, so that the
-// stage-A lanes reading x[n + 512 r] of the two halves hit disjoint banks
-template <bool SC16>
-struct R8Stage {
-  static constexpr int SB = SC16 ? 4 : 8;               // bytes per staged sample
-  static constexpr int SPC = 16 / SB;                   // samples per 16-byte chunk
-  static constexpr int PS = 1024 / SB;                  // samples per DMA piece
-  static constexpr int SPAN = 4096 + SPC;               // staged samples per row
-  static constexpr int NPIECE = (SPAN + PS - 1) / PS;   // 33 (fc32) / 17 (sc16)
-  static constexpr int LASTC = (SPAN - (NPIECE - 1) * PS) / SPC;   // chunks of the last piece
-  static constexpr int HALF = 2048 / PS;                // first piece of the upper half
-  static constexpr int SHIFT = 128 / SB;
-  static constexpr int SLOTB = ((SPAN + SHIFT) * SB + 15) / 16 * 16;
-  static_assert(NPIECE <= 48 && LASTC >= 1 && LASTC <= 64, "three pieces per wave at most");
-  MIMO_DEV static uint32_t piece_off(uint32_t b) { return b * 1024u + (b >= (uint32_t)HALF ? SHIFT * SB : 0u); }
-  MIMO_DEV static int pos(int p) { return p + (p >= 2048 ? SHIFT : 0); }
-  MIMO_DEV static v2f read(const char *sl, uint32_t p, float scale) {
-    const int i = pos((int)p);
-    if constexpr (SC16) {
-      const Iq<true> cv{nullptr, scale};
-      const float2 w = cv.cvt(reinterpret_cast<const short2 *>(sl)[i]);
-      return v2f{w.x, w.y};
-    } else {
-      return reinterpret_cast<const v2f *>(sl)[i];
-    }
-  }
-};
-
-// the wave-local 512-point forward transform of region rg (RegPlan<9, 8>: radix 8, 8, 8) with
-// the streaming decode's exchange layouts (x1 after pass 0, x2 after pass 1; lds_pad left both
-// radix-8 stores 2-way bank-conflicted); input and output in natural order, element lane + 64 e
-MIMO_DEV void wave512_fwd(v2f *rg, const v2f *w1, int lane) {
-  using PL = RegPlan<9, 8>;
-  static_assert(PL::NP == 3 && PL::RM == 8 && PL::T == 64, "plan 8, 8, 8 on one wave");
-  v2f v[8];
-  int t = lane;
-  asm volatile("" : "+v"(t));
-#pragma unroll
-  for (int r = 0; r < 8; r++) v[r] = rg[t + 64 * r];
-  reg_compute<9, 8, 0, false>(v, w1);
-  {   // x1: element 8 t + r at 33 (t >> 2) + 8 (t & 3) + (r ^ m), m = 4 ((t >> 1) & 1)
-    const int m = ((t >> 1) & 1) << 2;
-    const int B = 33 * (t >> 2) + 8 * (t & 3);
-    v2f *lo = rg + B + m, *hi = rg + B - m;
-#pragma unroll
-    for (int r = 0; r < 4; r++) lo[r] = v[r];
-#pragma unroll
-    for (int r = 4; r < 8; r++) hi[r] = v[r];
-  }
-  wave_lds_sync();
-  {   // pass 1 loads elements t + 64 r
-    const v2f *p = rg + 33 * (t >> 5) + ((t & 31) ^ (((t >> 4) & 1) << 2));
-#pragma unroll
-    for (int r = 0; r < 8; r++) v[r] = p[66 * r];
-  }
-  reg_compute<9, 8, 1, false>(v, w1);
-  {   // x2: element 64 (t/8) + t%8 + 8 r
-    v2f *q = rg + 64 * (t >> 3) + (t & 7) + 8 * (t >> 3);
-#pragma unroll
-    for (int r = 0; r < 8; r++) q[8 * r + 2 * (r >> 2)] = v[r];
-  }
-  wave_lds_sync();
-  {   // pass 2 loads elements t + 64 r
-    const v2f *p = rg + x2pad(t);
-#pragma unroll
-    for (int r = 0; r < 8; r++) v[r] = p[72 * r];
-  }
-  reg_compute<9, 8, 2, false>(v, w1);
-  wave_lds_sync();
-#pragma unroll
-  for (int r = 0; r < 8; r++) rg[t + 64 * r] = v[r];
-}
-
-// vmcnt wait with a compile-time count (the staged residue decode's counted waits)
-template <int N>
-MIMO_DEV void vm_wait_imm() {
-  asm volatile("s_waitcnt vmcnt(%0)" :: "n"(N) : "memory");
-}
-// LDS-DMA of one dword per lane (global_load_lds_dword: lane l's 4 bytes, from its own
-// address, to lds + 4 l), inline asm for the same reason as dma16: invisible to the compiler's
-// waits, which would drain the staging DMA in flight at the next barrier. (A register-destination
-// asm load is no alternative: the compiler may move the register while the load is in flight.)
-MIMO_DEV void dma_u32(uint32_t voff, __attribute__((address_space(1))) const void *sbase, uint32_t lds) {
-  uint32_t keep;
-  asm volatile("s_nop 4\n\ts_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t"
-               "global_load_lds_dword %1, %2\n\ts_mov_b32 m0, %0"
-               : "=&s"(keep) : "v"(voff), "s"(sbase), "s"(lds) : "memory");
-}
-
-template <int REF, int OUTS, bool SC16>
-__global__ __launch_bounds__(kR8T) void decode_res8_kernel(DecodeArgs a) {
-  constexpr int NA = 8, M = 4096, MS = kR8MS, RS = kR8RS, T = kR8T;
-  using SP = R8Stage<SC16>;
-  extern __shared__ __attribute__((aligned(16))) float2 lds_raw[];
-  v2f *img = reinterpret_cast<v2f *>(lds_raw);         // [NA][RS]: c_q, then X_g[8 k + q]
-  char *ring = reinterpret_cast<char *>(img + NA * RS);  // [3][SP::SLOTB]: staged antenna rows
-  v2f *wnl = reinterpret_cast<v2f *>(ring + 3 * SP::SLOTB);   // [MS]: W_4096^{n q}
-  v2f *w1l = wnl + MS;                                  // [64][2]: the 512-point plan's twiddles
-  uint32_t *rl = reinterpret_cast<uint32_t *>(w1l + 128);   // [16 waves][4][64]: reference dwords
-  __shared__ uint32_t pfx[kStreamMaxFrames + 1];
-  __shared__ int64_t fbody[kStreamMaxFrames];
-  __shared__ uint32_t fcr[kStreamMaxFrames];           // capture | reference row << 16
-  __shared__ uint32_t fgq[kStreamMaxFrames];           // first group | (last group - first) << 16
-  __shared__ v2f ptab[kStreamMaxQam];
-  __shared__ uint8_t gidx[kStreamMaxQam];
-  const int tid = threadIdx.x;
-  const uint32_t wv = __builtin_amdgcn_readfirstlane((uint32_t)tid >> 6);
-  // the lane (and thread) index recomputed where used, from mbcnt in a volatile asm: per-lane
-  // roles then never stay live across the symbol loop, where the register allocator (64 VGPRs
-  // of weights) would spill them and reload them behind a wait that drains the staging DMA
-  auto lane_now = []() __attribute__((always_inline)) -> uint32_t {
-    uint32_t l;
-    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
-    return l;
-  };
-  auto tid_now = [&]() __attribute__((always_inline)) -> uint32_t { return wv * 64u + lane_now(); };
-  // residue class and group: blocks b, b + 8, .., b + 56 (one XCD) are the classes of a group
-  const uint32_t q = (blockIdx.x >> 3) & 7u;
-  const uint32_t G = gridDim.x / kR8Groups;
-  const uint32_t grp = (blockIdx.x & 7u) + 8u * (blockIdx.x >> 6);
-  for (uint32_t e = tid; e < a.qam.L * a.qam.L; e += T) {
-    const float2 p = qam_point(e, a.qam);
-    ptab[e] = v2f{p.x, p.y};
-    const uint32_t mI = e / a.qam.L, mQ = e % a.qam.L;
-    gidx[e] = (uint8_t)((gray_enc(mI) << a.qam.b) | gray_enc(mQ));
-  }
-  for (uint32_t f0 = 0; f0 <= a.n_frames; f0 += T) {
-    const uint32_t f = f0 + tid;
-    if (f < a.n_frames) {
-      const FrameInfo &I = a.info[f];
-      pfx[f] = (I.status == 0) ? min(I.n_sym, a.max_out) : 0u;
-      fbody[f] = I.base + (int64_t)I.i0 + (int64_t)a.cp;
-      fcr[f] = I.cap | (I.ref << 16);
-    } else if (f == a.n_frames) {
-      pfx[f] = 0;
-    }
-  }
-  __syncthreads();
-  if (tid == 0) {
-    uint32_t acc = 0;
-    for (uint32_t f = 0; f <= a.n_frames; f++) {
-      const uint32_t v = pfx[f];
-      pfx[f] = acc;
-      acc += v;
-    }
-  }
-  // W_8^{q} (uniform), W_4096^{n q} and the 512-point plan's base twiddles tabled in LDS
-  const v2f w8 = uni(twiddle<false>(a.tw, (int)(q * (kTwN / 8))));
-  static_assert(RegPlan<9, 8>::NTW == 2, "two base twiddles per lane");
-  if (tid < MS) wnl[tid] = twiddle<false>(a.tw, (int)((((uint32_t)tid * q) & (M - 1)) * (kTwN / M)));
-  if (tid < 64) reg_twiddles<9, 8>(w1l + 2 * tid, a.tw, tid);
-  __syncthreads();
-  const uint32_t total = pfx[a.n_frames];
-  const uint32_t chunk = (total + G - 1) / G;
-  const uint32_t i_begin = grp * chunk;
-  const uint32_t i_end = min(i_begin + chunk, total);
-  if (i_begin >= i_end) return;                       // uniform (the whole group alike)
-  // each frame's first covering group and its group count (the EVM records' indices: the
-  // divisions here, not in the loop)
-  for (uint32_t ff = tid; ff < a.n_frames; ff += T) {
-    const uint32_t g0 = pfx[ff] / chunk;
-    const uint32_t g1 = pfx[ff + 1] > pfx[ff] ? (pfx[ff + 1] - 1) / chunk : g0;
-    fgq[ff] = g0 | ((g1 - g0) << 16);
-  }
-  __syncthreads();
-  uint32_t f = 0;
-  {
-    uint32_t lo = 0, hi = a.n_frames;
-    while (hi - lo > 1) {
-      const uint32_t mid = (lo + hi) >> 1;
-      if (pfx[mid] <= i_begin) lo = mid; else hi = mid;
-    }
-    f = __builtin_amdgcn_readfirstlane(lo);
-  }
-  uint32_t s = __builtin_amdgcn_readfirstlane(i_begin - pfx[f]);
-
-  // ---- staging: antenna row g of symbol (ff, ss), SP::NPIECE LDS-DMA pieces of 1 KB from the
-  // SP::SPC-aligned sample at or before the body start e (offset odd = e mod SPC); piece b
-  // (SP::PS samples) lands at b PS samples into the ring slot, the upper half of the row
-  // (b >= SP::NPIECE / 2) SP::SHIFT samples further: the stage-A reads of the two halves then
-  // fall on different LDS banks. Wave w issues pieces w, w + 16, w + 32 (PW of them: the same
-  // count for every row, also at the capture's edges, where the pieces come from a clamped
-  // source and the row is then rewritten with guarded loads, so the counted waits hold)
-  constexpr uint32_t PW0 = (uint32_t)(SP::NPIECE + 15) / 16;       // pieces per row: wave 0
-  constexpr uint32_t PW1 = (uint32_t)(SP::NPIECE + 14) / 16;       // ... every other wave
-  static_assert(SP::NPIECE > 32 ? (PW0 == 3 && PW1 == 2) : (PW0 == 2 && PW1 == 1), "pieces per wave");
-  const uint32_t ring_base = (uint32_t)(uintptr_t)ring;
-  // a symbol's staging source, computed once per symbol (scalar work: the CU's one scalar
-  // unit serves all 16 waves, and per-row 64-bit address arithmetic in every wave cost ~2k
-  // cycles per row): row 0's body start in the batch, the body start within the capture, and
-  // whether every row's staged span lies inside the capture (the worst-case alignment offset)
-  struct SymSrc {
-    int64_t e0;       // row 0's body start in the batch (sample index); row g at + g stride
-    int64_t rel;      // the body start within its capture row
-  };
-  // every row's staged span inside the capture (the worst-case alignment offset)
-  auto inside = [&](const SymSrc &y) __attribute__((always_inline)) -> bool {
-    return y.rel >= SP::SPC - 1 && y.rel + SP::SPAN <= (int64_t)a.frame_len;
-  };
-  auto sym_src = [&](uint32_t ff, uint32_t ss) __attribute__((always_inline)) -> SymSrc {
-    const int64_t body = fbody[ff] + (int64_t)((uint64_t)ss * a.SL);
-    const uint32_t cr = __builtin_amdgcn_readfirstlane(fcr[ff]);
-    SymSrc y;
-    y.rel = (int64_t)rfl64((uint64_t)body);
-    y.e0 = (int64_t)rfl64((uint64_t)((int64_t)((uint64_t)(cr & 0xFFFFu) * NA * a.stride) + body));
-    return y;
-  };
-  auto issue_row = [&](const SymSrc &y, uint32_t g, uint32_t slot) __attribute__((always_inline)) {
-    const int64_t e = y.e0 + (int64_t)g * (int64_t)a.stride;
-    int64_t a0 = e & ~(int64_t)(SP::SPC - 1);         // aligned batch sample index
-    if (!inside(y)) {                                  // uniform: a clamped source (rewritten later)
-      const int64_t rs = e - y.rel;                    // the row's first sample
-      const int64_t lo = (rs + SP::SPC - 1) & ~(int64_t)(SP::SPC - 1);
-      const int64_t hi = (rs + (int64_t)a.frame_len - SP::SPAN) & ~(int64_t)(SP::SPC - 1);
-      a0 = a0 < lo ? lo : (a0 > hi ? hi : a0);
-    }
-    const auto src = sgpr_ptr(reinterpret_cast<const char *>(a.iq) + a0 * SP::SB);
-    const uint32_t dst = ring_base + slot * (uint32_t)SP::SLOTB;
-    const uint32_t l16 = lane_now() * 16u;
-#pragma unroll
-    for (int j = 0; j < 3; j++) {
-      const uint32_t b = wv + 16u * (uint32_t)j;      // uniform
-      if (b < (uint32_t)SP::NPIECE && (b + 1 < (uint32_t)SP::NPIECE || l16 < 16u * SP::LASTC))
-        dma16(b * 1024u + l16, src, __builtin_amdgcn_readfirstlane(dst + SP::piece_off(b)));
-    }
-  };
-  // a row whose span leaves the capture: every staged position rewritten from guarded loads
-  // (zeros outside), after its DMA has landed (capture edges only; the loads' own waits drain
-  // the staging in flight, which costs time there only)
-  auto fix_row = [&](const SymSrc &y, uint32_t g, uint32_t slot) __attribute__((always_inline)) {
-    if (inside(y)) return;                             // uniform
-    const int64_t e = y.e0 + (int64_t)g * (int64_t)a.stride;
-    const int64_t odd = e & (SP::SPC - 1), rs = e - y.rel;
-    const auto xs = iq_row<SC16>(a.iq, a.iq_scale, (uint64_t)rs);
-    char *sl = ring + slot * SP::SLOTB;
-    for (int p = tid; p < SP::SPAN; p += T) {
-      const int64_t n = y.rel - odd + p;
-      const bool in = n >= 0 && n < (int64_t)a.frame_len;
-      if constexpr (SC16) {
-        const short2 v = in ? reinterpret_cast<const short2 *>(a.iq)[rs + n] : make_short2(0, 0);
-        reinterpret_cast<short2 *>(sl)[SP::pos(p)] = v;
-      } else {
-        const float2 v = in ? xs.at(n) : make_float2(0.0f, 0.0f);
-        reinterpret_cast<float2 *>(sl)[SP::pos(p)] = v;
-      }
-    }
-    __syncthreads();
-  };
-  // the next item (uniform)
-  auto next_of = [&](uint32_t &ff, uint32_t &ss) __attribute__((always_inline)) {
-    ss++;
-    if (ss >= pfx[ff + 1] - pfx[ff]) {
-      do { ff++; } while (pfx[ff + 1] == pfx[ff]);
-      ss = 0;
-    }
-    ff = __builtin_amdgcn_readfirstlane(ff);
-    ss = __builtin_amdgcn_readfirstlane(ss);
-  };
-
-  // stage C thread roles: subcarrier k = 8 (tid >> 1) + q, output streams 4 h .. 4 h + 3
-  v2f Wr[4][NA];                                       // W * gain * dn of the four streams
-  auto load_w = [&](uint32_t ff) __attribute__((always_inline)) {
-    const uint32_t tt = tid_now(), h = tt & 1u, k = 8 * (tt >> 1) + q;
-    const float gk = a.gain[(uint64_t)ff * M + k] * a.dn;
-#pragma unroll
-    for (int j = 0; j < 4; j++)
-#pragma unroll
-      for (int r = 0; r < NA; r++) {
-        const float2 w = a.W[(((uint64_t)ff * NA + 4 * h + j) * NA + r) * M + k];
-        Wr[j][r] = v2f{w.x * gk, w.y * gk};
-      }
-  };
-  const v2f inv_sc = v2f{a.qam.inv_scale, a.qam.inv_scale};
-  const v2f Lf = v2f{(float)a.qam.L, (float)a.qam.L};
-  const uint32_t Lm1 = a.qam.L - 1;
-  float e_num[4], e_den[4];
-  uint32_t n_err[2][4];                                // per lane parity (stream half), SGPRs
-#pragma unroll
-  for (int j = 0; j < 4; j++) {
-    e_num[j] = e_den[j] = 0.0f;
-    n_err[0][j] = n_err[1][j] = 0u;
-  }
-  // per-wave EVM partials of this (group, frame) segment (frame boundaries only): the sums
-  // over the wave's 32 lanes of each parity by a fixed xor butterfly over lane bits 1..5
-  // (bitwise reproducible); the errors are wave counts already
-  auto flush = [&](uint32_t ff) __attribute__((always_inline)) {
-    const uint32_t lane = lane_now();
-    const uint32_t gq = fgq[ff];
-    const uint32_t jrec = (grp - (gq & 0xFFFFu)) * kR8Groups + q;
-    if (tid == 0 && pfx[ff] >= i_begin && q == 0)   // the frame's first group, class 0
-      a.nrec[ff] = ((gq >> 16) + 1) * kR8Groups;
-#pragma unroll
-    for (int j = 0; j < 4; j++) {
-#pragma unroll
-      for (int off = 2; off < 64; off <<= 1) {
-        e_num[j] += __shfl_xor(e_num[j], off);
-        e_den[j] += __shfl_xor(e_den[j], off);
-      }
-    }
-    // lanes 0 and 1 (parities 0, 1): streams 4 h .. 4 h + 3, three components each
-    if (lane < 2) {
-      double *ep = a.evm_part + (((uint64_t)ff * a.rec_stride + jrec) * (T / 64) + wv) * NA * 3 + 12 * lane;
-#pragma unroll
-      for (int j = 0; j < 4; j++) {
-        ep[3 * j + 0] = (double)e_num[j];
-        ep[3 * j + 1] = (double)e_den[j];
-        ep[3 * j + 2] = (double)(lane ? n_err[1][j] : n_err[0][j]);
-      }
-    }
-#pragma unroll
-    for (int j = 0; j < 4; j++) {
-      e_num[j] = e_den[j] = 0.0f;
-      n_err[0][j] = n_err[1][j] = 0u;
-    }
-  };
-
-  // stage A thread roles: position n = tid >> 1 of the row, half hA = tid & 1 of the sum over r
-  // (r = 4 hA .. 4 hA + 3; lanes 2 n and 2 n + 1 combine through a DPP swap)
-  const v2f sgn_q = (q & 1u) ? v2f{-1.0f, -1.0f} : v2f{1.0f, 1.0f};   // W_8^{4 q}
-  constexpr int NST = ((OUTS & 1) ? 4 : 0) + ((OUTS & 2) ? 4 : 0);    // stores per symbol
-  constexpr int NREFL = REF == 1 ? 4 : 0;                               // reference loads
-  // prologue: the first symbol's rows 0 and 1
-  SymSrc ycur = sym_src(f, s);
-  issue_row(ycur, 0, 0);
-  issue_row(ycur, 1, 1);
-  uint32_t krow = 0;                                   // rows issued for this workgroup so far, mod 3
-  bool first = true, new_frame = true;
-  // diagnostics build (-DDS_PROF, RMIMO_DEC_PROF=1): wave 0's shader cycles per symbol in the row
-  // waits, stage A, stage B and stage C into prof [symbols, waits, A, B, C, -, -, -]
-  DSP(unsigned long long r8t[5] = {0, 0, 0, 0, 0};)
-  for (uint32_t i = i_begin; i < i_end; i++) {
-    DSP(const unsigned long long r8_0 = __builtin_amdgcn_s_memtime();)
-    const bool more = i + 1 < i_end;
-    uint32_t fn = f, sn = s;
-    SymSrc ynext = ycur;
-    if (more) {
-      next_of(fn, sn);
-      ynext = sym_src(fn, sn);
-    }
-    if (new_frame) load_w(f);                          // (one call site: one register assignment)
-    // ---- stage A: the eight antenna rows, two in flight behind the one being summed (rows
-    // unrolled: each row's counted wait is a compile-time count per wave class and flag)
-    const bool w0 = wv == 0;                            // (wave 0 issues a row's last piece)
-    auto row_step = [&](auto gc) __attribute__((always_inline)) {
-      constexpr uint32_t g = decltype(gc)::value;
-      // ops this wave issued after row g's pieces, left in flight by the counted wait
-#define R8W(EXPR)                                   \
-  do {                                              \
-    if (w0) { constexpr uint32_t PWc = PW0; vm_wait_imm<(EXPR)>(); } \
-    else { constexpr uint32_t PWc = PW1; vm_wait_imm<(EXPR)>(); }    \
-  } while (0)
-      DSP(const unsigned long long r8_w = __builtin_amdgcn_s_memtime();)
-      if constexpr (g == 0) {
-        if (first) R8W(PWc); else R8W(PWc + NST);
-      } else if constexpr (g == 1) {
-        if (first) R8W(PWc + NREFL); else R8W(NST + PWc + NREFL);
-      } else if constexpr (g == 2) {
-        R8W(NREFL + PWc);
-      } else if constexpr (g < 7) {
-        R8W(PWc);
-      } else {
-        if (more) R8W(PWc); else vm_wait_imm<0>();
-      }
-#undef R8W
-      __syncthreads();                                 // row g landed; row g - 1's readers done
-      DSP(r8t[1] += __builtin_amdgcn_s_memtime() - r8_w;)
-      const uint32_t slot = (krow + g) % 3u;
-      fix_row(ycur, g, slot);
-      // row g + 2 into row g - 1's slot (the next symbol's rows 0, 1 from g = 6, 7)
-      if constexpr (g + 2 < (uint32_t)NA) issue_row(ycur, g + 2, (krow + g + 2) % 3u);
-      else if (more) issue_row(ynext, g + 2 - NA, (krow + g + 2) % 3u);
-      if constexpr (g == 0 && REF == 1) {   // this symbol's reference indices: the dword holding byte k
-        const uint32_t tt = tid_now(), h = tt & 1u, k = 8 * (tt >> 1) + q;
-        const uint64_t rowstep = a.o_ts;
-        const auto rref = sgpr_ptr(a.ref_idx + rfl64((uint64_t)(fcr[f] >> 16) * NA * a.max_out * a.M_occ + (uint64_t)s * a.o_ss));
-        const uint32_t rb = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)rl + wv * 1024u);
-#pragma unroll
-        for (int j = 0; j < 4; j++)
-          dma_u32(((4 * h + j) * (uint32_t)rowstep + k) & ~3u, rref, rb + 256u * (uint32_t)j);
-      }
-      // c_q[n] of antenna g: sum over r of x[n + 512 r] W_8^{r q} (two halves of four), times
-      // W_4096^{n q}
-      {
-        const uint32_t tt = tid_now(), n = tt >> 1, hA = tt & 1u;
-        const uint32_t odd = (uint32_t)((ycur.e0 + (int64_t)g * (int64_t)a.stride) & (SP::SPC - 1));
-        const char *sl = ring + slot * SP::SLOTB;
-        const uint32_t p0 = n + odd + 2048u * hA;
-        v2f c = SP::read(sl, p0 + 1536u, a.iq_scale);
-#pragma unroll
-        for (int j = 2; j >= 0; j--) c = cmac_pk(SP::read(sl, p0 + 512u * (uint32_t)j, a.iq_scale), c, w8);   // c = x_j + c W_8^q
-        const v2f o = v2f{__int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(c.x), 0xB1, 0xf, 0xf, false)),
-                          __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(c.y), 0xB1, 0xf, 0xf, false))};
-        if (hA == 0) {
-          v2f cc = c + o * sgn_q;                      // S_0 + W_8^{4q} S_1
-          cc = cmul_pk(cc, wnl[n]);
-          img[g * RS + n] = cc;
-        }
-      }
-    };
-    row_step(std::integral_constant<uint32_t, 0>{});
-    row_step(std::integral_constant<uint32_t, 1>{});
-    row_step(std::integral_constant<uint32_t, 2>{});
-    row_step(std::integral_constant<uint32_t, 3>{});
-    row_step(std::integral_constant<uint32_t, 4>{});
-    row_step(std::integral_constant<uint32_t, 5>{});
-    row_step(std::integral_constant<uint32_t, 6>{});
-    row_step(std::integral_constant<uint32_t, 7>{});
-    krow = (krow + NA) % 3u;
-    first = false;
-    __syncthreads();                                   // every c_q of the symbol in the image
-    DSP(const unsigned long long r8_a = __builtin_amdgcn_s_memtime(); r8t[2] += r8_a - r8_0;)
-    // ---- stage B: antenna g's 512-point transform on wave g
-    if (wv < (uint32_t)NA) {
-      const int ln = (int)lane_now();
-      v2f w1[2];
-      w1[0] = w1l[2 * ln];
-      w1[1] = w1l[2 * ln + 1];
-      wave512_fwd(img + wv * RS, w1, ln);
-    }
-    __syncthreads();                                   // X_g[8 k' + q] at img[g][k']
-    DSP(const unsigned long long r8_b = __builtin_amdgcn_s_memtime(); r8t[3] += r8_b - r8_a;)
-    // ---- stage C: apply (antenna by antenna into four accumulators), demap, EVM, stores
-    const uint32_t tC = tid_now(), lane = tC & 63u, kq = tC >> 1, h = tC & 1u, k = 8 * kq + q;
-    v2f acc[4] = {v2f{0.0f, 0.0f}, v2f{0.0f, 0.0f}, v2f{0.0f, 0.0f}, v2f{0.0f, 0.0f}};
-    {
-      const v2f *xp = img + kq;
-#pragma unroll
-      for (int g = 0; g < NA; g++) {
-        const v2f Xg = xp[g * RS];
-#pragma unroll
-        for (int j = 0; j < 4; j++) acc[j] = cmac_pk(acc[j], Wr[j][g], Xg);
-      }
-    }
-    if constexpr (REF == 1) {   // this wave's reference dwords landed (only later rows after them)
-      if (!more) vm_wait_imm<0>();
-      else if (w0) vm_wait_imm<2 * PW0>();
-      else vm_wait_imm<2 * PW1>();
-    }
-    const uint32_t cr = fcr[f];
-    const uint64_t frame_id = a.frame_id0 + (cr >> 16);
-    const uint64_t rowstep = a.o_ts;
-    const uint64_t ob0 = rfl64(((uint64_t)f * NA) * a.max_out * a.M_occ + (uint64_t)s * a.o_ss);
-    const auto osym = sgpr_ptr(reinterpret_cast<v2f *>(a.out_sym) + ob0);
-    const auto oidx = sgpr_ptr(a.out_idx + ob0);
-#pragma unroll
-    for (int j = 0; j < 4; j++) {
-      const uint32_t t = 4 * h + (uint32_t)j;
-      const uint32_t off = t * (uint32_t)rowstep + k;   // < 2^32: checked at launch
-      const v2f y = acc[j];
-      const uint32_t d = gidx[qam_level_pair_pk(y, inv_sc, Lf, Lm1, a.qam.L)];
-      uint32_t refi;
-      if constexpr (REF == 1)   // (byte k & 3 = q & 3 of the dword: a uniform shift)
-        refi = (rl[wv * 256u + 64u * (uint32_t)j + (uint32_t)lane] >> (8u * (q & 3u))) & 0xFFu;
-      else if constexpr (REF == 2)
-        refi = (uint32_t)(hash5(a.ref_seed, DOM_DATA, frame_id, t, (uint64_t)s * a.M_occ + k) &
-                          (uint64_t)(a.qam.L * a.qam.L - 1));
-      else refi = d;
-      const unsigned long long bal = __builtin_amdgcn_ballot_w64(refi != d);
-      n_err[0][j] += (uint32_t)__builtin_popcountll(bal & 0x5555555555555555ull);
-      n_err[1][j] += (uint32_t)__builtin_popcountll(bal & 0xAAAAAAAAAAAAAAAAull);
-      const v2f sp = ptab[refi];
-      const v2f er = y - sp;
-      e_num[j] = __builtin_fmaf(er.x, er.x, __builtin_fmaf(er.y, er.y, e_num[j]));
-      e_den[j] = __builtin_fmaf(sp.x, sp.x, __builtin_fmaf(sp.y, sp.y, e_den[j]));
-      // (plain stores: the eight classes' outputs -- every eighth subcarrier each -- merge into
-      // whole lines in the XCD's L2; non-temporal partial-line stores would not)
-      if constexpr (OUTS & 1) osym[off] = y;
-      if constexpr (OUTS & 2) oidx[off] = (uint8_t)d;
-    }
-    new_frame = fn != f;
-    if (!more || new_frame) flush(f);
-    DSP(r8t[4] += __builtin_amdgcn_s_memtime() - r8_b; r8t[0]++;)
-    f = fn;
-    s = sn;
-    ycur = ynext;
-  }
-  DSP(if (a.prof && threadIdx.x == DS_PROF_TID) {
-    for (int qq = 0; qq < 5; qq++) atomicAdd(&a.prof[qq], r8t[qq]);
-  })
-}
-
-// the residue-class decode's LDS and grid: two images; 64 workgroups per 8 XCDs x 8 classes
-static size_t res8_lds_bytes(bool sc16) {
-  return sizeof(float2) * (8 * kR8RS + kR8MS + 128) + 16 * 1024 +
-         3 * (size_t)(sc16 ? R8Stage<true>::SLOTB : R8Stage<false>::SLOTB);
-}
-static uint32_t res8_grid(uint32_t n_cu) { return 64u * std::max(1u, n_cu / 64u); }
-
-bool decode_res8_accepts(const DecodeArgs &a, int log2M, uint32_t n_frames) {
-  // opt-in (RMIMO_DECODE_RES=1): measured 2.58 ms per C4 step against the split form's 1.35
-  // (profiles/r04/pmc_c4.json: waves parked 74% on its register-staged loads, VALU 6%)
-  static const bool on = [] { const char *e = getenv("RMIMO_DECODE_RES"); return e && e[0] == '1'; }();
-  return on && a.N == 8 && log2M == 12 && a.detector != 3 && a.all_occ &&
-         n_frames <= kStreamMaxFrames && a.qam.L * a.qam.L <= kStreamMaxQam && a.cpe == 0 &&
-         ((uintptr_t)a.iq & 15u) == 0 && a.frame_len >= 2 * 4096 + 64 &&
-         (a.ref_mode != 1 || ((uintptr_t)a.ref_idx & 3u) == 0);
-}
-
-// EVM records per frame the residue decode may write (the classes of every group)
-uint32_t res8_records(uint32_t n_cu) { return res8_grid(n_cu); }
-
-uint32_t launch_decode_res8(const DecodeArgs &a, int log2M, uint32_t n_frames, hipStream_t s) {
-  if (!a.nrec || !decode_res8_accepts(a, log2M, n_frames)) return 0;
-  if (res8_records(a.n_cu) > a.rec_stride) return 0;  // EVM space
-  if ((uint64_t)a.N * a.max_out * a.M_occ >= (1ull << 32)) return 0;   // 32-bit lane offsets
-  const int outs = (a.out_sym ? 1 : 0) | (a.out_idx ? 2 : 0);
-  void (*kern)(DecodeArgs) = nullptr;
-#define R8K(R, S)                                                              \
-  (outs == 3 ? decode_res8_kernel<R, 3, S> : outs == 2 ? decode_res8_kernel<R, 2, S> \
-   : outs == 1 ? decode_res8_kernel<R, 1, S> : decode_res8_kernel<R, 0, S>)
-  if (a.sc16) kern = a.ref_mode == 1 ? R8K(1, true) : a.ref_mode == 2 ? R8K(2, true) : R8K(0, true);
-  else kern = a.ref_mode == 1 ? R8K(1, false) : a.ref_mode == 2 ? R8K(2, false) : R8K(0, false);
-#undef R8K
-  const size_t shm = res8_lds_bytes(a.sc16 != 0);
-  if (hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
-                          (int)shm) != hipSuccess)
-    return 0;
-  hipLaunchKernelGGL(kern, dim3(res8_grid(a.n_cu)), dim3(kR8T), shm, s, a);
-  return kR8T / 64;
-}
-
 bool decode_split_accepts(const DecodeArgs &a, int log2M) {
   // (the apply reads 16 bytes of reference indices per lane)
   return a.N == 8 && a.detector != 3 && a.all_occ && log2M >= 9 && log2M <= 12 &&
@@ -2176,12 +1625,15 @@ bool decode_split_accepts(const DecodeArgs &a, int log2M) {
 }
 
 // symbols per group: every symbol in one group (the spectra of the whole batch in the
-// scratch) unless RMIMO_SPLIT_GROUP = G > 0 (the Infinity-Cache-sized groups, e.g. 32: measured
+// scratch). Infinity-Cache-sized groups (e.g. 32, compile with -DDS_SPLIT_GROUP=32) measured
 // slower at C4 x 8 -- 2.10 vs 1.58 ms per decode -- because each group's apply re-reads its
-// chunk's weights, 16x the weight traffic, and each launch is a quarter of the chip)
+// chunk's weights, 16x the weight traffic, and each launch is a quarter of the chip
 uint32_t split_group_symbols(uint32_t max_out) {
-  static const int env = [] { const char *e = getenv("RMIMO_SPLIT_GROUP"); return e ? atoi(e) : 0; }();
-  const uint32_t g = env <= 0 ? max_out : (uint32_t)env;
+#ifdef DS_SPLIT_GROUP
+  const uint32_t g = DS_SPLIT_GROUP;
+#else
+  const uint32_t g = max_out;
+#endif
   return std::max(1u, std::min(g, max_out));
 }
 
@@ -2234,7 +1686,11 @@ uint32_t launch_decode_split(const DecodeArgs &a, int log2M, uint32_t n_frames, 
     hipLaunchKernelGGL(kp, dim3(a.n_cu * resident_blocks((const void *)kp, TP, shm)), dim3(TP), \
                        shm, s, g);                                                       \
   } while (0)
-    static const bool one_item = [] { const char *e = getenv("RMIMO_SPECTRA_ITEM"); return e && e[0] == '1'; }();
+#ifdef DS_SPECTRA_ITEM   // A/B build: one workgroup per (symbol, antenna) instead of the persistent form
+    constexpr bool one_item = true;
+#else
+    constexpr bool one_item = false;
+#endif
     switch (log2M) {
       case 9: SPECTRA(9); break;
       case 10: SPECTRA(10); break;
@@ -2243,9 +1699,9 @@ uint32_t launch_decode_split(const DecodeArgs &a, int log2M, uint32_t n_frames, 
     }
 #undef SPECTRA
 #undef SPECTRA_P
-    static const bool v1_env = [] { const char *e = getenv("RMIMO_APPLY_V1"); return e && e[0] == '1'; }();
-    // (the 128-subcarrier form stores 16 bytes of symbols and 2 of indices per lane)
-    const bool v1 = v1_env || ((uintptr_t)a.out_sym & 15u) || ((uintptr_t)a.out_idx & 1u);
+    // (the 128-subcarrier form stores 16 bytes of symbols and 2 of indices per lane: the
+    // 64-subcarrier form takes outputs without that alignment)
+    const bool v1 = ((uintptr_t)a.out_sym & 15u) || ((uintptr_t)a.out_idx & 1u);
     if (v1) {
       if (a.ref_mode == 1) hipLaunchKernelGGL((apply_split_kernel<8, 1>), g2, dim3(256), 0, s, g);
       else if (a.ref_mode == 2) hipLaunchKernelGGL((apply_split_kernel<8, 2>), g2, dim3(256), 0, s, g);
@@ -2316,9 +1772,8 @@ static uint32_t stream_launch(const DecodeArgs &a, hipStream_t s) {
 }
 
 static bool stream_geometry_ok(const DecodeArgs &a, int log2M, uint32_t n_frames) {
-  static const bool off = [] { const char *e = getenv("RMIMO_DECODE_STREAM"); return e && e[0] == '0'; }();
   // (capture and reference row of a frame are packed in 16 bits each in LDS)
-  if (off || a.detector == 3 || !a.all_occ || n_frames > kStreamMaxFrames ||
+  if (a.detector == 3 || !a.all_occ || n_frames > kStreamMaxFrames ||
       a.n_caps > 0xFFFFu || a.n_refs > 0xFFFFu ||
       a.qam.L * a.qam.L > kStreamMaxQam)
     return false;

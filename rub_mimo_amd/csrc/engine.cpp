@@ -220,7 +220,7 @@ struct mimo_rx {
   float2 *tw = nullptr;
   Codes codes;
   DevBuf<float> vscale;
-  DevBuf<int8_t> s1sign;
+  DevBuf<int8_t> s1sign, s1sign_w;   // signs [N][nac][M]; ls_window_kernel's order
   DevBuf<int32_t> occ;
   // workspace
   uint32_t cap_frames = 0;
@@ -233,8 +233,6 @@ struct mimo_rx {
   DevBuf<float> gain;
   DevBuf<double> nvp, evm_part, evm_out, lspart, evm_chunk;
   DevBuf<float2> lsq;                   // fused search + LS: X/S1 per access code
-  DevBuf<uint32_t> ls_arrive;           // fused LS combine: [F][N][N] counters (self-resetting)
-  size_t cap_ls_arrive = 0;
   DevBuf<uint32_t> evm_cnt;             // per-frame chunk counters of evm_kernel (self-resetting)
   DevBuf<uint32_t> nrec;                // per-frame EVM records of the streaming decode
   size_t cap_lspart = 0;
@@ -381,21 +379,10 @@ int run_sync(mimo_rx *h, const float2 *iq, uint64_t stride, uint32_t F, uint64_t
     a.iq = iq; a.stride = stride; a.frame_len = frame_len;
     a.sc16 = h->cur_sc16; a.iq_scale = h->cur_scale;
     a.N = h->N; a.M = h->M; a.cp = h->cp;
-    // diagnostics only: RMIMO_SC_BAND overrides the exact-recompute band (a band below the
-    // fp32 error bound breaks parity)
-    static const double band_env = [] { const char *e = getenv("RMIMO_SC_BAND"); return e ? atof(e) : -1.0; }();
     a.thr = h->thr;
-    a.band = band_env >= 0.0 ? band_env : sc_band(h->M);
+    a.band = sc_band(h->M);
     static const int diag_env = [] { const char *e = getenv("RMIMO_SC_DIAG"); return e ? atoi(e) : 0; }();
     a.diag = (uint32_t)diag_env;
-    // workgroups per (item, antenna) of the exact pass, each a contiguous share of the item's
-    // iterations: 1 (default), 2 or 4 (RMIMO_SC_SPLIT; 1 there selects 4, as before)
-    static const uint32_t split_env = [] {
-      const char *e = getenv("RMIMO_SC_SPLIT");
-      const int v = e ? atoi(e) : 0;
-      return v == 1 ? (uint32_t)(kScSpan / kScIterLen) : (v == 2 || v == 4) ? (uint32_t)v : 1u;
-    }();
-    a.split_iters = split_env;
     a.chunk_len = K; a.chunk_lo = chunk_lo; a.chunk_hi = nchunks;
     a.trig = h->trig.p; a.rec = h->rec.p; a.rec_stride = h->cap_chunks;
     a.cand = stream ? h->cand.p : nullptr;
@@ -409,10 +396,9 @@ int run_sync(mimo_rx *h, const float2 *iq, uint64_t stride, uint32_t F, uint64_t
     add_fill(h->queue.p, 3 * sizeof(uint32_t), 0u);
     a.queue = h->queue.p;
     a.hot_count = h->queue.p + 1;
-    // screened path (default when the geometry allows it; RMIMO_SC_LEGACY=1 selects the
-    // per-chunk item kernel): one hot item per listed chunk
-    static const bool legacy = [] { const char *e = getenv("RMIMO_SC_LEGACY"); return e && e[0] == '1'; }();
-    const bool screen = !legacy && sc_screen_ok(h->M);
+    // screened path where the geometry allows it (else the per-chunk item kernel): one hot item
+    // per listed chunk
+    const bool screen = sc_screen_ok(h->M);
     const uint64_t n_list = (nchunks - chunk_lo) * (uint64_t)F;
     const uint32_t hot_cap = screen ? (uint32_t)n_list : 8 * F + 32;
     if (hot_cap > h->cap_hot) {
@@ -577,37 +563,33 @@ int run_estimate(mimo_rx *h, const float2 *iq, uint64_t stride, uint32_t F, uint
   la.iq = iq; la.stride = stride; la.frame_len = frame_len;
   la.N = h->N; la.M = h->M; la.nac = h->nac; la.n_slots = h->n_slots;
   la.keys = h->keys.p; la.s1sign = h->s1sign.p; la.occ_index = h->occ.p;
+  la.s1sign_w = h->s1sign_w.p;
   la.keep_bias = h->keep_bias; la.scale = h->ls_scale; la.info = h->info.p;
   la.n_groups = (h->nac + kLsCodesPerGroup - 1) / kLsCodesPerGroup;
   la.n_nvp = h->N * h->N * ((h->M + 255) / 256);
   la.G = h->G.p; la.nv_part = h->nvp.p; la.tw = h->tw;
-  if (h->search_ls) {
+  la.sc16 = h->cur_sc16; la.iq_scale = h->cur_scale;
+  // LS straight from the windows (ls_window_kernel) after a search that only finds the keys,
+  // unless the opt-in CFO rotates the LS terms between the search and the combine (or
+  // RMIMO_LS_FORM=terms: the search's fused terms and ls_combine_q_kernel, the parity tests'
+  // reference for this form)
+  static const bool ls_terms = [] { const char *e = getenv("RMIMO_LS_FORM"); return e && strcmp(e, "terms") == 0; }();
+  const bool ls_win = h->search_ls && !cfo && !ls_terms && h->log2M >= 9 && h->log2M <= 12;
+  if (h->search_ls && ls_win) {
+    sa.xcd_order = 1;
+    hipEvent_t e = h->timer.begin(s);
+    launch_search_ls(sa, h->log2F, h->log2M, F, s);   // keys only (sa.lsq null)
+    h->timer.end(2, e, s);
+    e = h->timer.begin(s);
+    launch_ls_window(la, h->log2M, F, s);
+    h->timer.end(3, e, s);
+  } else if (h->search_ls) {
     // search of slot pairs with the LS terms fused in, then the fixed-order LS combine
     HIPCHK(h->lsq.ensure((size_t)F * h->N * h->N * h->nac * h->M));
     sa.s1sign = h->s1sign.p; sa.lsq = h->lsq.p; sa.nac = h->nac;
     sa.cfo_part = (cfo && cfo->fold) ? cfo->part : nullptr;   // folded CFO: derotating loads
-    static const int xcd = [] { const char *e = getenv("RMIMO_SEARCH_XCD"); return e ? atoi(e) : 1; }();
-    sa.xcd_order = (uint32_t)xcd;
-    static const int fr_chunk = [] { const char *e = getenv("RMIMO_LS_CHUNK"); return e ? atoi(e) : 32; }();
-    sa.fr_chunk = (uint32_t)std::max(fr_chunk, 1);
+    sa.xcd_order = 1;
     la.lsq = h->lsq.p;
-    // opt-in (RMIMO_LS_FUSE=1, not with CFO, whose stage 2 rotates the terms in between): the
-    // LS combine fused into the search's last workgroup per (frame, rx, tx). Measured slower
-    // than the separate ls_combine_q_kernel (C3 search + LS 0.555 vs 0.521 ms, C4 0.673 vs
-    // 0.586; DESIGN "LS combine fused into the search")
-    static const bool ls_fuse = [] { const char *e = getenv("RMIMO_LS_FUSE"); return e && e[0] == '1'; }();
-    const bool fuse = ls_fuse && !cfo && search_ls_wave_enabled() && h->codes.codespec_w.p;
-    if (fuse) {
-      const size_t need = (size_t)F * h->N * h->N;
-      if (need > h->cap_ls_arrive) {
-        HIPCHK(h->ls_arrive.ensure(need));
-        HIPCHK(hipMemsetAsync(h->ls_arrive.p, 0, sizeof(uint32_t) * need, s));
-        h->cap_ls_arrive = need;
-      }
-      sa.ls_arrive = h->ls_arrive.p;
-      sa.G = h->G.p; sa.nv_part = h->nvp.p; sa.n_nvp = la.n_nvp;
-      sa.occ_index = h->occ.p; sa.keep_bias = h->keep_bias; sa.ls_scale = h->ls_scale;
-    }
     hipEvent_t e = h->timer.begin(s);
     launch_search_ls(sa, h->log2F, h->log2M, F, s);
     h->timer.end(2, e, s);
@@ -616,8 +598,8 @@ int run_estimate(mimo_rx *h, const float2 *iq, uint64_t stride, uint32_t F, uint
       launch_cfo_batch(*cfo, F, 2, s);
       la.cfo_part = cfo->part;
     }
-    e = h->timer.begin(s);   // (fused: the LS stage's clock stays, empty)
-    if (!fuse) launch_ls_combine_q(la, F, s);
+    e = h->timer.begin(s);
+    launch_ls_combine_q(la, F, s);
     h->timer.end(3, e, s);
   } else {
     hipEvent_t e = h->timer.begin(s);
@@ -653,17 +635,6 @@ int run_estimate(mimo_rx *h, const float2 *iq, uint64_t stride, uint32_t F, uint
   return MIMO_OK;
 }
 
-// diagnostics that force the per-symbol decode kernels: RMIMO_DECODE_GRID=1 (the
-// one-workgroup-per-symbol grid, A/B against the persistent form) and RMIMO_DEC_EXPT
-bool decode_grid_only() {
-  static const bool v = [] { const char *e = getenv("RMIMO_DECODE_GRID"); return e && e[0] == '1'; }();
-  return v;
-}
-int decode_expt() {
-  static const int v = [] { const char *e = getenv("RMIMO_DEC_EXPT"); return e ? atoi(e) : 0; }();
-  return v;
-}
-
 int run_decode(mimo_rx *h, const float2 *iq, uint64_t stride, uint32_t F, uint64_t frame_len,
                uint32_t max_out, float2 *out_sym, uint8_t *out_idx, int ref_mode,
                const uint8_t *ref_idx, uint64_t ref_seed, uint64_t frame_id0, hipStream_t s,
@@ -690,8 +661,7 @@ int run_decode(mimo_rx *h, const float2 *iq, uint64_t stride, uint32_t F, uint64
   d.qam = h->qam; d.evm_part = h->evm_part.p; d.tw = h->tw;
   d.n_frames = F; d.n_cu = h->n_cu;
   d.n_caps = n_caps ? n_caps : F; d.n_refs = F;
-  d.all_occ = (h->M_occ == h->M && !decode_grid_only()) ? 1 : 0;
-  d.expt = decode_expt();
+  d.all_occ = (h->M_occ == h->M) ? 1 : 0;
   static const bool dprof = [] { const char *e = getenv("RMIMO_DEC_PROF"); return e && e[0] == '1'; }();
   if (dprof) {
     if (!h->sc_prof.p) HIPCHK(h->sc_prof.ensure(28));
@@ -702,13 +672,8 @@ int run_decode(mimo_rx *h, const float2 *iq, uint64_t stride, uint32_t F, uint64
   d.nrec = h->nrec.p;
   d.cpe = h->cfo ? (cfo_fold_part ? 2 : 1) : 0;
   d.cfo_part = cfo_fold_part;
-  static const bool no_split = [] { const char *e = getenv("RMIMO_DECODE_SPLIT"); return e && e[0] == '0'; }();
   d.rec_stride = max_out;
-  // (the split records' stride only where the split kernels can run: RMIMO_DEC_EXPT forces
-  // the per-symbol kernels, whose records are max_out apart)
-  if (d.expt == 0 && decode_res8_accepts(d, h->log2M, F))   // residue-class records per frame
-    d.rec_stride = std::max(d.rec_stride, res8_records(h->n_cu));
-  if (!no_split && d.expt == 0 && decode_split_accepts(d, h->log2M)) {
+  if (decode_split_accepts(d, h->log2M)) {
     // [F][group][N][M] complex64 spectra of the 8x8 split decode (one symbol group)
     if (h->spec.ensure((size_t)F * split_group_symbols(max_out) * h->N * h->M) != hipSuccess)
       return fail(MIMO_ERR_NOMEM, "split decode scratch");
@@ -755,7 +720,7 @@ int run_decode(mimo_rx *h, const float2 *iq, uint64_t stride, uint32_t F, uint64
   ea.counter = h->evm_cnt.p;
   ea.nrec = per_frame ? h->nrec.p : nullptr;
   // per workgroup segment (streaming, residue-class), not per chunk x range
-  ea.few = (path == MIMO_DECODE_STREAM || path == MIMO_DECODE_RESIDUE) ? 1 : 0;
+  ea.few = (path == MIMO_DECODE_STREAM) ? 1 : 0;
   e = h->timer.begin(s);
   launch_evm(ea, F, s);
   h->timer.end(6, e, s);
@@ -838,8 +803,7 @@ int mimo_rx_create(const mimo_rx_config *cfg, void *hip_stream, mimo_rx **out) {
   // several lag chunks per slot) and a separate LS pass.
   uint32_t F = 1;
   while (F < 2 * h->SL + h->M - 1 || F < 2 * h->M) F <<= 1;
-  static const bool no_fuse = [] { const char *e = getenv("RMIMO_SEARCH_LS"); return e && e[0] == '0'; }();
-  h->search_ls = !no_fuse && F <= 16384 && search_ls_supported(ilog2(F), ilog2(h->M));
+  h->search_ls = F <= 16384 && search_ls_supported(ilog2(F), ilog2(h->M));
   if (!h->search_ls) {
     F = 1;
     while (F < h->SL + h->M - 1) F <<= 1;
@@ -876,6 +840,18 @@ int mimo_rx_create(const mimo_rx_config *cfg, void *hip_stream, mimo_rx **out) {
   const double FF = (double)F * (double)F, MM = (double)h->M * (double)h->M;
   vs[0] = (float)((double)m_s0 / (MM * FF));
   for (uint32_t sl = 1; sl < h->n_slots; sl++) vs[sl] = (float)(1.0 / ((double)h->M * FF));
+  if (h->M >= 512) {   // ls_window_kernel: thread lt's 8 subcarriers lt + (M/8) e adjacent
+    const uint32_t T = h->M / 8;
+    std::vector<int8_t> sw(sign.size());
+    for (size_t row = 0; row < (size_t)N * h->nac; row++)
+      for (uint32_t lt = 0; lt < T; lt++)
+        for (uint32_t e = 0; e < 8; e++) sw[row * h->M + 8 * lt + e] = sign[row * h->M + lt + T * e];
+    if (h->s1sign_w.ensure(sw.size()) != hipSuccess ||
+        hipMemcpy(h->s1sign_w.p, sw.data(), sw.size(), hipMemcpyHostToDevice) != hipSuccess) {
+      mimo_rx_destroy(h);
+      return fail(MIMO_ERR_HIP, "table upload failed");
+    }
+  }
   if (h->vscale.ensure(h->n_slots) != hipSuccess || h->s1sign.ensure(sign.size()) != hipSuccess ||
       h->occ.ensure(h->M) != hipSuccess ||
       hipMemcpy(h->vscale.p, vs.data(), sizeof(float) * vs.size(), hipMemcpyHostToDevice) !=
@@ -1375,17 +1351,16 @@ static uint32_t batch_fpc(const mimo_batch *b) {
 static bool cfo_folds(const mimo_rx *h, const mimo_batch *b, bool widened) {
   if (!h->cfo || !h->search_ls) return false;
   if (b->sample_format == MIMO_SAMPLE_SC16 && !widened) return false;
-  static const bool off = [] { const char *e = getenv("RMIMO_CFO_FOLD"); return e && e[0] == '0'; }();
-  if (off || b->ref_mode != 1 || (!b->d_out_sym) != (!b->d_out_idx)) return false;
+  if (b->ref_mode != 1 || (!b->d_out_sym) != (!b->d_out_idx)) return false;
   DecodeArgs probe{};
   probe.N = h->N; probe.detector = h->det;
-  probe.all_occ = (h->M_occ == h->M && !decode_grid_only()) ? 1 : 0;
+  probe.all_occ = (h->M_occ == h->M) ? 1 : 0;
   probe.n_caps = b->n_frames; probe.n_refs = b->n_frames * batch_fpc(b); probe.qam = h->qam;
   probe.ref_mode = b->ref_mode; probe.ref_idx = reinterpret_cast<const uint8_t *>(b->d_ref_idx);
   probe.stride = b->stride; probe.max_out = b->max_out_syms; probe.M_occ = h->M_occ;
   probe.out_sym = reinterpret_cast<float2 *>(b->d_out_sym);
   probe.out_idx = reinterpret_cast<uint8_t *>(b->d_out_idx);
-  return decode_expt() == 0 && decode_stream_accepts(probe, h->log2M, b->n_frames * batch_fpc(b));
+  return decode_stream_accepts(probe, h->log2M, b->n_frames * batch_fpc(b));
 }
 
 static int run_batch(mimo_rx *h, const mimo_batch *b, hipStream_t s) {
@@ -1399,18 +1374,16 @@ static int run_batch(mimo_rx *h, const mimo_batch *b, hipStream_t s) {
     // where the configuration takes them; otherwise widened once into an internal fc32 batch
     DecodeArgs probe{};
     probe.N = h->N; probe.detector = h->det;
-    probe.all_occ = (h->M_occ == h->M && !decode_grid_only()) ? 1 : 0;
+    probe.all_occ = (h->M_occ == h->M) ? 1 : 0;
     probe.n_caps = b->n_frames; probe.n_refs = slots; probe.qam = h->qam;
     probe.ref_mode = b->ref_mode; probe.ref_idx = reinterpret_cast<const uint8_t *>(b->d_ref_idx);
     probe.stride = b->stride; probe.max_out = b->max_out_syms; probe.M_occ = h->M_occ;
     probe.out_sym = reinterpret_cast<float2 *>(b->d_out_sym);
     probe.out_idx = reinterpret_cast<uint8_t *>(b->d_out_idx);
     probe.sc16 = 1;
-    static const bool no_split = [] { const char *e = getenv("RMIMO_DECODE_SPLIT"); return e && e[0] == '0'; }();
-    const bool fused = sc_screen_ok(h->M) && h->search_ls && !h->cfo && decode_expt() == 0 &&
+    const bool fused = sc_screen_ok(h->M) && h->search_ls && !h->cfo &&
                        (decode_stream_accepts(probe, h->log2M, slots) ||
-                        decode_res8_accepts(probe, h->log2M, slots) ||
-                        (!no_split && decode_split_accepts(probe, h->log2M)));
+                        decode_split_accepts(probe, h->log2M));
     if (fused) {
       h->cur_sc16 = 1;
       h->cur_scale = b->sc16_scale;

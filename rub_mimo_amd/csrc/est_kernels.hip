@@ -12,6 +12,8 @@
 // F-sample window segment, multiply by conj(FFT_F(zero-padded code)), IFFT_F; lags
 // [0, F-M] are exact linear correlations. First-maximum semantics (strict '>', initial 0,
 // framing.cc:718, 735) are kept by packing (value bits, ~index) into one 64-bit atomicMax.
+#include <cstring>
+
 #include "fft.hpp"
 #include "fft_reg.hpp"
 #include "kernels.hpp"
@@ -386,7 +388,7 @@ void search_ls_kernel(SearchArgs a) {
   constexpr int PBM = lds_padded_len(M), NL = 2 * M / T;
   static_assert(2 * M % T == 0, "whole windows per thread");
   const bool valid0 = s0 != 0, valid1 = ns > 1;
-  if (!valid0 && !valid1) return;                     // uniform
+  if ((!valid0 && !valid1) || !a.lsq) return;         // uniform (no lsq: ls_window_kernel)
   const int64_t w0 = I.base + (int64_t)key_index(s_key[0]);
   const int64_t w1v = I.base + (int64_t)key_index(s_key[1]);
   if constexpr (LSREG) {
@@ -463,120 +465,10 @@ void search_ls_kernel(SearchArgs a) {
   }
 }
 
-// LS term stores and the fused combine's loads. Fused, they are agent-coherent (relaxed
-// agent-scope atomics: sc1, written through / read past the XCD's L2), so the arrival needs no
-// L2 write-back or invalidate (an agent-scope fence per workgroup costs ~6x the search); else
-// non-temporal, read once by ls_combine_q_kernel.
+// LS term store: non-temporal, read once by ls_combine_q_kernel
 template <typename PT>   // v2f * or gptr<v2f>
-__device__ __forceinline__ void ls_term_store(PT p, v2f t, bool coherent) {
-  if (coherent) {
-    unsigned long long b;
-    __builtin_memcpy(&b, &t, sizeof(b));
-    __hip_atomic_store((gptr<unsigned long long>)p, b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  } else {
-    __builtin_nontemporal_store(t, p);
-  }
-}
-__device__ __forceinline__ v2f ls_term_load(const v2f *p) {
-  const unsigned long long b = __hip_atomic_load(reinterpret_cast<const unsigned long long *>(p),
-                                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  v2f t;
-  __builtin_memcpy(&t, &b, sizeof(t));
-  return t;
-}
-
-// The LS combine of one (frame, rx, tx), run by the search workgroup that stored its last
-// access code's terms (framing.cc:801-824): ls_combine_q_kernel's arithmetic and order -- per
-// subcarrier the codes' X/S1 summed in code order in fp64, G = (bias + sum) * scale, and the
-// training residual's variance -- with its reduction tree: a 64-lane xor butterfly per 64
-// subcarriers, then the four of each 256 summed left to right into the same nv_part entry.
-// G and nv_part are therefore bitwise those of the separate kernel.
-template <int T>
-__device__ __forceinline__ void ls_combine_fused(const SearchArgs &a, uint32_t f, uint32_t r,
-                                                 uint32_t t, double *red) {
-  const uint32_t M = a.M, N = a.N, nac = a.nac;
-  const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
-  const uint32_t rt = r * N + t, nitems = (M + 63) / 64;
-  const v2f *q0 = reinterpret_cast<const v2f *>(a.lsq) + (((uint64_t)f * N + r) * N + t) * nac * M;
-  const double bias = (a.keep_bias && r == t) ? 1.0 : 0.0;
-  // (every code's term of the lane's subcarrier loaded before any is summed: one memory
-  // latency per subcarrier instead of one per batch; codes beyond CMAX in further rounds)
-  constexpr uint32_t CMAX = 24;
-  for (uint32_t it = wv; it < nitems; it += T / 64) {   // uniform per wave
-    const uint32_t k = it * 64 + lane;
-    double nv = 0.0;
-    if (k < M) {
-      const bool occ = a.occ_index[k] >= 0;
-      const v2f *q = q0 + k;
-      double sr = 0.0, si = 0.0, s2 = 0.0;
-      for (uint32_t c0 = 0; c0 < nac; c0 += CMAX) {
-        v2f vb[CMAX];
-#pragma unroll
-        for (uint32_t j = 0; j < CMAX; j++)
-          if (c0 + j < nac) vb[j] = ls_term_load(q + (uint64_t)(c0 + j) * M);
-#pragma unroll
-        for (uint32_t j = 0; j < CMAX; j++) {
-          if (c0 + j < nac) {
-            sr += (double)vb[j].x;
-            si += (double)vb[j].y;
-            s2 += (double)vb[j].x * vb[j].x + (double)vb[j].y * vb[j].y;
-          }
-        }
-      }
-      a.G[(((uint64_t)f * M + k) * N + r) * N + t] =
-          occ ? make_float2((float)((bias + sr) * a.ls_scale), (float)(si * a.ls_scale))
-              : make_float2(0.0f, 0.0f);
-      if (occ) nv = s2 - (sr * sr + si * si) / (double)nac;
-    }
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) nv += __shfl_xor(nv, off);
-    if (lane == 0) red[it] = nv;
-  }
-  __syncthreads();
-  const uint32_t nb = (M + 255) / 256;
-  for (uint32_t b = tid; b < nb; b += T) {
-    double v = red[4 * b];
-#pragma unroll
-    for (uint32_t j = 1; j < 4; j++) v += 4 * b + j < nitems ? red[4 * b + j] : 0.0;
-    a.nv_part[(uint64_t)f * a.n_nvp + (uint64_t)rt * nb + b] = v;
-  }
-  __syncthreads();                                     // red free for the next combine
-}
-
-// Arrival of a slot-pair workgroup whose LS terms are stored: one count per valid slot on its
-// (frame, rx, tx) counter, issued after every wave's coherent term stores have completed (the
-// release without an L2 write-back); the workgroup that brings a counter to nac runs that
-// (frame, rx, tx)'s combine, its coherent loads issued after the count returned, and re-arms the
-// counter for the next launch.
-template <int T>
-__device__ __forceinline__ void ls_arrive(const SearchArgs &a, uint32_t f, uint32_t r,
-                                          uint32_t s0, bool valid0, bool valid1, double *red,
-                                          uint32_t *s_last) {
-  const uint32_t N = a.N;
-  const uint32_t tx0 = valid0 ? (s0 - 1) % N : 0u, tx1 = s0 % N;   // slots s0, s0 + 1
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's coherent term stores done
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    uint32_t *ctr = a.ls_arrive + ((uint64_t)f * N + r) * N;
-    s_last[0] = s_last[1] = 0u;
-    if (valid0 && valid1 && tx0 == tx1) {              // (N = 1: both slots one tx)
-      const uint32_t old = __hip_atomic_fetch_add(&ctr[tx0], 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      s_last[0] = old + 2u == a.nac;
-    } else {
-      if (valid0)
-        s_last[0] = __hip_atomic_fetch_add(&ctr[tx0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u == a.nac;
-      if (valid1)
-        s_last[1] = __hip_atomic_fetch_add(&ctr[tx1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u == a.nac;
-    }
-    if (s_last[0]) __hip_atomic_store(&ctr[tx0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (s_last[1]) __hip_atomic_store(&ctr[tx1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  __syncthreads();
-  const uint32_t l0 = s_last[0], l1 = s_last[1];
-  if (l0 | l1) {   // (the terms are read with coherent loads issued after the counts)
-    if (l0) ls_combine_fused<T>(a, f, r, tx0, red);
-    if (l1) ls_combine_fused<T>(a, f, r, tx1, red);
-  }
+__device__ __forceinline__ void ls_term_store(PT p, v2f t) {
+  __builtin_nontemporal_store(t, p);
 }
 
 // The same search + LS with the FFT_F split into one workgroup-wide radix-B pass and B
@@ -612,26 +504,8 @@ void search_ls_wave_kernel(SearchArgs a) {
     const uint32_t x = b % 8, q = G / 8, rem = G % 8;
     const uint32_t lid = x * q + min(x, rem) + b / 8;
     const uint32_t nf = gridDim.y, nrx = a.N;
-    if (a.xcd_order == 2) {   // slot pair fastest: a (frame, rx)'s pairs together on one XCD
-      const uint32_t np = gridDim.x / nrx, fr = lid / np;
-      bx = (lid % np) * nrx + fr % nrx;
-      f = fr / nrx;
-    } else if (a.xcd_order == 3) {
-      // chunks of fr_chunk (frame, rx)s in dispatch order, each walked as order 1 (every XCD a
-      // contiguous range of slot pairs): a chunk's (frame, rx)s complete while the next chunk
-      // searches, so the fused LS combines of all but the last chunk overlap the search
-      const uint32_t np = gridDim.x / nrx, nfr = nf * nrx, K = a.fr_chunk;
-      const uint32_t c = b / (np * K), fr0 = c * K, Kc = min(K, nfr - fr0);
-      const uint32_t bl = b - c * np * K, Gc = np * Kc;
-      const uint32_t xl = bl % 8, ql = Gc / 8, rl = Gc % 8;
-      const uint32_t l = xl * ql + min(xl, rl) + bl / 8;
-      const uint32_t fr = fr0 + l % Kc;
-      bx = (l / Kc) * nrx + fr % nrx;
-      f = fr / nrx;
-    } else {
-      bx = (lid / (nrx * nf)) * nrx + lid % nrx;
-      f = (lid / nrx) % nf;
-    }
+    bx = (lid / (nrx * nf)) * nrx + lid % nrx;
+    f = (lid / nrx) % nf;
   }
   const FrameInfo &I = a.info[f];
   if (I.status != 0) return;
@@ -647,7 +521,13 @@ void search_ls_wave_kernel(SearchArgs a) {
   v2f v[16], X[16];
   // segment loads in the block pass's order: v[i B + rr] = x[n_i + 1024 rr], n_i = tid + T i
   // (a uniform branch: inside the capture plain loads off one base, else clamped indices)
+#ifdef SL_ABL_NOLOAD   // timing ablation (tools/abl_search.sh): no segment loads
+#pragma unroll
+  for (int e = 0; e < 16; e++) v[e] = v2f{(float)e, (float)(tid + (int)abs0)};
+  if (false) {
+#else
   if (inb) {
+#endif
     const auto xb = xs.row((uint64_t)abs0);
 #pragma unroll
     for (int i = 0; i < NB; i++)
@@ -714,8 +594,10 @@ void search_ls_wave_kernel(SearchArgs a) {
     for (int e = 0; e < 16; e++) v[e] = rg[lds_pad(reg_index<10, 16>(lane, e))];
   }
   // wave-local 1024-point forward transform of c_q: X[B k + q], k = lane + 64 e, in v[e]
+#ifndef SL_ABL_NOFWD   // timing ablation: no forward sub-transforms
   reg_compute<10, 16, 0, false>(v, w1);
   wave1024_rest<false>(rg, v, w1, lane);
+#endif
 #pragma unroll
   for (int e = 0; e < 16; e++) X[e] = v[e];
   for (uint32_t u = 0; u < ns; u++) {                 // uniform
@@ -724,8 +606,10 @@ void search_ls_wave_kernel(SearchArgs a) {
         reinterpret_cast<const v2f *>(a.codespec_w + (size_t)slot * F) + wq * 1024 + lane;
 #pragma unroll
     for (int e = 0; e < 16; e++) v[e] = vmulc(X[e], csp[64 * e]);
+#ifndef SL_ABL_NOINV   // timing ablation: no inverse sub-transforms
     reg_compute<10, 16, 0, true>(v, w1);
     wave1024_rest<true>(rg, v, w1, lane);
+#endif
     // Y_q[m'] (m' = lane + 64 e) -> region q; then the radix-B pass over q per m'
     if constexpr (B > 1) {
 #pragma unroll
@@ -789,10 +673,13 @@ void search_ls_wave_kernel(SearchArgs a) {
   }
   // LS terms of the pair's access codes, as search_ls_kernel (register-resident form where
   // the workgroup holds two M-point windows of M/8 threads, else batched through LDS)
+#ifdef SL_ABL_NOLS   // timing ablation: no LS terms
+  return;
+#endif
   constexpr int PBM = lds_padded_len(M), NL = 2 * M / T;
   static_assert(2 * M % T == 0, "whole windows per thread");
   const bool valid0 = s0 != 0, valid1 = ns > 1;
-  if (!valid0 && !valid1) return;                     // uniform
+  if ((!valid0 && !valid1) || !a.lsq) return;         // uniform (no lsq: ls_window_kernel)
   const int64_t w0 = I.base + (int64_t)key_index(s_key[0]);
   const int64_t w1v = I.base + (int64_t)key_index(s_key[1]);
   constexpr bool LSREG = 2 * (M / 8) == T && LOG2M >= 9;
@@ -847,7 +734,7 @@ void search_ls_wave_kernel(SearchArgs a) {
         const int8_t sv = sg[k];
         const float sgn = (float)sv;
         const v2f term = sv ? xw[e] * v2f{sgn, sgn} : v2f{0.0f, 0.0f};
-        ls_term_store(&q[k], term, a.ls_arrive != nullptr);   // read once, by the combine
+        ls_term_store(&q[k], term);   // read once, by the combine
       }
     }
   } else {
@@ -884,14 +771,7 @@ void search_ls_wave_kernel(SearchArgs a) {
       const float2 Xk = lb[uu * PBM + lds_pad(k)];
       const int sgn = sg[k];
       const float2 t = sgn > 0 ? Xk : (sgn < 0 ? cneg(Xk) : make_float2(0.0f, 0.0f));
-      if (a.ls_arrive) ls_term_store(reinterpret_cast<v2f *>(q) + k, v2f{t.x, t.y}, true);
-      else q[k] = t;
-    }
-  }
-  if constexpr (!CFO) {   // fused LS combine (the CFO path rotates the terms first: separate)
-    if (a.ls_arrive) {    // uniform
-      __shared__ uint32_t s_last[2];
-      ls_arrive<T>(a, f, r, s0, valid0, valid1, reinterpret_cast<double *>(lds_raw), s_last);
+      q[k] = t;
     }
   }
 }
@@ -1503,9 +1383,12 @@ static bool search_ls_try(const SearchArgs &a, int log2F, int log2M, uint32_t nf
   return false;
 }
 
-bool search_ls_wave_enabled() {   // on; RMIMO_SEARCH_WAVE=0 is the A/B switch back to the block form
-  static const bool on = [] { const char *e = getenv("RMIMO_SEARCH_WAVE"); return !(e && e[0] == '0'); }();
-  return on;
+// the search form, a parity-test switch: the wave-local search_ls_wave_kernel (F >= 1024), or
+// RMIMO_SEARCH_FORM=block: search_ls_kernel, the same two slots per transform with
+// workgroup-wide exchanges
+bool search_ls_wave_enabled() {
+  static const bool block = [] { const char *e = getenv("RMIMO_SEARCH_FORM"); return e && strcmp(e, "block") == 0; }();
+  return !block;
 }
 
 bool search_ls_supported(int log2F, int log2M) {
@@ -1514,6 +1397,145 @@ bool search_ls_supported(int log2F, int log2M) {
 
 bool launch_search_ls(const SearchArgs &a, int log2F, int log2M, uint32_t n_frames, hipStream_t s) {
   return search_ls_try<10, 1>(a, log2F, log2M, n_frames, s);
+}
+
+// ------------------------------------------------------------------------------------
+// LS estimate of one (frame, rx, tx) straight from its nac access-code windows (framing.cc:
+// 797-824): workgroup (rx tx, frame), M/8 threads with 8 subcarriers each (k = lt + T e); per
+// code c the window at the search's key of slot 1 + c N + tx is loaded one code ahead (the
+// barriers of the transform order LDS only, so the prefetch stays in flight), transformed in
+// registers (the fused search's LS transform: RegPlan<LOG2M, 8> with the conflict-free
+// exchange layouts), multiplied by the S1 sign and summed in fp64 in code order. G and the
+// residual-variance partials are then ls_combine_q_kernel's bit for bit -- the same fp32 terms,
+// summed in the same order, and the same reduction tree (64-lane butterfly, the four 64-runs of
+// each 256-subcarrier block left to right) -- without the terms' round trip through HBM
+// (268 MB each way per C3 x 64 batch).
+template <int LOG2M, bool SC16>
+__global__ __launch_bounds__((1 << LOG2M) / 8) __attribute__((amdgpu_waves_per_eu(4)))
+void ls_window_kernel(LsArgs a) {
+  using PM = RegPlan<LOG2M, 8>;
+  constexpr int M = 1 << LOG2M, T = PM::T, NW = T / 64;
+  static_assert(T % 64 == 0, "whole waves");
+  extern __shared__ __attribute__((aligned(16))) float2 lds_raw[];
+  v2f *buf = reinterpret_cast<v2f *>(lds_raw);
+  // the |X/S1|^2 sums live in LDS after the image (thread lt's at 8 lt + e, its own entries:
+  // each thread reads and writes only them), the complex sums in registers
+  double *s2l = reinterpret_cast<double *>(lds_raw + reg_image_len<LOG2M, 8>()) + 8 * threadIdx.x;
+  __shared__ double red[M / 64];
+  const uint32_t rt = blockIdx.x, f = blockIdx.y;
+  const FrameInfo &I = a.info[f];
+  if (I.status != 0) return;
+  const uint32_t N = a.N, r = rt / N, t = rt % N, nac = a.nac;
+  const int lt = threadIdx.x, lane = lt & 63;
+  const uint32_t wv = __builtin_amdgcn_readfirstlane((uint32_t)lt >> 6);
+  const int64_t L = (int64_t)a.frame_len;
+  const auto xs = iq_row<SC16>(a.iq, a.iq_scale, ((uint64_t)I.cap * N + r) * a.stride);
+  const unsigned long long *kp = a.keys + ((uint64_t)f * N + r) * a.n_slots + 1 + t;
+  auto load_win = [&](uint32_t c, v2f *xw) {
+#ifdef LSW_ABL_NOLOAD   // timing ablation (tools/build_var.sh): no window loads
+#pragma unroll
+    for (int e = 0; e < 8; e++) xw[e] = v2f{(float)(e + c), (float)lt};
+    return;
+#endif
+    const int64_t wb = I.base + (int64_t)key_index(kp[(uint64_t)c * N]);
+    if (wb >= 0 && wb + M <= L) {                      // uniform: one row base
+      const auto xr = xs.row((uint64_t)wb);
+#pragma unroll
+      for (int e = 0; e < 8; e++) {
+        const float2 v = xr.at(reg_index<LOG2M, 8>(lt, e));
+        xw[e] = v2f{v.x, v.y};
+      }
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; e++) {
+        const int64_t n = wb + reg_index<LOG2M, 8>(lt, e);
+        const float2 v = xs.at(n < 0 ? 0 : (n >= L ? L - 1 : n));
+        xw[e] = (n >= 0 && n < L) ? v2f{v.x, v.y} : v2f{0.0f, 0.0f};
+      }
+    }
+  };
+  // the code's 8 signs of this thread, one 8-byte load (s1sign_w: [t][c][lt][e])
+  auto load_sign = [&](uint32_t c) {
+    return *reinterpret_cast<const uint2 *>(a.s1sign_w + ((size_t)t * nac + c) * M + 8 * lt);
+  };
+  v2f wm[PM::NTW > 0 ? PM::NTW : 1];
+  reg_twiddles<LOG2M, 8>(wm, a.tw, lt);
+  double sr[8], si[8];
+#pragma unroll
+  for (int e = 0; e < 8; e++) {
+    sr[e] = si[e] = 0.0;
+    s2l[e] = 0.0;
+  }
+  v2f xn[8];
+  load_win(0, xn);
+  uint2 sn = load_sign(0);
+  for (uint32_t c = 0; c < nac; c++) {
+    v2f xw[8];
+#pragma unroll
+    for (int e = 0; e < 8; e++) xw[e] = xn[e];
+    const uint2 sv = sn;
+    if (c + 1 < nac) {                                 // uniform: the next code in flight
+      load_win(c + 1, xn);
+      sn = load_sign(c + 1);
+    }
+#ifdef LSW_ABL_NOPF   // timing ablation: the next code's loads complete before this transform
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
+#ifndef LSW_ABL_NOFFT   // timing ablation: no transform
+    reg_compute<LOG2M, 8, 0, false>(xw, wm);
+    reg_rest_lay<LOG2M, 8, 1, false, true>(buf, xw, wm, lt);
+#endif
+#pragma unroll
+    for (int e = 0; e < 8; e++) {
+      // X / S1 (S1 = +-1: a product with the sign, exact; a null subcarrier's term is +0)
+      const int8_t s8 = (int8_t)(((e < 4 ? sv.x : sv.y) >> (8 * (e & 3))) & 0xFFu);
+      const float sgn = (float)s8;
+      const v2f term = s8 ? xw[e] * v2f{sgn, sgn} : v2f{0.0f, 0.0f};
+      sr[e] += (double)term.x;
+      si[e] += (double)term.y;
+      s2l[e] += (double)term.x * term.x + (double)term.y * term.y;
+    }
+  }
+  const double bias = (a.keep_bias && r == t) ? 1.0 : 0.0;
+#pragma unroll
+  for (int e = 0; e < 8; e++) {
+    const uint32_t k = (uint32_t)reg_index<LOG2M, 8>(lt, e);
+    const bool occ = a.occ_index[k] >= 0;
+    a.G[(((uint64_t)f * M + k) * N + r) * N + t] =
+        occ ? make_float2((float)((bias + sr[e]) * a.scale), (float)(si[e] * a.scale))
+            : make_float2(0.0f, 0.0f);
+    double nv = occ ? s2l[e] - (sr[e] * sr[e] + si[e] * si[e]) / (double)nac : 0.0;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) nv += __shfl_xor(nv, off);
+    // the wave's 64 subcarriers 64 wv + T e + lane: run (64 wv + T e) / 64 of the frame
+    if (lane == 0) red[(64 * wv + T * e) / 64] = nv;
+  }
+  __syncthreads();
+  for (int b = lt; b < M / 256; b += T)
+    a.nv_part[(uint64_t)f * a.n_nvp + (uint64_t)rt * (M / 256) + b] =
+        red[4 * b] + red[4 * b + 1] + red[4 * b + 2] + red[4 * b + 3];
+  (void)NW;
+}
+
+bool launch_ls_window(const LsArgs &a, int log2M, uint32_t n_frames, hipStream_t s) {
+  if (a.cfo_part || !a.s1sign_w || log2M < 9 || log2M > 12) return false;
+  if (!n_frames) return true;
+  void (*kern)(LsArgs) = nullptr;
+  size_t shm = 0;
+  int T = 0;
+  switch (log2M) {
+#define LSW(L2)                                                                             \
+  case L2:                                                                                  \
+    kern = a.sc16 ? ls_window_kernel<L2, true> : ls_window_kernel<L2, false>;               \
+    shm = sizeof(float2) * reg_image_len<L2, 8>() + sizeof(double) * (1 << L2);             \
+    T = (1 << L2) / 8;                                                                      \
+    break;
+    LSW(9) LSW(10) LSW(11) LSW(12)
+#undef LSW
+  }
+  (void)hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
+  hipLaunchKernelGGL(kern, dim3(a.N * a.N, n_frames), dim3(T), shm, s, a);
+  return true;
 }
 
 void launch_ls_combine_q(const LsArgs &a, uint32_t n_frames, hipStream_t s) {

@@ -241,20 +241,26 @@ MIMO_DEV void reg_load_lay(const v2f *buf, v2f *v, int tid) {
   }
 }
 
-// reg_rest with the exchange layouts above (images of reg_image_len entries)
-template <int LOG2N, int PTS, int P, bool INV>
+// a workgroup barrier that orders LDS only: waits for this wave's LDS accesses, not for its
+// global loads in flight (__syncthreads' release fence would drain those: a prefetch of the
+// next item's data would complete at the first exchange)
+MIMO_DEV void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// reg_rest with the exchange layouts above (images of reg_image_len entries); KEEPVM: the
+// barriers leave global loads in flight (lds_barrier)
+template <int LOG2N, int PTS, int P, bool INV, bool KEEPVM = false>
 MIMO_DEV void reg_rest_lay(v2f *buf, v2f *v, const v2f *w1, int tid) {
   using PL = RegPlan<LOG2N, PTS>;
   if constexpr (P < PL::NP) {
     int t = tid;
     asm volatile("" : "+v"(t));
     constexpr int LAY = reg_ex_layout<LOG2N, PTS>(P - 1);
-    __syncthreads();
+    if constexpr (KEEPVM) lds_barrier(); else __syncthreads();
     reg_store_lay<LOG2N, PTS, P - 1, LAY>(buf, v, t);
-    __syncthreads();
+    if constexpr (KEEPVM) lds_barrier(); else __syncthreads();
     reg_load_lay<LOG2N, PTS, P, LAY>(buf, v, t);
     reg_compute<LOG2N, PTS, P, INV>(v, w1);
-    reg_rest_lay<LOG2N, PTS, P + 1, INV>(buf, v, w1, tid);
+    reg_rest_lay<LOG2N, PTS, P + 1, INV, KEEPVM>(buf, v, w1, tid);
   }
 }
 

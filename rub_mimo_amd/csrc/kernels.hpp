@@ -68,7 +68,6 @@ struct ScArgs {
   unsigned long long *cand;
   int no_skip;
   uint32_t diag;            // diagnostics (RMIMO_SC_DIAG bits 8/16: skip in-place resolve/finalize)
-  uint32_t split_iters;     // sc_exact_kernel: workgroups per (item, antenna), 1, 2 or 4 (0 = 1)
   uint32_t *snap;           // sc_exact_kernel: copy of *hot_count (the items of this phase), or null
 };
 
@@ -168,18 +167,8 @@ struct SearchArgs {
   float2 *lsq;                     // [F][N][N][nac][M] X/S1 per access code
   uint32_t nac;
   uint32_t xcd_order;              // search_ls_kernel: slot pair slowest within each XCD
-  uint32_t fr_chunk;               // xcd_order 3: (frame, rx)s per chunk
   const double *cfo_part;          // opt-in CFO, folded: derotate the loads by stage 1 (or null)
   float *corr_trace;               // DEBUG_LOG: [F][N][n_slots][SL] every lag's metric (or null)
-  // LS combine fused into the search (search_ls_wave_kernel, no CFO): the last workgroup to
-  // store a (frame, rx, tx)'s terms sums them as ls_combine_q_kernel does (or null: off)
-  uint32_t *ls_arrive;             // [F][N][N] arrival counters, zero between launches
-  float2 *G;                       // [F][M][N][N]
-  double *nv_part;                 // [F][n_nvp] residual-variance partials, ls_combine_q's layout
-  uint32_t n_nvp;
-  const int32_t *occ_index;        // [M] -> j or -1
-  int keep_bias;
-  float ls_scale;                  // dft_normalizer / float(nac)
 };
 void launch_search(const SearchArgs &a, int log2F, uint32_t n_frames, hipStream_t s);
 // true when (log2F, log2M) has a search_ls_kernel instance (it then ran)
@@ -192,9 +181,13 @@ bool search_ls_wave_enabled();
 struct LsArgs {
   const float2 *iq;
   uint64_t stride, frame_len;
+  int sc16;                        // capture at the sc16 wire format (ls_window_kernel)
+  float iq_scale;
   uint32_t N, M, nac, n_slots;
   const unsigned long long *keys;
   const int8_t *s1sign;            // [N][nac][M]
+  const int8_t *s1sign_w;          // [N][nac][M/8][8]: sign of subcarrier lt + (M/8) e at 8 lt + e
+                                   // (ls_window_kernel's thread order, one 8-byte load per code)
   const int32_t *occ_index;        // [M] -> j or -1
   int keep_bias;
   float scale;                     // dft_normalizer / float(nac) (framing.cc:821)
@@ -212,6 +205,9 @@ struct LsArgs {
 constexpr uint32_t kLsCodesPerGroup = 4;   // access codes FFT'd per LS workgroup
 void launch_ls(const LsArgs &a, int log2M, uint32_t n_frames, hipStream_t s);
 void launch_ls_combine_q(const LsArgs &a, uint32_t n_frames, hipStream_t s);
+// the LS estimate straight from the access-code windows at the search's keys, no terms in HBM
+// (ls_window_kernel; 512 <= M <= 4096, no CFO): false when the geometry has no instance
+bool launch_ls_window(const LsArgs &a, int log2M, uint32_t n_frames, hipStream_t s);
 
 // per-subcarrier weights, framing.cc:826-831 -> 1344-1367 (+ NxN ZF/MMSE)
 struct WeightArgs {
@@ -293,8 +289,6 @@ struct DecodeArgs {
   int cpe;                         // opt-in CFO: decision-directed common-phase tracking; 2 =
                                    // folded: the kernel also derotates by the frame's estimate
   const double *cfo_part;          // folded CFO: the stage partials (cfo_stage_eps)
-  int expt;                        // diagnostics (RMIMO_DEC_EXPT): bit 0 IQ from one symbol,
-                                   // bit 1 no output stores, bit 2 weights of subcarrier 0
 };
 // returns the number of EVM partial sets written per symbol (see EvmArgs::parts), 0 when no
 // kernel takes the configuration (nothing launched: an sc16 batch the streaming kernel does not
@@ -316,9 +310,6 @@ bool decode_stream_cpe(const DecodeArgs &a);
 uint32_t launch_decode_split(const DecodeArgs &a, int log2M, uint32_t n_frames, hipStream_t s);
 // one-pass 8x8 decode by residue class (M = 4096): accepts / launches (0: not handled), and
 // the EVM records per frame it may write (rec_stride must hold them)
-bool decode_res8_accepts(const DecodeArgs &a, int log2M, uint32_t n_frames);
-uint32_t launch_decode_res8(const DecodeArgs &a, int log2M, uint32_t n_frames, hipStream_t s);
-uint32_t res8_records(uint32_t n_cu);
 bool decode_split_accepts(const DecodeArgs &a, int log2M);
 uint32_t split_group_symbols(uint32_t max_out);
 // the split decode's symbol groups, symbol ranges per (group, chunk) and EVM records per frame

@@ -1618,21 +1618,14 @@ void sc_exact_kernel(ScArgs a) {
   // the next screen phase appends after this phase's items: their count, for its exact launch
   // (the kernel boundary orders this store before the next screen's appends)
   if (a.snap && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) *a.snap = count_raw;
-  // one (antenna, iteration) of an item per workgroup, iteration fastest: an item's passes are
-  // dispatched together, ahead of the grid's empty tail. Each iteration starts from its own
-  // window sums (history of M samples), so an item's iterations run side by side instead of
-  // one after the other: the item's critical path is one iteration, not four.
-  // (a.split_iters = 0: one workgroup per antenna walks the item's iterations in turn)
-  // (a.split_iters = IT > 1: IT workgroups per antenna, workgroup itw the kScIters / IT
-  // iterations from itw kScIters / IT)
-  const uint32_t IT = a.split_iters > 1 ? a.split_iters : 1u;
-  const uint32_t s = blockIdx.x / IT;
-  const int itw = (int)(blockIdx.x % IT);
-  const int KI = kScIters / (int)IT;
+  // one (item, antenna) pass per workgroup (blockIdx.x the antenna), walking the item's unproven
+  // iterations in turn (splitting them over 2 or 4 workgroups, each with its own M-sample
+  // history setup, measured 1.5-2.2x slower: DESIGN.md)
+  const uint32_t s = blockIdx.x;
+  uint32_t slot = item0 + blockIdx.y;
   // the first slot's record is read before the count is known (it is inside the allocation
   // whatever the count, and used only if the slot is live): in phase 1 (item0 = 0) its loads
   // go out with the count's instead of one memory latency after it
-  uint32_t slot = item0 + blockIdx.y;
   const ScHot *hs = a.hot + min(slot, a.hot_cap - 1u);
   uint32_t f_n = hs->f;
   int64_t w0_n = hs->w0;
@@ -1655,21 +1648,11 @@ void sc_exact_kernel(ScArgs a) {
   int it_hi = (int)std::min<int64_t>(kScIters - 1, (fmax - w0) / kScIt);
   const auto x = iq_row<S>(a.iq, a.iq_scale, ((uint64_t)f * a.N + s) * a.stride);
   const bool vec = x.pair_ok();
-  if (tid == 0 && itw == 0) hp->lo[s] = w0 + (int64_t)it_lo * kScIt;   // first evaluated position
-  bool active = true;
-  if (IT > 1) {
-    const int k0 = itw * KI, k1 = k0 + KI - 1;        // this workgroup's iterations
-    for (int it = k0; it <= k1; it++)
-      if (it < it_lo || it > it_hi) hp->wbits[((int)s * kScIters + it) * kScT + tid] = 0;
-    it_lo = it_lo > k0 ? it_lo : k0;
-    it_hi = it_hi < k1 ? it_hi : k1;
-    active = it_lo <= it_hi;                          // uniform
-  } else {
-    for (int it = 0; it < kScIters; it++)
-      if (it < it_lo || it > it_hi) hp->wbits[((int)s * kScIters + it) * kScT + tid] = 0;
-  }
+  if (tid == 0) hp->lo[s] = w0 + (int64_t)it_lo * kScIt;   // first evaluated position
+  for (int it = 0; it < kScIters; it++)
+    if (it < it_lo || it > it_hi) hp->wbits[((int)s * kScIters + it) * kScT + tid] = 0;
   const int64_t ib_lo = w0 + (int64_t)it_lo * kScIt;
-  if (active) {
+  {
   // the first two blocks' loads, then the history [ib_lo - M, ib_lo) -> its ring slots: all in
   // flight together (the window sums below wait for the history only). Block it_lo + j goes
   // through register set j & 1 (pre, pre2): each iteration refills the set it consumed two
@@ -1944,7 +1927,7 @@ void sc_exact_kernel(ScArgs a) {
     atomicAdd(&a.prof[18], pq_walk);
     atomicAdd(&a.prof[19], pq_first);
   }
-  }   // active
+  }
   // the item's last antenna pass: plateau rule over every antenna's words
   if (a.prof && tid == 0) {
     const unsigned long long t = (unsigned long long)wall_clock64();
@@ -1963,7 +1946,7 @@ void sc_exact_kernel(ScArgs a) {
   __syncthreads();
   if (tid == 0)
     s_last = (__hip_atomic_fetch_add(&hp->arrived, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) ==
-              hp->n_done * IT - 1u) ? 1 : 0;
+              hp->n_done - 1u) ? 1 : 0;
   __syncthreads();
   if (s_last && !(a.diag & 16)) {
     // the acquire of the arrival counter (agent scope) invalidated this CU's L1: plain 16-byte
@@ -2089,9 +2072,8 @@ void launch_sc_screen(const ScreenArgs &a, uint32_t n_frames, hipStream_t s) {
   const uint64_t span = end - std::min<uint64_t>(end, a.chunk_lo * a.chunk_len);
   // positions per workgroup: 8192 up to M = 2048 (twice the workgroups; a phase-1 screen of
   // 64 C3 captures is ~830 workgroups at 16384, under one per SIMD), 16384 above (the 2D-block
-  // history, M positions, would be half of an 8192 span); RMIMO_SCR_SPAN=8192 | 16384 forces one
-  static const int span_env = [] { const char *e = getenv("RMIMO_SCR_SPAN"); return e ? atoi(e) : 0; }();
-  const int sp = span_env == 8192 ? 8192 : span_env == 16384 ? kScrSpan : a.M <= 2048 ? 8192 : kScrSpan;
+  // history, M positions, would be half of an 8192 span)
+  const int sp = a.M <= 2048 ? 8192 : kScrSpan;
   const uint32_t gx = (uint32_t)((span + sp - 1) / sp);
   if (!gx) return;
   if (sp == 8192) {
@@ -2118,8 +2100,7 @@ void launch_sc_exact(const ScArgs &a, hipStream_t s) {
                               (int)shm);
     set_shm[v] = shm;
   }
-  hipLaunchKernelGGL(kern, dim3(a.N * (a.split_iters > 1 ? a.split_iters : 1),
-                                 std::min<uint32_t>(a.hot_cap, 256)), dim3(kScT), shm, s, a);
+  hipLaunchKernelGGL(kern, dim3(a.N, std::min<uint32_t>(a.hot_cap, 256)), dim3(kScT), shm, s, a);
 }
 
 __global__ __launch_bounds__(256) void sc_trace_kernel(const float2 *iq, uint64_t stride,

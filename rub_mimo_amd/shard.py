@@ -39,11 +39,12 @@ def split_streams(n_streams, world, rank):
     return s0, s0 + base + (1 if rank < extra else 0)
 
 
-def reduce_stats(stats, elapsed, dist=None, device="cpu"):
+def reduce_stats(stats, elapsed, dist=None, device="cpu", force=False):
     """Sum the counters and take the max elapsed over ranks; identity when dist is None or the
-    group has one rank. Returns (totals dict, elapsed_max)."""
+    group has one rank (force: run the collectives at world size 1 too -- the device test of
+    the RCCL path on one GPU). Returns (totals dict, elapsed_max)."""
     if dist is None or not dist.is_available() or not dist.is_initialized() or \
-            dist.get_world_size() == 1:
+            (dist.get_world_size() == 1 and not force):
         return {k: float(stats[k]) for k in STAT_KEYS}, float(elapsed)
     import torch
     t = torch.tensor([float(elapsed)], dtype=torch.float64, device=device)
@@ -51,6 +52,14 @@ def reduce_stats(stats, elapsed, dist=None, device="cpu"):
     c = torch.tensor([float(stats[k]) for k in STAT_KEYS], dtype=torch.float64, device=device)
     dist.all_reduce(c, op=dist.ReduceOp.SUM)
     return dict(zip(STAT_KEYS, (float(v) for v in c.tolist()))), float(t.item())
+
+
+def wire_bytes(t):
+    """The tensor as the bytes RCCL moves: NCCL/RCCL point-to-point has no int16 (torch's NCCL
+    process group refuses Short tensors), so sc16 wire buffers travel as uint8 views of the same
+    memory; other dtypes pass unchanged."""
+    import torch
+    return t.view(torch.uint8) if t.dtype == torch.int16 else t
 
 
 def scatter_from_rank0(dist, src, dst, rank, world):
@@ -67,11 +76,11 @@ def scatter_from_rank0(dist, src, dst, rank, world):
         if src is None or src.shape[0] != world:
             raise ValueError("rank 0 needs src with a leading dimension of world size")
         for r in range(1, world):
-            ops.append(dist.P2POp(dist.isend, src[r], r))
+            ops.append(dist.P2POp(dist.isend, wire_bytes(src[r]), r))
     else:
         if dst is None:
             raise ValueError("ranks >= 1 need a dst tensor")
-        ops.append(dist.P2POp(dist.irecv, dst, 0))
+        ops.append(dist.P2POp(dist.irecv, wire_bytes(dst), 0))
     return dist.batch_isend_irecv(ops)
 
 
