@@ -217,6 +217,10 @@ int mimo_rx_get_sc_exact_count(mimo_rx *h, uint64_t *out);
 enum { MIMO_DECODE_NONE = 0, MIMO_DECODE_STREAM = 1, MIMO_DECODE_SPLIT = 2,
        MIMO_DECODE_SYMBOL = 3 };
 int mimo_rx_get_decode_path(const mimo_rx *h, int32_t *path);
+/* persistent grids (the streaming and split decodes) sized for n_cu CUs instead of the device's
+ * count (diagnostic: a handle whose stream is CU-masked; 0 restores the device's count). Call
+ * before the handle's first batch (captured graphs keep the grid they were captured with). */
+int mimo_rx_set_grid_cus(mimo_rx *h, uint32_t n_cu);
 /* roofline probe (diagnostic, no reference counterpart): the streaming decode's memory pattern
  * without its arithmetic -- per symbol N rows of M + 2 complex64 samples staged by LDS-DMA and
  * N x M uint8 reference indices, N x M complex64 + N x M uint8 written symbol-major, on the

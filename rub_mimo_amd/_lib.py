@@ -95,6 +95,7 @@ SIGNATURES = {
     "mimo_rx_get_stage_times": (C.c_int, [_vp, _P(C.c_double), _P(_u32)]),
     "mimo_rx_get_sc_exact_count": (C.c_int, [_vp, _P(_u64)]),
     "mimo_rx_get_decode_path": (C.c_int, [_vp, _P(_i32)]),
+    "mimo_rx_set_grid_cus": (C.c_int, [_vp, _u32]),
     "mimo_probe_decode_pattern": (C.c_int, [_vp, _u64, _u32, _u32, _u32, _u32, _u32, _u32, _vp,
                                             _vp, _vp, C.c_int, _vp, _P(C.c_float)]),
     "mimo_rx_get_cfo_mode": (C.c_int, [_vp, _P(_i32)]),

@@ -1615,6 +1615,17 @@ int mimo_rx_batch_W(mimo_rx *h, float *W, uint32_t F) {
   return MIMO_OK;
 }
 
+int mimo_rx_set_grid_cus(mimo_rx *h, uint32_t n_cu) {
+  if (!h) return fail(MIMO_ERR_ARG, "null handle");
+  int dev = 0, ncu = 0;
+  if (n_cu == 0 && hipGetDevice(&dev) == hipSuccess &&
+      hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && ncu > 0)
+    n_cu = (uint32_t)ncu;
+  if (n_cu == 0) return fail(MIMO_ERR_ARG, "no CU count");
+  h->n_cu = n_cu;
+  return MIMO_OK;
+}
+
 int mimo_rx_set_timing(mimo_rx *h, int enable) {
   if (!h) return fail(MIMO_ERR_ARG, "null handle");
   h->timer.on = enable != 0;

@@ -17,3 +17,9 @@ for v in base lsw_noload lsw_nopf lsw_nofft base; do
   python -c "
 import json; d=json.load(open('gpurun_out/r06e/b_$v.json')); st=d['stages_ms_per_step']; print('$v', 'ms %.4f'%d['ms_per_step'], ' '.join('%s %.4f'%(k,v) for k,v in st.items()))"
 done
+# the S&C exact pass's in-kernel profile at HEAD (diagnostics: per-pass timeline, slowest pass)
+RMIMO_SC_PROF=1 RMIMO_SC_COUNT=1 $T 200 python bench.py --cpu-baseline 0 --sc16-steps 0 --steps 2 --warmup 1 > gpurun_out/r06e/scprof.json 2> gpurun_out/r06e/scprof.err || { tail gpurun_out/r06e/scprof.err; exit 1; }
+grep -E "exact_prof|exact_split|sc_count" gpurun_out/r06e/scprof.err | tail -12
+# space sharing: stage times on CU-masked streams, the overlapped-step lower bound per split
+$T 400 python tools/exp_cumask.py --out gpurun_out/r06e/cumask.json > gpurun_out/r06e/cumask.txt 2>&1 || { tail gpurun_out/r06e/cumask.txt; exit 1; }
+tail -8 gpurun_out/r06e/cumask.txt
