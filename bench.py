@@ -104,6 +104,10 @@ def parse():
                     help="EVM reference: 0 decided symbols, 1 transmitted indices from HBM, "
                          "2 transmitted indices regenerated from the seed")
     ap.add_argument("--pmc-json", default=None)
+    ap.add_argument("--pipeline", type=int, default=0,
+                    help="D > 0: two receivers alternate batches, batch i's decode on D CUs "
+                         "beside batch i+1's front stages (S&C .. weights) on the other CUs "
+                         "(CU-masked HIP streams, mimo_batch.stages); 0: one serial stream")
     a = ap.parse_args()
     w = WORKLOADS[a.workload]
     for k in ("M", "cp", "streams", "nac", "pid", "qam", "snr", "detector", "frames"):
@@ -135,6 +139,27 @@ def spawn_ranks(args):
         if c != 0 and rc == 0:
             rc = c
     return rc
+
+
+def cu_masked_stream(lo, hi):
+    """A HIP stream whose kernels run on CUs [lo, hi) only (hi None: the device's count):
+    hipExtStreamCreateWithCUMask from the HIP runtime already loaded in this process (a
+    contiguous range of mask bits spreads evenly over the XCDs). Returns the raw handle."""
+    import torch
+    path = next(ln.split()[-1] for ln in open("/proc/self/maps") if "libamdhip64.so" in ln)
+    hip = ctypes.CDLL(path)
+    n = torch.cuda.get_device_properties(0).multi_processor_count
+    hi = n if hi is None else hi
+    words = (n + 31) // 32
+    mask = (ctypes.c_uint32 * words)()
+    for c in range(lo, hi):
+        mask[c // 32] |= 1 << (c % 32)
+    s = ctypes.c_void_p()
+    hip.hipExtStreamCreateWithCUMask.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_uint32,
+                                                 ctypes.POINTER(ctypes.c_uint32)]
+    if hip.hipExtStreamCreateWithCUMask(ctypes.byref(s), words, mask) != 0:
+        raise SystemExit("hipExtStreamCreateWithCUMask failed")
+    return s.value
 
 
 def decode_kernel_name(M, N, args, path=None):
@@ -379,7 +404,69 @@ def main():
         return time.perf_counter() - t0
 
     timed_scatter = args.ingest == "scatter"
-    if timed_scatter:
+    pipe_info = None
+    if args.pipeline and (timed_scatter or args.cfo or c5):
+        raise SystemExit("--pipeline: resident one-frame-per-capture batches without --cfo only")
+    if args.pipeline:
+        # ---- pipelined: handle h = i % 2 runs batch i's front half on stream sF (the CUs
+        # [D, n_cu)) and its decode half on stream sD (CUs [0, D)); batch i's decode runs
+        # beside batch i+1's front half. Events order: front(i) -> decode(i) (the handle's
+        # workspace), decode(i - 2) -> front(i) (the same handle's workspace reused)
+        D = args.pipeline
+        n_cu_dev = torch.cuda.get_device_properties(dev).multi_processor_count
+        if not 0 < D < n_cu_dev or D % 8:
+            raise SystemExit("--pipeline: D must be a multiple of 8 in (0, %d)" % n_cu_dev)
+        sF_raw, sD_raw = cu_masked_stream(D, None), cu_masked_stream(0, D)
+        sF = torch.cuda.ExternalStream(sF_raw, device=dev)
+        sD = torch.cuda.ExternalStream(sD_raw, device=dev)
+        hs = []
+        for _ in range(2):
+            r_ = Receiver(RxParams(M=M, cp_len=cp, num_streams=N, num_access_codes=nac,
+                                   pid_max=pid, detector=det, qam_order=args.qam), stream=sF_raw)
+            _lib.check(_lib.lib().mimo_rx_set_grid_cus(r_._h, D), "set_grid_cus")
+            hs.append(r_)
+        evF = [torch.cuda.Event(), torch.cuda.Event()]
+        evD = [torch.cuda.Event(), torch.cuda.Event()]
+
+        def pstep(i):
+            h = i & 1
+            if i >= 2:
+                sF.wait_event(evD[h])
+            kw = dict(max_out=pid, out_sym=out_sym, out_idx=out_idx, ref_mode=args.ref_mode,
+                      ref_idx=ref_rows if args.ref_mode == 1 else None, ref_seed=args.seed,
+                      frame_id0=frame_id0, sc16=sc16, sc16_scale=wscale, out_layout=layout)
+            hs[h].process(src, L, L, F, stream=sF_raw, stages=_lib.STAGES_FRONT, **kw)
+            evF[h].record(sF)
+            sD.wait_event(evF[h])
+            hs[h].process(src, L, L, F, stream=sD_raw, stages=_lib.STAGES_DECODE, **kw)
+            evD[h].record(sD)
+
+        torch.cuda.synchronize(dev)
+        for i in range(max(args.warmup, 2) * 2):   # every (handle, half) captured and replayed
+            pstep(i)
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for i in range(args.steps):
+            pstep(i + 2 * max(args.warmup, 2))
+        torch.cuda.synchronize(dev)
+        elapsed = time.perf_counter() - t0
+        # the serial step of the same batch on the whole chip, for the line
+        for _ in range(2):
+            step()
+        torch.cuda.synchronize(dev)
+        t1 = time.perf_counter()
+        for _ in range(args.steps):
+            step()
+        torch.cuda.synchronize(dev)
+        pipe_info = {"decode_cus": D, "front_cus": n_cu_dev - D,
+                     "serial_ms_per_step": (time.perf_counter() - t1) / args.steps * 1e3,
+                     "note": "batch i's decode (mimo_batch.stages = DECODE) on D CUs beside "
+                             "batch i+1's S&C, search, LS and weights (stages = FRONT) on the "
+                             "others; two handles alternate batches; serial_ms_per_step is the "
+                             "whole chain on the whole chip, one stream"}
+        hs[0].results(F * K)
+        del hs
+    elif timed_scatter:
         wire = make_wire()
         pipe = ScatterPipeline(dist if world > 1 else None, wire, (F, N, L, 2), torch.int16, dev,
                                rank, world)
@@ -637,6 +724,7 @@ def main():
         "decode_pattern_ms": pattern["ms"] if pattern else None,
         "decode_vs_pattern": pattern["decode_vs_pattern"] if pattern else None,
         "decode_pattern": pattern,
+        "pipeline": pipe_info,
         "cpu_baseline": cpu,
         "evm_db_delta_vs_cpu": evm_delta,
         "scan_rate_all_captures": scanned_total / elapsed,

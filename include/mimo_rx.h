@@ -167,10 +167,18 @@ typedef struct mimo_batch {
    * (one call per symbol with the N stream arrays, framing.cc:587) -- and a sequential write
    * stream per decode workgroup (fewer concurrent HBM write streams: the C3 decode ~7% faster) */
   uint32_t out_layout;
+  /* MIMO_STAGES_ALL (0): the whole receive chain. MIMO_STAGES_FRONT (1): S&C, plateau, search,
+   * LS and weights only; MIMO_STAGES_DECODE (2): the replay decode and EVM only, of the batch
+   * the same handle last ran MIMO_STAGES_FRONT on (same arguments). The two halves may run on
+   * different streams (the caller orders them with events), e.g. batch i's decode on one CU
+   * partition beside batch i+1's front stages on another handle and partition. Not with
+   * cfo_correct. */
+  uint32_t stages;
 } mimo_batch;
 
 enum { MIMO_SAMPLE_FC32 = 0, MIMO_SAMPLE_SC16 = 1 };
 enum { MIMO_LAYOUT_STREAM_MAJOR = 0, MIMO_LAYOUT_SYMBOL_MAJOR = 1 };
+enum { MIMO_STAGES_ALL = 0, MIMO_STAGES_FRONT = 1, MIMO_STAGES_DECODE = 2 };
 
 /* Positions are those a framesync started at `origin` reports (origin 0 for one frame per
  * capture): add origin for the capture sample. */

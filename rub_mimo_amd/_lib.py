@@ -24,6 +24,8 @@ FRAME_OK, FRAME_NO_SYNC, FRAME_INCOMPLETE, FRAME_RESCAN, FRAME_NONE = 0, 1, 2, 3
 DECODE_NONE, DECODE_STREAM, DECODE_SPLIT, DECODE_SYMBOL = 0, 1, 2, 3
 # mimo_batch.out_layout: [F][N][max_out][M_occ] or [F][max_out][N][M_occ]
 LAYOUT_STREAM_MAJOR, LAYOUT_SYMBOL_MAJOR = 0, 1
+# mimo_batch.stages: the whole chain, the front half (S&C .. weights) or the decode half
+STAGES_ALL, STAGES_FRONT, STAGES_DECODE = 0, 1, 2
 
 
 class RxConfig(C.Structure):
@@ -43,7 +45,7 @@ class Batch(C.Structure):
                 ("d_ref_idx", C.c_void_p), ("ref_seed", C.c_uint64), ("frame_id0", C.c_uint64),
                 ("frames_per_capture", C.c_uint32), ("ref_stride", C.c_uint32),
                 ("d_ref_starts", C.c_void_p), ("sample_format", C.c_uint32),
-                ("sc16_scale", C.c_float), ("out_layout", C.c_uint32)]
+                ("sc16_scale", C.c_float), ("out_layout", C.c_uint32), ("stages", C.c_uint32)]
 
 
 class FrameResult(C.Structure):

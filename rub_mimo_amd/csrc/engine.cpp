@@ -1387,7 +1387,7 @@ static int run_batch(mimo_rx *h, const mimo_batch *b, hipStream_t s) {
     if (fused) {
       h->cur_sc16 = 1;
       h->cur_scale = b->sc16_scale;
-    } else {
+    } else if (b->stages != MIMO_STAGES_DECODE) {
       const size_t need = (size_t)b->n_frames * h->N * b->stride;
       if (h->wide.ensure(need) != hipSuccess) return fail(MIMO_ERR_NOMEM, "sc16 widening buffer");
       hipEvent_t e = h->timer.begin(s);
@@ -1396,9 +1396,23 @@ static int run_batch(mimo_rx *h, const mimo_batch *b, hipStream_t s) {
       h->timer.end(0, e, s);     // timed with the S&C stage (one extra launch)
       if (!ok) return fail(MIMO_ERR_ARG, "sc16 widening: bad geometry");
       iq = h->wide.p;
+    } else {
+      iq = h->wide.p;            // (widened by this batch's front half)
     }
   } else if (b->sample_format != MIMO_SAMPLE_FC32) {
     return fail(MIMO_ERR_ARG, "mimo_batch.sample_format must be MIMO_SAMPLE_FC32 or _SC16");
+  }
+  const bool front = b->stages != MIMO_STAGES_DECODE, decode = b->stages != MIMO_STAGES_FRONT;
+  if (!front) {   // the decode half of a batch whose front half this handle ran last
+    const int rc = run_decode(h, iq, b->stride, slots, b->frame_len, b->max_out_syms,
+                              reinterpret_cast<float2 *>(b->d_out_sym),
+                              reinterpret_cast<uint8_t *>(b->d_out_idx), b->ref_mode,
+                              reinterpret_cast<const uint8_t *>(b->d_ref_idx), b->ref_seed,
+                              b->frame_id0, s, b->n_frames, nullptr);
+    h->cur_sc16 = 0;
+    h->cur_scale = 1.0f;
+    h->cur_layout = 0;
+    return rc;
   }
   int rc = run_sync(h, iq, b->stride, b->n_frames, b->frame_len, 0, true, s, fpc,
                     fpc > 1 ? b->d_ref_starts : nullptr, b->ref_stride, true);
@@ -1434,7 +1448,7 @@ static int run_batch(mimo_rx *h, const mimo_batch *b, hipStream_t s) {
                              h->cfo ? &ca : nullptr);
   if (!rc && h->cfo && !fold && h->search_ls)   // stage 2's data-region derotation
     launch_cfo_batch_rot2(ca, slots, s);
-  if (!rc)
+  if (!rc && decode)
     rc = run_decode(h, iq, b->stride, slots, b->frame_len, b->max_out_syms,
                     reinterpret_cast<float2 *>(b->d_out_sym),
                     reinterpret_cast<uint8_t *>(b->d_out_idx), b->ref_mode,
@@ -1466,7 +1480,7 @@ static bool same_batch(const mimo_batch &x, const mimo_batch &y) {
          x.d_ref_idx == y.d_ref_idx && x.ref_seed == y.ref_seed && x.frame_id0 == y.frame_id0 &&
          batch_fpc(&x) == batch_fpc(&y) && x.d_ref_starts == y.d_ref_starts &&
          x.ref_stride == y.ref_stride && x.sample_format == y.sample_format &&
-         x.sc16_scale == y.sc16_scale && x.out_layout == y.out_layout;
+         x.sc16_scale == y.sc16_scale && x.out_layout == y.out_layout && x.stages == y.stages;
 }
 
 int mimo_rx_process_batch(mimo_rx *h, const mimo_batch *b, void *hip_stream) {
@@ -1478,6 +1492,9 @@ int mimo_rx_process_batch(mimo_rx *h, const mimo_batch *b, void *hip_stream) {
     return fail(MIMO_ERR_ARG, "mimo_batch.out_layout must be MIMO_LAYOUT_STREAM_MAJOR or _SYMBOL_MAJOR");
   if (batch_fpc(b) > 64)
     return fail(MIMO_ERR_ARG, "frames_per_capture must be at most 64");
+  if (b->stages > MIMO_STAGES_DECODE) return fail(MIMO_ERR_ARG, "mimo_batch.stages must be 0, 1 or 2");
+  if (b->stages != MIMO_STAGES_ALL && h->cfo)
+    return fail(MIMO_ERR_UNSUPPORTED, "split stages with cfo_correct");
   // the unfolded CFO stages derotate each frame's window into one scratch capture per
   // capture: back-to-back frames' windows overlap there, so that combination is refused (the
   // folded form has no scratch)

@@ -123,8 +123,9 @@ class Receiver:
     def process(self, iq, stride, frame_len, n_frames, max_out=None, out_sym=None, out_idx=None,
                 ref_mode=0, ref_idx=None, ref_seed=0, frame_id0=0, stream=None,
                 frames_per_capture=1, ref_starts=None, ref_stride=0, sc16=False,
-                sc16_scale=None, out_layout=0):
-        """One batch (mimo_rx_process_batch). frames_per_capture > 1: every capture is a
+                sc16_scale=None, out_layout=0, stages=0):
+        """One batch (mimo_rx_process_batch). stages: _lib.STAGES_ALL, or the front half
+        (STAGES_FRONT) / decode half (STAGES_DECODE) of it (see mimo_batch.stages). frames_per_capture > 1: every capture is a
         stream of back-to-back frames, received as fresh framesyncs re-armed after each frame
         (frame slots [capture][frames_per_capture]; see include/mimo_rx.h). sc16: iq holds
         the UHD sc16 wire format (interleaved int16 I/Q), read as float(i16) * sc16_scale.
@@ -135,7 +136,7 @@ class Receiver:
                        P.pid_max if max_out is None else max_out, _ptr(out_sym), _ptr(out_idx),
                        ref_mode, _ptr(ref_idx), ref_seed, frame_id0, frames_per_capture,
                        ref_stride, _ptr(ref_starts), 1 if sc16 else 0,
-                       SC16_SCALE if sc16_scale is None else sc16_scale, out_layout)
+                       SC16_SCALE if sc16_scale is None else sc16_scale, out_layout, stages)
         check(lib().mimo_rx_process_batch(self._h, C.byref(b), stream), "process_batch")
         self._last = n_frames * max(1, frames_per_capture)
 

@@ -1530,3 +1530,56 @@ def test_capture_ring_feeds_sc16_batch():
     for x, y in zip(ra, rb):
         assert x["status"] == y["status"] and x["sync_index"] == y["sync_index"]
     assert torch.equal(sa, sb) and torch.equal(ia, ib)
+
+
+def test_split_stages_equal_whole_batch():
+    """mimo_batch.stages: the front half (S&C .. weights) then the decode half of a batch, on two
+    different streams ordered by an event, write bitwise the outputs and results of the whole
+    chain in one call (C3 geometry, symbol-major, reference rows; fc32 and sc16 read in place);
+    a decode half on the other handle of a pair leaves each handle's own batch intact."""
+    import torch
+    M, cp, N, nac, pid, qam, F = 2048, 152, 4, 20, 12, 64, 3
+    S = Synthesizer(SynthParams(M=M, cp_len=cp, num_streams=N, num_access_codes=nac, pid=pid,
+                                qam_order=qam, seed=71, snr_db=30.0))
+    L = max(S.frame_len(i) for i in range(F))
+    iq = torch.empty((F, N, L), dtype=torch.complex64, device="cuda")
+    tx = torch.empty((F, N, pid, M), dtype=torch.uint8, device="cuda")
+    S.generate(iq, L, L, F, tx_idx=tx)
+    ref_rows = tx.transpose(1, 2).contiguous()
+    scale = float(torch.view_as_real(iq).abs().max()) * 1.01 / 32767.0
+    w16 = (torch.view_as_real(iq) / scale).round_().clamp_(-32768, 32767).to(torch.int16)
+    P = RxParams(M=M, cp_len=cp, num_streams=N, num_access_codes=nac, pid_max=pid,
+                 detector=_lib.DET_MMSE, qam_order=qam)
+
+    def run(src, sc16, split):
+        rxs = [Receiver(P), Receiver(P)]
+        outs = []
+        s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+        for h, rx in enumerate(rxs):
+            y = torch.zeros((F, pid, N, M), dtype=torch.complex64, device="cuda")
+            d = torch.zeros((F, pid, N, M), dtype=torch.uint8, device="cuda")
+            kw = dict(max_out=pid, out_sym=y, out_idx=d, ref_mode=1, ref_idx=ref_rows, sc16=sc16,
+                      sc16_scale=scale, out_layout=_lib.LAYOUT_SYMBOL_MAJOR)
+            if split:
+                rx.process(src, L, L, F, stream=s1.cuda_stream, stages=_lib.STAGES_FRONT, **kw)
+                ev = torch.cuda.Event()
+                ev.record(s1)
+                s2.wait_event(ev)
+                rx.process(src, L, L, F, stream=s2.cuda_stream, stages=_lib.STAGES_DECODE, **kw)
+            else:
+                rx.process(src, L, L, F, **kw)
+            outs.append((y, d))
+        torch.cuda.synchronize()
+        return [(y.cpu(), d.cpu(), rx.results(F)) for (y, d), rx in zip(outs, rxs)]
+
+    for src, sc16 in ((iq, False), (w16, True)):
+        whole = run(src, sc16, False)
+        split = run(src, sc16, True)
+        for (y0, d0, r0), (y1, d1, r1) in zip(whole, split):
+            assert any(r["status"] == _lib.FRAME_OK for r in r0)
+            assert torch.equal(y0.view(torch.int32), y1.view(torch.int32))
+            assert torch.equal(d0, d1)
+            for a, b in zip(r0, r1):
+                assert a["status"] == b["status"] and a["sync_index"] == b["sync_index"]
+                assert a["evm_num"].tobytes() == b["evm_num"].tobytes()
+                assert np.array_equal(a["errors"], b["errors"])
