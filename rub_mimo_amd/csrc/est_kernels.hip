@@ -1418,9 +1418,10 @@ void ls_window_kernel(LsArgs a) {
   static_assert(T % 64 == 0, "whole waves");
   extern __shared__ __attribute__((aligned(16))) float2 lds_raw[];
   v2f *buf = reinterpret_cast<v2f *>(lds_raw);
-  // the |X/S1|^2 sums live in LDS after the image (thread lt's at 8 lt + e, its own entries:
-  // each thread reads and writes only them), the complex sums in registers
-  double *s2l = reinterpret_cast<double *>(lds_raw + reg_image_len<LOG2M, 8>()) + 8 * threadIdx.x;
+  // the |X/S1|^2 sums live in LDS after the image (thread lt's at e T + lt: each thread reads
+  // and writes only its own entries, lane-contiguous -- conflict-free 8-byte accesses), the
+  // complex sums in registers
+  double *s2l = reinterpret_cast<double *>(lds_raw + reg_image_len<LOG2M, 8>()) + threadIdx.x;
   __shared__ double red[M / 64];
   const uint32_t rt = blockIdx.x, f = blockIdx.y;
   const FrameInfo &I = a.info[f];
@@ -1464,7 +1465,7 @@ void ls_window_kernel(LsArgs a) {
 #pragma unroll
   for (int e = 0; e < 8; e++) {
     sr[e] = si[e] = 0.0;
-    s2l[e] = 0.0;
+    s2l[e * T] = 0.0;
   }
   v2f xn[8];
   load_win(0, xn);
@@ -1493,7 +1494,7 @@ void ls_window_kernel(LsArgs a) {
       const v2f term = s8 ? xw[e] * v2f{sgn, sgn} : v2f{0.0f, 0.0f};
       sr[e] += (double)term.x;
       si[e] += (double)term.y;
-      s2l[e] += (double)term.x * term.x + (double)term.y * term.y;
+      s2l[e * T] += (double)term.x * term.x + (double)term.y * term.y;
     }
   }
   const double bias = (a.keep_bias && r == t) ? 1.0 : 0.0;
@@ -1504,7 +1505,7 @@ void ls_window_kernel(LsArgs a) {
     a.G[(((uint64_t)f * M + k) * N + r) * N + t] =
         occ ? make_float2((float)((bias + sr[e]) * a.scale), (float)(si[e] * a.scale))
             : make_float2(0.0f, 0.0f);
-    double nv = occ ? s2l[e] - (sr[e] * sr[e] + si[e] * si[e]) / (double)nac : 0.0;
+    double nv = occ ? s2l[e * T] - (sr[e] * sr[e] + si[e] * si[e]) / (double)nac : 0.0;
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) nv += __shfl_xor(nv, off);
     // the wave's 64 subcarriers 64 wv + T e + lane: run (64 wv + T e) / 64 of the frame
