@@ -485,6 +485,28 @@ int run_sync(mimo_rx *h, const float2 *iq, uint64_t stride, uint32_t F, uint64_t
       HIPCHK(hipStreamSynchronize(s));
       fprintf(stderr, "sc_count hot_items %u (screen %d, frames %u, chunks %llu)\n", q[1],
               screen ? 1 : 0, F, (unsigned long long)nchunks);
+      static const bool items_env = [] { const char *e = getenv("RMIMO_SC_COUNT"); return e[1] == '+'; }();
+      if (items_env && screen) {   // per item: frame, chunk, unproven range and its iterations
+        const uint32_t n = std::min(q[1], hot_cap);
+        std::vector<ScHot> hv(n);
+        std::vector<unsigned long long> mn((size_t)F * nchunks), mx((size_t)F * nchunks);
+        HIPCHK(hipMemcpyAsync(hv.data(), h->hot.p, sizeof(ScHot) * n, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipMemcpyAsync(mn.data(), h->scr_min.p, sizeof(unsigned long long) * mn.size(),
+                              hipMemcpyDeviceToHost, s));
+        HIPCHK(hipMemcpyAsync(mx.data(), h->scr_max.p, sizeof(unsigned long long) * mx.size(),
+                              hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        for (uint32_t i = 0; i < n; i++) {
+          const ScHot &it = hv[i];
+          const size_t ci = (size_t)it.f * nchunks + it.chunk;
+          const long long lo = (long long)mn[ci] - it.w0, hi = (long long)mx[ci] - it.w0;
+          const long long a0 = std::max<long long>(0, (lo - (long long)h->cp - 2) / kScIterLen);
+          const long long a1 = std::min<long long>(kScSpan / kScIterLen - 1, hi / kScIterLen);
+          fprintf(stderr, "sc_item %u f %u chunk %llu w0 %lld c0 %lld unproven [%lld, %lld] (%lld) "
+                  "iterations %lld-%lld\n", i, it.f, (unsigned long long)it.chunk, (long long)it.w0,
+                  (long long)it.c0, lo, hi, hi - lo + 1, a0, a1);
+        }
+      }
     }
     h->timer.end(0, e, s);
     if (prof_env && screen) {   // diagnostics: exact-kernel timeline (wall clock, 100 MHz)
