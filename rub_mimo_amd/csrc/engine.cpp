@@ -591,17 +591,25 @@ int run_estimate(mimo_rx *h, const float2 *iq, uint64_t stride, uint32_t F, uint
   la.n_nvp = h->N * h->N * ((h->M + 255) / 256);
   la.G = h->G.p; la.nv_part = h->nvp.p; la.tw = h->tw;
   la.sc16 = h->cur_sc16; la.iq_scale = h->cur_scale;
-  // LS straight from the windows (ls_window_kernel) after a search that only finds the keys,
-  // unless the opt-in CFO rotates the LS terms between the search and the combine (or
-  // RMIMO_LS_FORM=terms: the search's fused terms and ls_combine_q_kernel, the parity tests'
-  // reference for this form)
+  // LS straight from the windows (ls_window_kernel) after a search that only finds the keys
+  // (the opt-in CFO's stage 2 between them, its residual rotating each code's term in the LS
+  // kernel), unless RMIMO_LS_FORM=terms: the search's fused terms and ls_combine_q_kernel, the
+  // parity tests' reference for this form
   static const bool ls_terms = [] { const char *e = getenv("RMIMO_LS_FORM"); return e && strcmp(e, "terms") == 0; }();
-  const bool ls_win = h->search_ls && !cfo && !ls_terms && h->log2M >= 9 && h->log2M <= 12;
+  const bool ls_win = h->search_ls && !ls_terms && h->log2M >= 9 && h->log2M <= 12 &&
+                      (!cfo || h->nac <= 256);
   if (h->search_ls && ls_win) {
     sa.xcd_order = 1;
+    sa.cfo_part = (cfo && cfo->fold) ? cfo->part : nullptr;   // folded CFO: derotating loads
     hipEvent_t e = h->timer.begin(s);
     launch_search_ls(sa, h->log2F, h->log2M, F, s);   // keys only (sa.lsq null)
     h->timer.end(2, e, s);
+    if (cfo) {   // opt-in CFO stage 2: residual from the data prefixes
+      cfo->keys = h->keys.p; cfo->n_slots = h->n_slots; cfo->rot_window = 0;
+      launch_cfo_batch(*cfo, F, 2, s);
+      la.cfo_part = cfo->part;
+      la.cfo_fold = cfo->fold;
+    }
     e = h->timer.begin(s);
     launch_ls_window(la, h->log2M, F, s);
     h->timer.end(3, e, s);

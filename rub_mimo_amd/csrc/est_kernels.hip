@@ -1410,7 +1410,16 @@ bool launch_search_ls(const SearchArgs &a, int log2F, int log2M, uint32_t n_fram
 // summed in the same order, and the same reduction tree (64-lane butterfly, the four 64-runs of
 // each 256-subcarrier block left to right) -- without the terms' round trip through HBM
 // (268 MB each way per C3 x 64 batch).
-template <int LOG2M, bool SC16>
+//   With the opt-in CFO (CFO: a.cfo_part) the fused form's two corrections are one phasor
+// sequence on the window's samples: the folded form's stage-1 derotation (the search's
+// exp(-j 2 pi nu1 n) at window sample n - base) and the stage-2 residual's rotation of the code's
+// term (exp(-j 2 pi nu2 (key + M/2)), ls_combine_q_kernel's) -- a constant per window, so it can
+// multiply the samples instead of the transform's output. Per code a start phasor tabled in LDS
+// (fp64 phase, both parts), per thread its lane's step exp(-j 2 pi nu1 lt): one complex product
+// per code and thread, then the 8-point recurrence. G agrees with the fused form to fp32
+// rounding (test_ls_window_with_cfo_equals_fused_terms). Workgroup (rx 0, tx 0) records the
+// frame's total estimate.
+template <int LOG2M, bool SC16, bool CFO>
 __global__ __launch_bounds__((1 << LOG2M) / 8) __attribute__((amdgpu_waves_per_eu(4)))
 void ls_window_kernel(LsArgs a) {
   using PM = RegPlan<LOG2M, 8>;
@@ -1432,6 +1441,31 @@ void ls_window_kernel(LsArgs a) {
   const int64_t L = (int64_t)a.frame_len;
   const auto xs = iq_row<SC16>(a.iq, a.iq_scale, ((uint64_t)I.cap * N + r) * a.stride);
   const unsigned long long *kp = a.keys + ((uint64_t)f * N + r) * a.n_slots + 1 + t;
+  __shared__ v2f s_rot[CFO ? kLsRotCodes : 1];       // CFO: code c's start phasor
+  __shared__ double s_nu1, s_nu2;
+  __shared__ v2f s_step;
+  v2f q_lt = v2f{1.0f, 0.0f};                         // CFO: exp(-j 2 pi nu1 lt)
+  if constexpr (CFO) {
+    if (lt == 0) {
+      const double nu2 = cfo_stage_eps(a.cfo_part, f, 2) / (double)M;
+      s_nu2 = nu2;
+      if (rt == 0) {   // the frame's total estimate (stage 1 + stage 2), as ls_combine_q_kernel
+        const double eps = cfo_stage_eps(a.cfo_part, f, 1) + nu2 * M;
+        const_cast<FrameInfo &>(I).cfo_eps = (float)eps;
+        const_cast<FrameInfo &>(I).cfo_E = cfo_fixed_freq(eps, M);
+      }
+      s_nu1 = a.cfo_fold ? cfo_stage_eps(a.cfo_part, f, 1) / (double)M : 0.0;
+      s_step = phasor_cycles(s_nu1 * (double)(M / 8));
+    }
+    __syncthreads();
+    const double nu1 = s_nu1, nu2 = s_nu2;
+    for (uint32_t c = lt; c < nac; c += T) {
+      const double k = (double)key_index(kp[(uint64_t)c * N]);
+      s_rot[c] = phasor_cycles(nu1 * k + nu2 * (k + 0.5 * (double)M));
+    }
+    q_lt = phasor_cycles(nu1 * (double)lt);
+    __syncthreads();
+  }
   auto load_win = [&](uint32_t c, v2f *xw) {
 #ifdef LSW_ABL_NOLOAD   // timing ablation (tools/build_var.sh): no window loads
 #pragma unroll
@@ -1453,6 +1487,17 @@ void ls_window_kernel(LsArgs a) {
         const float2 v = xs.at(n < 0 ? 0 : (n >= L ? L - 1 : n));
         xw[e] = (n >= 0 && n < L) ? v2f{v.x, v.y} : v2f{0.0f, 0.0f};
       }
+    }
+  };
+  // CFO: window sample lt + e M/8 of code c times s_rot[c] q_lt step^e (when the code's
+  // transform starts, so the prefetch is not waited for at its issue)
+  auto derotate = [&](uint32_t c, v2f *xw) {
+    v2f rb = vmul(s_rot[c], q_lt);
+    const v2f st = s_step;
+#pragma unroll
+    for (int e = 0; e < 8; e++) {
+      xw[e] = vmul(xw[e], rb);
+      rb = vmul(rb, st);
     }
   };
   // the code's 8 signs of this thread, one 8-byte load (s1sign_w: [t][c][lt][e])
@@ -1482,6 +1527,7 @@ void ls_window_kernel(LsArgs a) {
 #ifdef LSW_ABL_NOPF   // timing ablation: the next code's loads complete before this transform
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #endif
+    if constexpr (CFO) derotate(c, xw);
 #ifndef LSW_ABL_NOFFT   // timing ablation: no transform
     reg_compute<LOG2M, 8, 0, false>(xw, wm);
     reg_rest_lay<LOG2M, 8, 1, false, true>(buf, xw, wm, lt);
@@ -1519,15 +1565,18 @@ void ls_window_kernel(LsArgs a) {
 }
 
 bool launch_ls_window(const LsArgs &a, int log2M, uint32_t n_frames, hipStream_t s) {
-  if (a.cfo_part || !a.s1sign_w || log2M < 9 || log2M > 12) return false;
+  if (!a.s1sign_w || log2M < 9 || log2M > 12 || (a.cfo_part && a.nac > (uint32_t)kLsRotCodes))
+    return false;
   if (!n_frames) return true;
   void (*kern)(LsArgs) = nullptr;
   size_t shm = 0;
   int T = 0;
+  const bool cfo = a.cfo_part != nullptr;
   switch (log2M) {
 #define LSW(L2)                                                                             \
   case L2:                                                                                  \
-    kern = a.sc16 ? ls_window_kernel<L2, true> : ls_window_kernel<L2, false>;               \
+    kern = cfo ? (a.sc16 ? ls_window_kernel<L2, true, true> : ls_window_kernel<L2, false, true>) \
+               : (a.sc16 ? ls_window_kernel<L2, true, false> : ls_window_kernel<L2, false, false>); \
     shm = sizeof(float2) * reg_image_len<L2, 8>() + sizeof(double) * (1 << L2);             \
     T = (1 << L2) / 8;                                                                      \
     break;

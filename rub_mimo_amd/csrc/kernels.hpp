@@ -201,12 +201,15 @@ struct LsArgs {
   const float2 *lsq;               // search_ls_kernel's X/S1 terms (ls_combine_q_kernel)
   const double *cfo_part;          // opt-in CFO: rotate code c's term by the stage-2 residual
   uint32_t M_cfo;                  // (M, window-relative; null: off)
+  int cfo_fold;                    // ls_window_kernel with CFO: derotate the window loads by the
+                                   // stage-1 estimate too (folded CFO; else the capture is)
 };
 constexpr uint32_t kLsCodesPerGroup = 4;   // access codes FFT'd per LS workgroup
 void launch_ls(const LsArgs &a, int log2M, uint32_t n_frames, hipStream_t s);
 void launch_ls_combine_q(const LsArgs &a, uint32_t n_frames, hipStream_t s);
 // the LS estimate straight from the access-code windows at the search's keys, no terms in HBM
-// (ls_window_kernel; 512 <= M <= 4096, no CFO): false when the geometry has no instance
+// (ls_window_kernel; 512 <= M <= 4096, CFO with nac <= 256): false when the geometry has no
+// instance
 bool launch_ls_window(const LsArgs &a, int log2M, uint32_t n_frames, hipStream_t s);
 
 // per-subcarrier weights, framing.cc:826-831 -> 1344-1367 (+ NxN ZF/MMSE)

@@ -656,6 +656,72 @@ def test_ls_window_equals_fused_terms():
             assert evm_delta(y, o["y"]) <= 1e-5, c
 
 
+
+def _cfo_ls_outputs(mode, seed=813, eps=0.3):
+    """A C3-geometry batch (4 captures, 24 data symbols) rotated by eps subcarrier spacings
+    through the opt-in CFO path ("fold": reference indices from HBM, the derotating loads;
+    "scratch": ref_mode 2, the stage-1 scratch capture): G, W, noise variances, EVM sums and the
+    frames' CFO estimates."""
+    import torch
+    from rub_mimo_amd.receiver import cfo_derotate
+    M, cp, N, nac, pid, qam, F = 2048, 152, 4, 20, 24, 64, 4
+    sp = SynthParams(M=M, cp_len=cp, num_streams=N, num_access_codes=nac, pid=pid,
+                     qam_order=qam, seed=seed, snr_db=30.0)
+    S = Synthesizer(sp)
+    L = sp.max_frame_len()
+    iq = torch.empty((F, N, L), dtype=torch.complex64, device="cuda")
+    tx = torch.empty((F, N, pid, M), dtype=torch.uint8, device="cuda")
+    S.generate(iq, L, L, F, tx_idx=tx)
+    cfo_derotate(iq, L, F * N, L, 0, -eps, M)
+    rxo = Receiver(RxParams(M=M, cp_len=cp, num_streams=N, num_access_codes=nac, pid_max=pid,
+                            detector=_lib.DET_MMSE, qam_order=qam, cfo_correct=True))
+    if mode == "fold":
+        rxo.process(iq, L, L, F, max_out=pid, ref_mode=1, ref_idx=tx)
+    else:
+        rxo.process(iq, L, L, F, max_out=pid, ref_mode=2, ref_seed=seed, frame_id0=0)
+    torch.cuda.synchronize()
+    res = rxo.results()
+    ok = np.array([r["status"] == _lib.FRAME_OK for r in res])
+    nv = np.array([r["noise_var"] for r in res], np.float64)
+    ev = np.array([[r["evm_num"], r["evm_den"]] for r in res], np.float64)
+    ce = np.array([r["cfo_eps"] for r in res], np.float64)
+    G, W = rxo.G(), rxo.W()
+    G[~ok] = 0
+    W[~ok] = 0
+    return G, W, nv, ev, ce, ok
+
+
+@pytest.mark.parametrize("mode", ["fold", "scratch"])
+def test_ls_window_with_cfo_equals_fused_terms(mode):
+    """With the opt-in CFO the default LS is ls_window_kernel too: the folded form's stage-1
+    derotation of the window and the stage-2 residual's rotation of the code's term (a constant
+    per window) are applied as one phasor sequence to the window's samples before the transform.
+    Against the fused-terms form (RMIMO_LS_FORM=terms in a child: the search's derotated terms,
+    rotated in fp64 and summed by ls_combine_q_kernel): G, W, noise variances and EVM sums to
+    fp32 rounding, the CFO estimates (recorded by the LS kernel of either form) equal."""
+    import subprocess
+    import sys
+    import tempfile
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    with tempfile.TemporaryDirectory() as td:
+        code = ("import sys; sys.path.insert(0, %r); sys.path.insert(0, %r)\n"
+                "import numpy as np, test_gpu as t\n"
+                "G, W, nv, ev, ce, ok = t._cfo_ls_outputs(%r)\n"
+                "np.savez(%r + '/o.npz', G=G, W=W, nv=nv, ev=ev, ce=ce, ok=ok)\n"
+                "print('terms ok')\n" % (root, os.path.join(root, "tests"), mode, td))
+        env = dict(os.environ, RMIMO_LS_FORM="terms")
+        out = subprocess.run([sys.executable, "-c", code], env=env, cwd=root, timeout=150,
+                             capture_output=True, text=True)
+        assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-4000:]
+        G, W, nv, ev, ce, ok = _cfo_ls_outputs(mode)
+        o = np.load(os.path.join(td, "o.npz"))
+    assert ok.sum() >= 2 and np.array_equal(ok, o["ok"])
+    assert np.array_equal(ce, o["ce"]) and np.all(np.abs(ce[ok] - 0.3) < 2e-5)
+    assert np.abs(G - o["G"]).max() <= 2e-6 * np.abs(o["G"]).max()
+    assert np.abs(W - o["W"]).max() <= 1e-5 * np.abs(o["W"]).max()
+    assert np.allclose(nv, o["nv"], rtol=1e-5, atol=0)
+    assert np.allclose(ev, o["ev"], rtol=1e-5, atol=0)
+
 def _sctype(M, kind):
     """None (the default allocation), "liquid" (guard bands and pilots) or "all" (every
     subcarrier a data carrier)."""
