@@ -118,41 +118,44 @@ __global__ __launch_bounds__(kCfoThreads) void cfo_batch_est_kernel(CfoBatchArgs
       }
     }
   } else if (live) {
-    // the block's symbols sym = b + kCfoBlocks j, every antenna, the prefix interiors: thread n
-    // takes sample n of each (symbol, antenna) run (runs are uniform, so no per-item division),
-    // U runs at a time with all 2U loads issued before the sums (a symbol-by-symbol loop waited
-    // one memory latency per symbol and antenna)
+    // the block's symbols sym = b + kCfoBlocks j, every antenna, the prefix interiors: the
+    // block's (run, sample) pairs -- run p = (symbol j, antenna r), sample n < inner --
+    // flattened over the threads (a thread per sample of one run left 256 - inner lanes idle),
+    // U pairs per thread with all 2U loads issued before the sums
     const uint32_t inner = a.cp > 2 * kCfoMargin ? a.cp - 2 * kCfoMargin : 0;
     const int64_t d0 = I.base + cfo_i0(a, f);               // data symbol 0's prefix
     // (the reads stay inside the framesync's window, as the reference's ring holds it: the
     // capture may hold more, the window does not)
     const int64_t wend = std::min<int64_t>(L, I.base + (int64_t)a.win);
     const uint32_t nsym = a.n_data > b ? (a.n_data - b + kCfoBlocks - 1) / kCfoBlocks : 0u;
-    const uint32_t runs = nsym * a.N;
+    const uint32_t items = nsym * a.N * inner;
+    const float inv_inner = inner ? 1.0f / (float)inner : 0.0f;
     const float2 *cap = src + (uint64_t)I.cap * a.N * a.stride;
     constexpr int U = 8;
-    for (uint32_t n0 = 0; n0 < inner; n0 += kCfoThreads) {
-      const uint32_t n = n0 + threadIdx.x;
-      for (uint32_t p0 = 0; p0 < runs; p0 += U) {
-        float2 u[U], v[U];
-        bool ok[U];
+    for (uint32_t g0 = 0; g0 < items; g0 += U * kCfoThreads) {
+      float2 u[U], v[U];
+      bool ok[U];
 #pragma unroll
-        for (int e = 0; e < U; e++) {
-          const uint32_t p = p0 + (uint32_t)e;          // uniform: run (symbol, antenna)
-          const uint32_t js = p / a.N, r = p % a.N;
-          const int64_t k = d0 + (int64_t)(b + js * kCfoBlocks) * a.SL + kCfoMargin + n;
-          ok[e] = p < runs && n < inner && k >= 0 && k + a.M < wend;
-          const float2 *row = cap + (uint64_t)(p < runs ? r : 0u) * a.stride;
-          const int64_t kk = ok[e] ? k : 0;
-          u[e] = row[kk];
-          v[e] = row[kk + (ok[e] ? a.M : 0)];
-        }
+      for (int e = 0; e < U; e++) {
+        const uint32_t g = g0 + (uint32_t)e * kCfoThreads + threadIdx.x;
+        // p = g / inner, n = g % inner (the fp32 quotient is within one of it: corrected)
+        int32_t p = (int32_t)((float)g * inv_inner);
+        int32_t n = (int32_t)g - p * (int32_t)inner;
+        if (n >= (int32_t)inner) { p++; n -= (int32_t)inner; }
+        if (n < 0) { p--; n += (int32_t)inner; }
+        const uint32_t js = (uint32_t)p / a.N, r = (uint32_t)p % a.N;
+        const int64_t k = d0 + (int64_t)(b + js * kCfoBlocks) * a.SL + kCfoMargin + n;
+        ok[e] = g < items && k >= 0 && k + a.M < wend;
+        const float2 *row = cap + (uint64_t)(g < items ? r : 0u) * a.stride;
+        const int64_t kk = ok[e] ? k : 0;
+        u[e] = row[kk];
+        v[e] = row[kk + (ok[e] ? a.M : 0)];
+      }
 #pragma unroll
-        for (int e = 0; e < U; e++) {
-          if (!ok[e]) continue;
-          re += (double)u[e].x * v[e].x + (double)u[e].y * v[e].y;
-          im += (double)u[e].x * v[e].y - (double)u[e].y * v[e].x;
-        }
+      for (int e = 0; e < U; e++) {
+        if (!ok[e]) continue;
+        re += (double)u[e].x * v[e].x + (double)u[e].y * v[e].y;
+        im += (double)u[e].x * v[e].y - (double)u[e].y * v[e].x;
       }
     }
   }
