@@ -422,8 +422,8 @@ int run_sync(mimo_rx *h, const float2 *iq, uint64_t stride, uint32_t F, uint64_t
     launch_fill(fa, s);   // trigger words, queue heads and screen flags in one launch
     static const bool prof_env = [] { const char *e = getenv("RMIMO_SC_PROF"); return e && e[0] == '1'; }();
     if (prof_env) {
-      if (!h->sc_prof.p) HIPCHK(h->sc_prof.ensure(28));
-      HIPCHK(hipMemsetAsync(h->sc_prof.p, 0, 28 * sizeof(unsigned long long), s));
+      if (!h->sc_prof.p) HIPCHK(h->sc_prof.ensure(32));
+      HIPCHK(hipMemsetAsync(h->sc_prof.p, 0, 32 * sizeof(unsigned long long), s));
       HIPCHK(hipMemsetAsync(h->sc_prof.p + 8, 0xFF, sizeof(unsigned long long), s));
       if (screen) HIPCHK(hipMemsetAsync(h->sc_prof.p, 0xFF, sizeof(unsigned long long), s));
       a.prof = h->sc_prof.p;
@@ -510,7 +510,7 @@ int run_sync(mimo_rx *h, const float2 *iq, uint64_t stride, uint32_t F, uint64_t
     }
     h->timer.end(0, e, s);
     if (prof_env && screen) {   // diagnostics: exact-kernel timeline (wall clock, 100 MHz)
-      unsigned long long v[28];
+      unsigned long long v[32];
       HIPCHK(hipMemcpyAsync(v, h->sc_prof.p, sizeof(v), hipMemcpyDeviceToHost, s));
       HIPCHK(hipStreamSynchronize(s));
       fprintf(stderr, "exact_prof passes %llu last_pass_end %.2f us finalize_end %.2f us "
@@ -532,6 +532,8 @@ int run_sync(mimo_rx *h, const float2 *iq, uint64_t stride, uint32_t F, uint64_t
               (double)(v[25] - v[0]) / 100.0, v[23] ? v[16] / (double)v[23] / 100.0 : 0.0,
               v[23] ? v[17] / (double)v[23] / 100.0 : 0.0, v[23] ? v[18] / (double)v[23] / 100.0 : 0.0,
               v[19] / np / 100.0, v[24]);
+      fprintf(stderr, "exact_windows max per iteration %llu, iterations with >= 2 windows %llu "
+              "(their passes' max duration %.2f us)\n", v[27], v[28], (double)v[29] / 100.0);
     } else if (prof_env) {   // diagnostics: per-item cycle split of the S&C kernel
       unsigned long long v[20];
       HIPCHK(hipMemcpyAsync(v, h->sc_prof.p, sizeof(v), hipMemcpyDeviceToHost, s));

@@ -1638,6 +1638,7 @@ void sc_exact_kernel(ScArgs a) {
   if (a.prof && tid == 0) atomicMin(&a.prof[0], t_item);
   unsigned long long t_res = 0;
   uint32_t n_win = 0, n_smp = 0;   // diagnostics: resolve windows and samples of this pass
+  bool multi_win = false;          // diagnostics: an iteration of this pass had >= 2 windows
   const uint32_t f = f_n;
   const int64_t L = (int64_t)a.frame_len;
   const int64_t w0 = w0_n;
@@ -1857,6 +1858,7 @@ void sc_exact_kernel(ScArgs a) {
     }
     const int namb = (a.diag & 8) ? 0 : min(s_namb, kLocAmb);          // uniform
     const unsigned long long t_r0 = a.prof ? (unsigned long long)wall_clock64() : 0ull;
+    const uint32_t n_win0 = n_win;
     if (namb > 0) {
       // exact fp32 recompute of this iteration's near-threshold samples (the oracle's chains,
       // as resolve_window): ascending order, then windows of <= kResSpread positions; per
@@ -1916,6 +1918,13 @@ void sc_exact_kernel(ScArgs a) {
       if (tid == 0) s_namb = 0;
       if (a.prof) t_res += (unsigned long long)wall_clock64() - t_r0;
     }
+    if (a.prof && tid == 0 && n_win > n_win0) {   // diagnostics: windows of this iteration
+      atomicMax(&a.prof[27], (unsigned long long)(n_win - n_win0));
+      if (n_win - n_win0 >= 2) {
+        atomicAdd(&a.prof[28], 1ull);
+        multi_win = true;
+      }
+    }
     Pc_re += tot[0]; Pc_im += tot[1]; Zc += tot[2]; Cc += tot[3]; Ac = Aend;
     hp->wbits[((int)s * kScIters + it) * kScT + tid] = (uint16_t)bits;
     __syncthreads();   // every lane's phase B reads of the ring precede the next block's writes
@@ -1940,6 +1949,7 @@ void sc_exact_kernel(ScArgs a) {
     atomicMax(&a.prof[13], (dur << 32) | ((unsigned long long)(it_hi - it_lo + 1) << 24) |
                                (t_res & 0xFFFFFFull));
     atomicMax(&a.prof[14], ((unsigned long long)n_win << 32) | n_smp);
+    if (multi_win) atomicMax(&a.prof[29], dur);
     atomicAdd(&a.prof[15], (unsigned long long)n_smp);
   }
   __threadfence();
