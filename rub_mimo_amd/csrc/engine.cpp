@@ -613,7 +613,8 @@ int run_estimate(mimo_rx *h, const float2 *iq, uint64_t stride, uint32_t F, uint
       la.cfo_fold = cfo->fold;
     }
     e = h->timer.begin(s);
-    launch_ls_window(la, h->log2M, F, s);
+    if (!launch_ls_window(la, h->log2M, F, s))   // (ls_win admits only what it launches)
+      return fail(MIMO_ERR_UNSUPPORTED, "ls_window_kernel: no instance for this geometry");
     h->timer.end(3, e, s);
   } else if (h->search_ls) {
     // search of slot pairs with the LS terms fused in, then the fixed-order LS combine
