@@ -1876,12 +1876,18 @@ void sc_exact_kernel(ScArgs a) {
         while (e < namb && s_sorted[e] - nmin < kResSpread) e++;
         const int64_t q0 = nmin - M + 1;              // table index i <-> position q0 + i
         const int W = (int)(s_sorted[e - 1] - nmin) + M;
+        // ring slots of positions q0 + i and q0 + i - RL: one 64-bit remainder per window, then
+        // a conditional wrap per entry (i < W < RING) -- a remainder per entry was ~2 us
+        const int sq = ring_slot(q0, w0, M, RING);
+        const int sqd = sq >= RL ? sq - RL : sq - RL + RING;
         for (int i = tid; i < W; i += kScT) {
-          const float2 vv = ring[ring_pad(ring_slot(q0 + i, w0, M, RING))];
+          const int sl = sq + i < RING ? sq + i : sq + i - RING;
+          const float2 vv = ring[ring_pad(sl)];
           const float z = vv.x * vv.x + vv.y * vv.y;
           rtz[i] = 0.5f * z;
           if (i >= RL) {
-            const float2 dv = ring[ring_pad(ring_slot(q0 + i - RL, w0, M, RING))];
+            const int sd = sqd + i < RING ? sqd + i : sqd + i - RING;
+            const float2 dv = ring[ring_pad(sd)];
             const float2 pp = cj_mul(dv, vv);
             rtp[i - RL] = make_float2((-1.0f) * pp.x, (-1.0f) * pp.y);
           }
