@@ -576,14 +576,24 @@ void search_ls_wave_kernel(SearchArgs a) {
   reg_twiddles<10, 16>(w1, a.tw, lane);
   if (tid == 0) { s_key[0] = 0ull; s_key[1] = 0ull; }
   // radix-B block pass (forward): DFT_B over rr, twiddle W_F^{nq}, c_q[n] -> region q
+  // (W_F^{n_i} of the thread's n_i read once: the inverse block passes use its conjugate --
+  // the same table entry twiddle<true> reads -- instead of reading it again per slot, one L2
+  // round trip exposed before each slot's recombination)
+  // (held at F = 8192, two per thread; at F = 2048, eight per thread, they would spill)
   v2f *rg = buf + wq * RB;                             // this wave's region
+  constexpr bool TW_ONCE = LOG2F == 13;             // (B = 8: two per thread)
+  v2f wfb[TW_ONCE ? NB : 1];
+  if constexpr (TW_ONCE) {
+#pragma unroll
+    for (int i = 0; i < NB; i++) wfb[i] = twiddle<false>(a.tw, (tid + T * i) * (kTwN / F));
+  }
   if constexpr (B > 1) {
 #pragma unroll
     for (int i = 0; i < NB; i++) {
       dft_small<B, false>(v + i * B);
       const int n = tid + T * i;
       v2f w[B > 1 ? B : 2];
-      twiddle_powers<B>(w, twiddle<false>(a.tw, n * (kTwN / F)));
+      twiddle_powers<B>(w, TW_ONCE ? wfb[TW_ONCE ? i : 0] : twiddle<false>(a.tw, n * (kTwN / F)));
 #pragma unroll
       for (int q = 1; q < B; q++) v[i * B + q] = vmul(v[i * B + q], w[q]);
 #pragma unroll
@@ -598,14 +608,43 @@ void search_ls_wave_kernel(SearchArgs a) {
   reg_compute<10, 16, 0, false>(v, w1);
   wave1024_rest<false>(rg, v, w1, lane);
 #endif
+  // both slots' code spectra in one round of loads: slot s0's product into v, slot s0 + 1's
+  // into X (the forward spectrum is not needed after), instead of one L2 round trip per slot
+  // (at F = 8192 only: the CFO variant, with its derotation state live, and the other
+  // transform sizes would spill -- one round per slot there)
+  constexpr bool CSP_PAIR = !CFO && LOG2F == 13;
+  if constexpr (!CSP_PAIR) {
 #pragma unroll
-  for (int e = 0; e < 16; e++) X[e] = v[e];
+    for (int e = 0; e < 16; e++) X[e] = v[e];
+  } else {
+    const v2f *__restrict__ csp0 =
+        reinterpret_cast<const v2f *>(a.codespec_w + (size_t)s0 * F) + wq * 1024 + lane;
+    const v2f *__restrict__ csp1 =
+        reinterpret_cast<const v2f *>(a.codespec_w + (size_t)(s0 + ns - 1) * F) + wq * 1024 + lane;
+    v2f c1[16];
+#pragma unroll
+    for (int e = 0; e < 16; e++) {
+      X[e] = v[e];
+      c1[e] = csp1[64 * e];
+      v[e] = csp0[64 * e];
+    }
+#pragma unroll
+    for (int e = 0; e < 16; e++) {
+      v[e] = vmulc(X[e], v[e]);
+      X[e] = vmulc(X[e], c1[e]);
+    }
+  }
   for (uint32_t u = 0; u < ns; u++) {                 // uniform
     const uint32_t slot = s0 + u;
-    const v2f *__restrict__ csp =
-        reinterpret_cast<const v2f *>(a.codespec_w + (size_t)slot * F) + wq * 1024 + lane;
+    if constexpr (!CSP_PAIR) {
+      const v2f *__restrict__ csp =
+          reinterpret_cast<const v2f *>(a.codespec_w + (size_t)slot * F) + wq * 1024 + lane;
 #pragma unroll
-    for (int e = 0; e < 16; e++) v[e] = vmulc(X[e], csp[64 * e]);
+      for (int e = 0; e < 16; e++) v[e] = vmulc(X[e], csp[64 * e]);
+    } else if (u) {
+#pragma unroll
+      for (int e = 0; e < 16; e++) v[e] = X[e];
+    }
 #ifndef SL_ABL_NOINV   // timing ablation: no inverse sub-transforms
     reg_compute<10, 16, 0, true>(v, w1);
     wave1024_rest<true>(rg, v, w1, lane);
@@ -617,14 +656,15 @@ void search_ls_wave_kernel(SearchArgs a) {
       __syncthreads();
 #pragma unroll
       for (int i = 0; i < NB; i++) {
-        // an opaque copy per use: the twiddle reads are issued here, not hoisted out of the
-        // slot loop and held in registers across it
+        // (no held twiddle: an opaque copy per use, so the reads are issued here and not
+        // hoisted out of the slot loop into registers held across it)
         int n = tid + T * i;
-        asm volatile("" : "+v"(n));
+        if constexpr (!TW_ONCE) asm volatile("" : "+v"(n));
 #pragma unroll
         for (int q = 0; q < B; q++) v[i * B + q] = buf[q * RB + lds_pad(n)];
         v2f w[B > 1 ? B : 2];
-        twiddle_powers<B>(w, twiddle<true>(a.tw, n * (kTwN / F)));
+        twiddle_powers<B>(w, TW_ONCE ? v2f{wfb[TW_ONCE ? i : 0].x, -wfb[TW_ONCE ? i : 0].y}
+                                     : twiddle<true>(a.tw, n * (kTwN / F)));
 #pragma unroll
         for (int q = 1; q < B; q++) v[i * B + q] = vmul(v[i * B + q], w[q]);
         dft_small<B, true>(v + i * B);
