@@ -555,9 +555,8 @@ void search_ls_wave_kernel(SearchArgs a) {
         if (n < 0 || n >= L) v[i * B + rr] = v2f{0.0f, 0.0f};
       }
   }
-  double nu = 0.0;                                    // CFO: eps0 / M, cycles per sample
-  if constexpr (CFO) {
-    nu = cfo_search_setup(cfo_lds, a.cfo_part, f, M, (double)T, 1024.0, (double)(M / 8));
+  if constexpr (CFO) {   // eps0 / M, cycles per sample (kept in cfo_lds.nu)
+    const double nu = cfo_search_setup(cfo_lds, a.cfo_part, f, M, (double)T, 1024.0, (double)(M / 8));
     // sample n_i + 1024 rr, n_i = tid + T i, relative to base: SL s0 + n_i + 1024 rr
     v2f ri = phasor_cycles32(nu * (double)((int64_t)a.SL * s0 + tid));
     const v2f sa = cfo_lds.step[0], sb = cfo_lds.step[1];
@@ -748,7 +747,8 @@ void search_ls_wave_kernel(SearchArgs a) {
       }
     }
     if constexpr (CFO) {   // window sample lt + e M/8, relative to base: wb - base + ...
-      v2f rb = phasor_cycles32(nu * (double)(wb - I.base + (int64_t)lt));
+      // (nu from LDS, not a register held across the search: fewer spills at F = 2048)
+      v2f rb = phasor_cycles32(cfo_lds.nu * (double)(wb - I.base + (int64_t)lt));
       const v2f st = cfo_lds.step[2];
 #pragma unroll
       for (int e = 0; e < 8; e++) {
@@ -788,7 +788,7 @@ void search_ls_wave_kernel(SearchArgs a) {
       const bool ok = (uu ? valid1 : valid0) && n >= 0 && n < L;
       win[e] = ok ? xs.at(n) : make_float2(0.0f, 0.0f);
       if constexpr (CFO) {
-        const v2f ph = phasor_cycles(nu * (double)(n - I.base));
+        const v2f ph = phasor_cycles(cfo_lds.nu * (double)(n - I.base));
         const v2f w = vmul(v2f{win[e].x, win[e].y}, ph);
         win[e] = make_float2(w.x, w.y);
       }
