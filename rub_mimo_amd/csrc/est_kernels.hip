@@ -1467,9 +1467,10 @@ void ls_window_kernel(LsArgs a) {
   static_assert(T % 64 == 0, "whole waves");
   extern __shared__ __attribute__((aligned(16))) float2 lds_raw[];
   v2f *buf = reinterpret_cast<v2f *>(lds_raw);
-  // the |X/S1|^2 sums live in LDS after the image (thread lt's at e T + lt: each thread reads
-  // and writes only its own entries, lane-contiguous -- conflict-free 8-byte accesses), the
-  // complex sums in registers
+  // the |X/S1|^2 sums in registers up to M = 2048 (124 VGPRs; an LDS read-modify-write per
+  // term cost 7 us of the kernel's 100); at M = 4096 they would spill and live in LDS after
+  // the image (thread lt's at e T + lt: lane-contiguous, conflict-free 8-byte accesses)
+  constexpr bool S2REG = LOG2M <= 11;
   double *s2l = reinterpret_cast<double *>(lds_raw + reg_image_len<LOG2M, 8>()) + threadIdx.x;
   __shared__ double red[M / 64];
   const uint32_t rt = blockIdx.x, f = blockIdx.y;
@@ -1546,11 +1547,12 @@ void ls_window_kernel(LsArgs a) {
   };
   v2f wm[PM::NTW > 0 ? PM::NTW : 1];
   reg_twiddles<LOG2M, 8>(wm, a.tw, lt);
-  double sr[8], si[8];
+  double sr[8], si[8], s2r[S2REG ? 8 : 1];
 #pragma unroll
   for (int e = 0; e < 8; e++) {
     sr[e] = si[e] = 0.0;
-    s2l[e * T] = 0.0;
+    if constexpr (S2REG) s2r[e] = 0.0;
+    else s2l[e * T] = 0.0;
   }
   v2f xn[8];
   load_win(0, xn);
@@ -1580,7 +1582,8 @@ void ls_window_kernel(LsArgs a) {
       const v2f term = s8 ? xw[e] * v2f{sgn, sgn} : v2f{0.0f, 0.0f};
       sr[e] += (double)term.x;
       si[e] += (double)term.y;
-      s2l[e * T] += (double)term.x * term.x + (double)term.y * term.y;
+      if constexpr (S2REG) s2r[e] += (double)term.x * term.x + (double)term.y * term.y;
+      else s2l[e * T] += (double)term.x * term.x + (double)term.y * term.y;
     }
   }
   const double bias = (a.keep_bias && r == t) ? 1.0 : 0.0;
@@ -1591,7 +1594,8 @@ void ls_window_kernel(LsArgs a) {
     a.G[(((uint64_t)f * M + k) * N + r) * N + t] =
         occ ? make_float2((float)((bias + sr[e]) * a.scale), (float)(si[e] * a.scale))
             : make_float2(0.0f, 0.0f);
-    double nv = occ ? s2l[e * T] - (sr[e] * sr[e] + si[e] * si[e]) / (double)nac : 0.0;
+    const double s2 = S2REG ? s2r[S2REG ? e : 0] : s2l[e * T];
+    double nv = occ ? s2 - (sr[e] * sr[e] + si[e] * si[e]) / (double)nac : 0.0;
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) nv += __shfl_xor(nv, off);
     // the wave's 64 subcarriers 64 wv + T e + lane: run (64 wv + T e) / 64 of the frame
@@ -1617,7 +1621,7 @@ bool launch_ls_window(const LsArgs &a, int log2M, uint32_t n_frames, hipStream_t
   case L2:                                                                                  \
     kern = cfo ? (a.sc16 ? ls_window_kernel<L2, true, true> : ls_window_kernel<L2, false, true>) \
                : (a.sc16 ? ls_window_kernel<L2, true, false> : ls_window_kernel<L2, false, false>); \
-    shm = sizeof(float2) * reg_image_len<L2, 8>() + sizeof(double) * (1 << L2);             \
+    shm = sizeof(float2) * reg_image_len<L2, 8>() + (L2 > 11 ? sizeof(double) * (1 << L2) : 0); \
     T = (1 << L2) / 8;                                                                      \
     break;
     LSW(9) LSW(10) LSW(11) LSW(12)
