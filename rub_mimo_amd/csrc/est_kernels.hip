@@ -1472,6 +1472,8 @@ void ls_window_kernel(LsArgs a) {
   // the image (thread lt's at e T + lt: lane-contiguous, conflict-free 8-byte accesses)
   constexpr bool S2REG = LOG2M <= 11;
   double *s2l = reinterpret_cast<double *>(lds_raw + reg_image_len<LOG2M, 8>()) + threadIdx.x;
+  // (up to M = 2048 the LDS the sums left holds a second transform image instead)
+  v2f *pa = buf, *pb = buf + reg_image_len<LOG2M, 8>();
   __shared__ double red[M / 64];
   const uint32_t rt = blockIdx.x, f = blockIdx.y;
   const FrameInfo &I = a.info[f];
@@ -1572,7 +1574,16 @@ void ls_window_kernel(LsArgs a) {
     if constexpr (CFO) derotate(c, xw);
 #ifndef LSW_ABL_NOFFT   // timing ablation: no transform
     reg_compute<LOG2M, 8, 0, false>(xw, wm);
-    reg_rest_lay<LOG2M, 8, 1, false, true>(buf, xw, wm, lt);
+    if constexpr (S2REG) {   // two images in turn, one barrier per exchange
+      reg_rest_pp<LOG2M, 8, 1, false>(pa, pb, xw, wm, lt);
+      if constexpr ((PM::NP - 1) & 1) {   // the next code starts on the image not used last
+        v2f *tmp = pa;
+        pa = pb;
+        pb = tmp;
+      }
+    } else {
+      reg_rest_lay<LOG2M, 8, 1, false, true>(buf, xw, wm, lt);
+    }
 #endif
 #pragma unroll
     for (int e = 0; e < 8; e++) {
@@ -1621,7 +1632,8 @@ bool launch_ls_window(const LsArgs &a, int log2M, uint32_t n_frames, hipStream_t
   case L2:                                                                                  \
     kern = cfo ? (a.sc16 ? ls_window_kernel<L2, true, true> : ls_window_kernel<L2, false, true>) \
                : (a.sc16 ? ls_window_kernel<L2, true, false> : ls_window_kernel<L2, false, false>); \
-    shm = sizeof(float2) * reg_image_len<L2, 8>() + (L2 > 11 ? sizeof(double) * (1 << L2) : 0); \
+    shm = sizeof(float2) * reg_image_len<L2, 8>() *                                          \
+              (L2 > 11 ? 1 : 2) + (L2 > 11 ? sizeof(double) * (1 << L2) : 0);              \
     T = (1 << L2) / 8;                                                                      \
     break;
     LSW(9) LSW(10) LSW(11) LSW(12)

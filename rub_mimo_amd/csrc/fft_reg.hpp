@@ -264,6 +264,28 @@ MIMO_DEV void reg_rest_lay(v2f *buf, v2f *v, const v2f *w1, int tid) {
   }
 }
 
+// reg_rest_lay through two images used in turn (exchange i stores into and loads from
+// img[i % 2]): one barrier per exchange instead of two -- the barrier after exchange i's store
+// also orders every wave's loads of exchange i - 1 (from the other image) before exchange
+// i + 1 stores there. Barriers order LDS only (lds_barrier). A caller chaining transforms
+// starts the next one on the image the last exchange did not use (NP - 1 exchanges: swap the
+// pair when that is odd).
+template <int LOG2N, int PTS, int P, bool INV>
+MIMO_DEV void reg_rest_pp(v2f *img0, v2f *img1, v2f *v, const v2f *w1, int tid) {
+  using PL = RegPlan<LOG2N, PTS>;
+  if constexpr (P < PL::NP) {
+    int t = tid;
+    asm volatile("" : "+v"(t));
+    constexpr int LAY = reg_ex_layout<LOG2N, PTS>(P - 1);
+    v2f *buf = ((P - 1) & 1) ? img1 : img0;
+    reg_store_lay<LOG2N, PTS, P - 1, LAY>(buf, v, t);
+    lds_barrier();
+    reg_load_lay<LOG2N, PTS, P, LAY>(buf, v, t);
+    reg_compute<LOG2N, PTS, P, INV>(v, w1);
+    reg_rest_pp<LOG2N, PTS, P + 1, INV>(img0, img1, v, w1, tid);
+  }
+}
+
 // LDS writes of this wave visible to its own reads; no code motion across
 MIMO_DEV void wave_lds_sync() {
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
