@@ -247,6 +247,36 @@ MIMO_DEV double cfo_search_setup(CfoSearchLds &c, const double *part, uint32_t f
   return c.nu;
 }
 
+// the wave's largest 64-bit key in every lane, over DPP and permlane swaps (quad xor 1 and 2,
+// the row's half-mirror and mirror, then the 16- and 32-lane swaps) instead of six rounds of
+// ds_bpermute through the LDS unit (__shfl_xor): the same maximum, a few cycles per step
+template <int CTRL>
+MIMO_DEV unsigned long long dpp_u64(unsigned long long x) {
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)x, CTRL, 0xf, 0xf, false);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)(x >> 32), CTRL, 0xf, 0xf, false);
+  return ((unsigned long long)hi << 32) | lo;
+}
+MIMO_DEV unsigned long long max_u64(unsigned long long a, unsigned long long b) { return a > b ? a : b; }
+MIMO_DEV unsigned long long wave_max_u64(unsigned long long x) {
+  x = max_u64(x, dpp_u64<0xB1>(x));    // quad_perm [1, 0, 3, 2]: lane ^ 1
+  x = max_u64(x, dpp_u64<0x4E>(x));    // quad_perm [2, 3, 0, 1]: lane ^ 2
+  x = max_u64(x, dpp_u64<0x141>(x));   // row_half_mirror: the other quad of the 8
+  x = max_u64(x, dpp_u64<0x140>(x));   // row_mirror: the other 8 of the row
+  {
+    const uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+    const auto l = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+    const auto h = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+    x = max_u64(((unsigned long long)h[0] << 32) | l[0], ((unsigned long long)h[1] << 32) | l[1]);
+  }
+  {
+    const uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+    const auto l = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
+    const auto h = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+    x = max_u64(((unsigned long long)h[0] << 32) | l[0], ((unsigned long long)h[1] << 32) | l[1]);
+  }
+  return x;
+}
+
 MIMO_DEV uint32_t key_index(unsigned long long k) {
   return k ? (0xFFFFFFFFu - (uint32_t)(k & 0xFFFFFFFFull)) : 0u;
 }
@@ -701,11 +731,7 @@ void search_ls_wave_kernel(SearchArgs a) {
                                      (unsigned long long)(0xFFFFFFFFu - (ws + i));
       best = (hi != 0u && key > best) ? key : best;
     }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-      const unsigned long long q = __shfl_xor(best, o);
-      best = q > best ? q : best;
-    }
+    best = wave_max_u64(best);
     if (lane == 0 && best) atomicMax(&s_key[u], best);
     __syncthreads();                                  // key final; every reader of buf is done
     if (tid == 0) a.keys[((uint64_t)f * a.N + r) * a.n_slots + slot] = s_key[u];
